@@ -1,0 +1,151 @@
+/*
+ * include/psn_lk.h -- C ABI of the MI355X-native Tracker2D optical-flow path.
+ *
+ * Replaces, for CPSNWhere_Tracker2D (psn_where/PSNWhere_Tracker2D.{h,cpp}),
+ * the two OpenCV 2.4.6 calls
+ *   cv::calcOpticalFlowPyrLK(curr, prev, ...)  backward, PSNWhere_Tracker2D.cpp:776-782
+ *   cv::calcOpticalFlowPyrLK(prev, curr, ...)  forward,  PSNWhere_Tracker2D.cpp:871-877
+ * and the per-frame gray ring buffer they read
+ *   cvtColor(BGR2GRAY) + resize(scale 1.0) into m_vecPtGrayFrameBuffer,
+ *   PSNWhere_Tracker2D.cpp:256-263 (ingest), :310-316 (rotation), .h:187.
+ *
+ * Plain C: pointers and sizes only, no C++/torch types. Every entry point
+ * returns 0 (PSN_LK_OK) or a negative PSN_LK_ERR_*; no exception or abort
+ * crosses the boundary (the reference's failure modes were assert() at
+ * PSNWhere_Tracker2D.cpp:253 and OpenCV's CV_Assert(winSize > 2)).
+ *
+ * Threading: a context is single-threaded and owns one HIP stream; distinct
+ * contexts (one per camera) may be driven concurrently, on one or several
+ * devices. Device memory is owned by the context; host arrays are only
+ * accessed during the call (host-array entry points are synchronous).
+ */
+#ifndef PSN_LK_H
+#define PSN_LK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSN_LK_ABI_VERSION 1
+
+#define PSN_LK_OK 0
+#define PSN_LK_ERR_ARG (-1)
+#define PSN_LK_ERR_WINSIZE (-2)     /* CV_Assert(winSize.width > 2 && winSize.height > 2) */
+#define PSN_LK_ERR_HIP (-3)         /* HIP runtime failure; see psn_lk_last_error */
+#define PSN_LK_ERR_NOMEM (-4)
+#define PSN_LK_ERR_SLOT (-5)        /* ring slot out of range or never filled */
+#define PSN_LK_ERR_LEVEL_CAP (-6)   /* query needs more pyramid levels than the ring holds */
+#define PSN_LK_ERR_COMM (-7)        /* RCCL failure */
+#define PSN_LK_ERR_UNSUPPORTED (-8) /* window larger than the LDS-resident limit */
+
+/* flags: OpenCV 2.4.6 values (video/tracking.hpp) + one accumulation-order bit */
+#define PSN_LK_USE_INITIAL_FLOW 4      /* cv::OPTFLOW_USE_INITIAL_FLOW */
+#define PSN_LK_GET_MIN_EIGENVALS 8     /* cv::OPTFLOW_LK_GET_MIN_EIGENVALS */
+#define PSN_LK_ACCUM_SCALAR 0x100      /* float sums in the scalar build's order (default: SSE2 build) */
+
+/* cv::TermCriteria type bits */
+#define PSN_LK_TERM_COUNT 1
+#define PSN_LK_TERM_EPS 2
+
+#define PSN_LK_MAX_LEVELS 8
+#define PSN_LK_MAX_WIN_PIXELS 16384    /* w*h kept LDS-resident per point */
+
+/* Arguments of cv::calcOpticalFlowPyrLK after prevImg/nextImg/points. The
+ * reference passes only winSize and leaves the rest at their defaults
+ * (PSNWhere_Tracker2D.cpp:782, :877); psn_lk_default_params() fills them. */
+typedef struct psn_lk_params {
+    int win_w, win_h;           /* winSize (default 21x21) */
+    int max_level;              /* maxLevel (default 3), truncated per buildOpticalFlowPyramid */
+    int term_type;              /* COUNT|EPS */
+    int max_count;              /* default 30, clamped to [0,100] */
+    double epsilon;             /* default 0.01, clamped to [0,10], squared */
+    int flags;                  /* PSN_LK_* flags above (default 0) */
+    double min_eig_threshold;   /* default 1e-4 */
+} psn_lk_params;
+
+/* One calcOpticalFlowPyrLK call on two ring slots over a contiguous range of
+ * the point arrays: points [first_pt, first_pt + num_pts). Several queries
+ * (e.g. one per detection box, each with its own window) run in ONE launch. */
+typedef struct psn_lk_query {
+    int prev_slot;              /* prevImg: pyramid of this ring slot */
+    int next_slot;              /* nextImg */
+    int first_pt;
+    int num_pts;
+    psn_lk_params params;
+} psn_lk_query;
+
+typedef struct psn_lk_ctx psn_lk_ctx;
+
+/* cv::calcOpticalFlowPyrLK defaults. */
+void psn_lk_default_params(psn_lk_params *p);
+
+/* Effective maxLevel of buildOpticalFlowPyramid for an image/window (the
+ * level-count truncation rule). Returns < 0 on bad arguments. */
+int psn_lk_effective_max_level(int width, int height, int win_w, int win_h, int max_level);
+
+/* Per-camera context (replaces CPSNWhere_Tracker2D::Initialize's ring setup,
+ * PSNWhere_Tracker2D.cpp:129-139): a device ring of `ring_slots` pyramids of
+ * max_level_cap+1 levels for width x height gray frames. */
+int psn_lk_create(int device, int width, int height, int ring_slots, int max_level_cap, psn_lk_ctx **out);
+void psn_lk_destroy(psn_lk_ctx *ctx);
+const char *psn_lk_last_error(psn_lk_ctx *ctx);
+
+/* Use an external HIP stream (hipStream_t as void*); NULL restores the
+ * context's own stream. */
+int psn_lk_set_stream(psn_lk_ctx *ctx, void *hip_stream);
+void *psn_lk_get_stream(psn_lk_ctx *ctx);
+int psn_lk_sync(psn_lk_ctx *ctx);
+
+/* Ingest one frame into ring slot `slot` and build its pyramid on device
+ * (replaces cvtColor(BGR2GRAY) + resize + the per-call pyramid rebuilds,
+ * PSNWhere_Tracker2D.cpp:257-262). channels: 1 (gray) or 3 (BGR).
+ * _device: `dev` is a device pointer; the call is asynchronous on the
+ * context stream. Host variant copies and returns after enqueueing. */
+int psn_lk_push_frame(psn_lk_ctx *ctx, int slot, const uint8_t *host, int stride, int channels);
+int psn_lk_push_frame_device(psn_lk_ctx *ctx, int slot, const uint8_t *dev, int stride, int channels);
+
+/* Batched LK (replaces cv::calcOpticalFlowPyrLK at PSNWhere_Tracker2D.cpp:776-782
+ * and :871-877). next_xy is written for EVERY point, including status==0 ones,
+ * as OpenCV does (the backward path feeds all of them to LocalSearchKLT,
+ * :787). err may be NULL. With PSN_LK_USE_INITIAL_FLOW, next_xy is read first.
+ * Host variant: synchronous. _device variant: device pointers, async. */
+int psn_lk_track(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const float *prev_xy, float *next_xy,
+                 uint8_t *status, float *err);
+int psn_lk_track_device(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const float *d_prev_xy,
+                        float *d_next_xy, uint8_t *d_status, float *d_err);
+
+/* One-shot cv::calcOpticalFlowPyrLK(prevImg, nextImg, prevPts, nextPts, status,
+ * err, winSize, maxLevel, criteria, flags, minEigThreshold) on two host gray
+ * images of the context's size, using two scratch slots of the context. */
+int psn_calc_optical_flow_pyr_lk(psn_lk_ctx *ctx, const uint8_t *prev_img, const uint8_t *next_img,
+                                 int stride, const float *prev_pts, float *next_pts, uint8_t *status,
+                                 float *err, int npts, const psn_lk_params *params);
+
+/* Copy pyramid level `level` of `slot` back to host (parity / debugging). */
+int psn_lk_read_level(psn_lk_ctx *ctx, int slot, int level, uint8_t *host, int stride);
+int psn_lk_level_size(psn_lk_ctx *ctx, int level, int *w, int *h);
+
+/* Device-side timing of the last psn_lk_push_frame / psn_lk_track calls
+ * (HIP events on the context stream) when enabled. Milliseconds. */
+int psn_lk_enable_timing(psn_lk_ctx *ctx, int on);
+int psn_lk_last_timing(psn_lk_ctx *ctx, float *push_ms, float *track_ms);
+
+/* ---- multi-GPU: per-camera tracklet slots all-gathered over RCCL/xGMI ----
+ * Replaces the in-process std::vector<stTrack2DResult> hand-off into
+ * CPSNWhere_Associator3D::Run (psn_where/PSNWhere.cpp:253, 264, 269). */
+typedef struct psn_comm psn_comm;
+#define PSN_COMM_UNIQUE_ID_BYTES 128
+int psn_comm_get_unique_id(void *id_out /* PSN_COMM_UNIQUE_ID_BYTES */);
+int psn_comm_init(int nranks, int rank, int device, const void *unique_id, psn_comm **out);
+int psn_comm_allgather(psn_comm *comm, const void *d_send, void *d_recv, size_t bytes_per_rank, void *hip_stream);
+void psn_comm_destroy(psn_comm *comm);
+
+int psn_lk_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSN_LK_H */

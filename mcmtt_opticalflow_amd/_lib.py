@@ -1,0 +1,118 @@
+"""ctypes binding of libpsn_lk.so (the C ABI declared in include/psn_lk.h).
+
+The library is built in-tree (mcmtt_opticalflow_amd/lib/libpsn_lk.so) by
+__graft_entry__.build(). There is NO fallback: if the HIP library is missing
+every entry point raises, so a test can never pass on a CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpsn_lk.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psn_lk.h")
+
+PSN_LK_OK = 0
+ERRORS = {
+    -1: "PSN_LK_ERR_ARG",
+    -2: "PSN_LK_ERR_WINSIZE",
+    -3: "PSN_LK_ERR_HIP",
+    -4: "PSN_LK_ERR_NOMEM",
+    -5: "PSN_LK_ERR_SLOT",
+    -6: "PSN_LK_ERR_LEVEL_CAP",
+    -7: "PSN_LK_ERR_COMM",
+    -8: "PSN_LK_ERR_UNSUPPORTED",
+}
+USE_INITIAL_FLOW = 4
+GET_MIN_EIGENVALS = 8
+ACCUM_SCALAR = 0x100
+TERM_COUNT = 1
+TERM_EPS = 2
+MAX_WIN_PIXELS = 16384
+COMM_UNIQUE_ID_BYTES = 128
+
+
+class PsnLkError(RuntimeError):
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+
+
+class LkParams(ctypes.Structure):
+    _fields_ = [
+        ("win_w", ctypes.c_int),
+        ("win_h", ctypes.c_int),
+        ("max_level", ctypes.c_int),
+        ("term_type", ctypes.c_int),
+        ("max_count", ctypes.c_int),
+        ("epsilon", ctypes.c_double),
+        ("flags", ctypes.c_int),
+        ("min_eig_threshold", ctypes.c_double),
+    ]
+
+
+class LkQuery(ctypes.Structure):
+    _fields_ = [
+        ("prev_slot", ctypes.c_int),
+        ("next_slot", ctypes.c_int),
+        ("first_pt", ctypes.c_int),
+        ("num_pts", ctypes.c_int),
+        ("params", LkParams),
+    ]
+
+
+def header_functions() -> list[str]:
+    """Names of every function declared in include/psn_lk.h."""
+    src = open(HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(psn_\w+)\s*\(", src)))
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ip, u8p, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p
+    L.psn_lk_abi_version.restype = ip
+    L.psn_lk_default_params.argtypes = [ctypes.POINTER(LkParams)]
+    L.psn_lk_default_params.restype = None
+    L.psn_lk_effective_max_level.argtypes = [ip] * 5
+    L.psn_lk_create.argtypes = [ip, ip, ip, ip, ip, ctypes.POINTER(vp)]
+    L.psn_lk_destroy.argtypes = [vp]
+    L.psn_lk_destroy.restype = None
+    L.psn_lk_last_error.argtypes = [vp]
+    L.psn_lk_last_error.restype = ctypes.c_char_p
+    L.psn_lk_set_stream.argtypes = [vp, vp]
+    L.psn_lk_get_stream.argtypes = [vp]
+    L.psn_lk_get_stream.restype = vp
+    L.psn_lk_sync.argtypes = [vp]
+    L.psn_lk_push_frame.argtypes = [vp, ip, u8p, ip, ip]
+    L.psn_lk_push_frame_device.argtypes = [vp, ip, vp, ip, ip]
+    L.psn_lk_track.argtypes = [vp, ctypes.POINTER(LkQuery), ip, fp, fp, u8p, fp]
+    L.psn_lk_track_device.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp]
+    L.psn_calc_optical_flow_pyr_lk.argtypes = [vp, u8p, u8p, ip, fp, fp, u8p, fp, ip, ctypes.POINTER(LkParams)]
+    L.psn_lk_read_level.argtypes = [vp, ip, ip, u8p, ip]
+    L.psn_lk_level_size.argtypes = [vp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]
+    L.psn_lk_enable_timing.argtypes = [vp, ip]
+    L.psn_lk_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    L.psn_comm_get_unique_id.argtypes = [vp]
+    L.psn_comm_init.argtypes = [ip, ip, ip, vp, ctypes.POINTER(vp)]
+    L.psn_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
+    L.psn_comm_destroy.argtypes = [vp]
+    L.psn_comm_destroy.restype = None
+    _lib = L
+    return L
+
+
+def default_params() -> LkParams:
+    p = LkParams()
+    load().psn_lk_default_params(ctypes.byref(p))
+    return p

@@ -1,0 +1,425 @@
+// C-ABI implementation of include/psn_lk.h (host side of libpsn_lk.so).
+//
+// One psn_lk_ctx per camera replaces what CPSNWhere_Tracker2D kept for
+// OpenCV: the 4-slot gray ring (m_vecPtGrayFrameBuffer, PSNWhere_Tracker2D.h:187,
+// allocated at PSNWhere_Tracker2D.cpp:258-261) -- here a device ring of full
+// pyramids, built ONCE per frame -- and the two calcOpticalFlowPyrLK call sites
+// (:776-782, :871-877), which rebuilt both pyramids and the Scharr planes on
+// every call.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "psn_lk.h"
+#include "psn_lk_kernels.h"
+
+using psn::LevelDev;
+
+struct psn_lk_ctx {
+    int device = 0;
+    int width = 0, height = 0;
+    int user_slots = 0, nslots = 0;  // user ring + 2 scratch slots (one-shot API)
+    int nlevels = 0;                 // max_level_cap + 1
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    uint8_t *d_pyr = nullptr;
+    LevelDev *d_slots = nullptr;
+    std::vector<LevelDev> h_slots;  // [nslots][kMaxLevels]
+    std::vector<char> filled;
+    // staging
+    uint8_t *d_src = nullptr;
+    size_t d_src_cap = 0;
+    float *d_prev = nullptr, *d_next = nullptr, *d_err = nullptr;
+    uint8_t *d_status = nullptr;
+    size_t d_pts_cap = 0;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool push_timed = false, track_timed = false;
+    std::string err;
+};
+
+static int set_err(psn_lk_ctx *c, int code, const char *fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                       \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return set_err((c), PSN_LK_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                               \
+    } while (0)
+
+extern "C" {
+
+int psn_lk_abi_version(void) { return PSN_LK_ABI_VERSION; }
+
+void psn_lk_default_params(psn_lk_params *p) {
+    if (!p) return;
+    p->win_w = 21;
+    p->win_h = 21;
+    p->max_level = 3;
+    p->term_type = PSN_LK_TERM_COUNT | PSN_LK_TERM_EPS;
+    p->max_count = 30;
+    p->epsilon = 0.01;
+    p->flags = 0;
+    p->min_eig_threshold = 1e-4;
+}
+
+int psn_lk_effective_max_level(int width, int height, int win_w, int win_h, int max_level) {
+    if (width <= 0 || height <= 0 || max_level < 0) return PSN_LK_ERR_ARG;
+    int sw = width, sh = height;
+    for (int level = 0; level <= max_level; level++) {
+        sw = (sw + 1) / 2;
+        sh = (sh + 1) / 2;
+        if (sw <= win_w || sh <= win_h) return level;
+    }
+    return max_level;
+}
+
+int psn_lk_create(int device, int width, int height, int ring_slots, int max_level_cap, psn_lk_ctx **out) {
+    if (!out || width <= 0 || height <= 0 || ring_slots <= 0 || max_level_cap < 0 ||
+        max_level_cap > psn::kPyrMaxTop)
+        return PSN_LK_ERR_ARG;
+    *out = nullptr;
+    psn_lk_ctx *c = new (std::nothrow) psn_lk_ctx();
+    if (!c) return PSN_LK_ERR_NOMEM;
+    c->device = device;
+    c->width = width;
+    c->height = height;
+    c->user_slots = ring_slots;
+    c->nslots = ring_slots + 2;
+    c->nlevels = max_level_cap + 1;
+    auto fail = [&](int rc) {
+        psn_lk_destroy(c);
+        return rc;
+    };
+    if (hipSetDevice(device) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    if (psn::lk_kernels_init() != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    c->stream = c->own_stream;
+    // slot layout: levels back to back, rows padded to 256 B (one HBM burst / 4 x 64-B lines)
+    size_t slot_bytes = 0;
+    std::vector<size_t> lv_off(c->nlevels);
+    std::vector<int> lw(c->nlevels), lh(c->nlevels), lp(c->nlevels);
+    {
+        int w = width, h = height;
+        for (int l = 0; l < c->nlevels; l++) {
+            lw[l] = w;
+            lh[l] = h;
+            lp[l] = (w + 255) & ~255;
+            lv_off[l] = slot_bytes;
+            slot_bytes += (size_t)lp[l] * h;
+            w = (w + 1) / 2;
+            h = (h + 1) / 2;
+        }
+    }
+    slot_bytes = (slot_bytes + 4095) & ~(size_t)4095;
+    if (hipMalloc(&c->d_pyr, slot_bytes * c->nslots) != hipSuccess) return fail(PSN_LK_ERR_NOMEM);
+    if (hipMemset(c->d_pyr, 0, slot_bytes * c->nslots) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    c->h_slots.assign((size_t)c->nslots * psn::kMaxLevels, LevelDev{nullptr, 0, 0, 0, 0});
+    for (int s = 0; s < c->nslots; s++)
+        for (int l = 0; l < c->nlevels; l++)
+            c->h_slots[(size_t)s * psn::kMaxLevels + l] = LevelDev{c->d_pyr + slot_bytes * s + lv_off[l], lw[l], lh[l], lp[l], 0};
+    if (hipMalloc(&c->d_slots, sizeof(LevelDev) * c->h_slots.size()) != hipSuccess) return fail(PSN_LK_ERR_NOMEM);
+    if (hipMemcpy(c->d_slots, c->h_slots.data(), sizeof(LevelDev) * c->h_slots.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(PSN_LK_ERR_HIP);
+    c->filled.assign(c->nslots, 0);
+    for (auto &e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    *out = c;
+    return PSN_LK_OK;
+}
+
+void psn_lk_destroy(psn_lk_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (void *p : {(void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
+                    (void *)c->d_err, (void *)c->d_status})
+        if (p) (void)hipFree(p);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char *psn_lk_last_error(psn_lk_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int psn_lk_set_stream(psn_lk_ctx *c, void *s) {
+    if (!c) return PSN_LK_ERR_ARG;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return PSN_LK_OK;
+}
+
+void *psn_lk_get_stream(psn_lk_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int psn_lk_sync(psn_lk_ctx *c) {
+    if (!c) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PSN_LK_OK;
+}
+
+int psn_lk_enable_timing(psn_lk_ctx *c, int on) {
+    if (!c) return PSN_LK_ERR_ARG;
+    c->timing = on != 0;
+    c->push_timed = c->track_timed = false;
+    return PSN_LK_OK;
+}
+
+int psn_lk_last_timing(psn_lk_ctx *c, float *push_ms, float *track_ms) {
+    if (!c) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (push_ms) {
+        *push_ms = -1.f;
+        if (c->push_timed) HIPCHK(c, hipEventElapsedTime(push_ms, c->ev[0], c->ev[1]));
+    }
+    if (track_ms) {
+        *track_ms = -1.f;
+        if (c->track_timed) HIPCHK(c, hipEventElapsedTime(track_ms, c->ev[2], c->ev[3]));
+    }
+    return PSN_LK_OK;
+}
+
+int psn_lk_level_size(psn_lk_ctx *c, int level, int *w, int *h) {
+    if (!c || level < 0 || level >= c->nlevels) return PSN_LK_ERR_ARG;
+    if (w) *w = c->h_slots[level].w;
+    if (h) *h = c->h_slots[level].h;
+    return PSN_LK_OK;
+}
+
+static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
+    psn::PyrBuildArgs a{};
+    a.src = dev;
+    a.src_stride = stride;
+    a.channels = channels;
+    a.nlevels = c->nlevels;
+    a.tile = (c->nlevels - 1) <= 4 ? 8 : 4;
+    for (int l = 0; l < c->nlevels; l++) a.lv[l] = c->h_slots[(size_t)slot * psn::kMaxLevels + l];
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(c, psn::launch_pyramid(a, c->stream));
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
+        c->push_timed = true;
+    }
+    c->filled[slot] = 1;
+    return PSN_LK_OK;
+}
+
+int psn_lk_push_frame_device(psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
+    if (!c || !dev || (channels != 1 && channels != 3) || stride < c->width * channels) return PSN_LK_ERR_ARG;
+    if (slot < 0 || slot >= c->user_slots) return set_err(c, PSN_LK_ERR_SLOT, "slot %d out of range", slot);
+    HIPCHK(c, hipSetDevice(c->device));
+    return push_device_impl(c, slot, dev, stride, channels);
+}
+
+static int push_host_impl(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, int channels) {
+    const size_t row = (size_t)c->width * channels, need = row * c->height;
+    if (c->d_src_cap < need) {
+        if (c->d_src) (void)hipFree(c->d_src);
+        c->d_src = nullptr;
+        c->d_src_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_src, need));
+        c->d_src_cap = need;
+    }
+    HIPCHK(c, hipMemcpy2DAsync(c->d_src, row, host, stride, row, c->height, hipMemcpyHostToDevice, c->stream));
+    int rc = push_device_impl(c, slot, c->d_src, (int)row, channels);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the host frame belongs to the caller after return
+    return PSN_LK_OK;
+}
+
+int psn_lk_push_frame(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, int channels) {
+    if (!c || !host || (channels != 1 && channels != 3) || stride < c->width * channels) return PSN_LK_ERR_ARG;
+    if (slot < 0 || slot >= c->user_slots) return set_err(c, PSN_LK_ERR_SLOT, "slot %d out of range", slot);
+    HIPCHK(c, hipSetDevice(c->device));
+    return push_host_impl(c, slot, host, stride, channels);
+}
+
+// Validate and plan one query into its device descriptor.
+static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::LkQueryDev &d, int &lds, bool allow_scratch) {
+    const psn_lk_params &p = q.params;
+    const int limit = allow_scratch ? c->nslots : c->user_slots;
+    if (q.prev_slot < 0 || q.prev_slot >= limit || q.next_slot < 0 || q.next_slot >= limit)
+        return set_err(c, PSN_LK_ERR_SLOT, "slot out of range (%d, %d)", q.prev_slot, q.next_slot);
+    if (!c->filled[q.prev_slot] || !c->filled[q.next_slot])
+        return set_err(c, PSN_LK_ERR_SLOT, "slot never filled (%d, %d)", q.prev_slot, q.next_slot);
+    if (p.win_w <= 2 || p.win_h <= 2) return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", p.win_w, p.win_h);
+    if (p.max_level < 0 || q.num_pts < 0 || q.first_pt < 0) return set_err(c, PSN_LK_ERR_ARG, "bad query");
+    if ((long)p.win_w * p.win_h > PSN_LK_MAX_WIN_PIXELS)
+        return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d exceeds %d px", p.win_w, p.win_h, PSN_LK_MAX_WIN_PIXELS);
+    const int ml = psn_lk_effective_max_level(c->width, c->height, p.win_w, p.win_h, p.max_level);
+    if (ml >= c->nlevels)
+        return set_err(c, PSN_LK_ERR_LEVEL_CAP, "query needs %d levels, ring holds %d", ml + 1, c->nlevels);
+    int max_count = (p.term_type & PSN_LK_TERM_COUNT) ? std::min(std::max(p.max_count, 0), 100) : 30;
+    double eps = (p.term_type & PSN_LK_TERM_EPS) ? std::min(std::max(p.epsilon, 0.), 10.) : 0.01;
+    const int w = p.win_w, h = p.win_h;
+    int tr = h;
+    const int budget = 160 * 1024 - 1024;
+    if (psn::lk_lds_bytes(w, h, tr) > 64 * 1024) {
+        while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
+        if (psn::lk_lds_bytes(w, h, tr) > budget)
+            return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d does not fit LDS", w, h);
+    }
+    d.prev_slot = q.prev_slot;
+    d.next_slot = q.next_slot;
+    d.wg_begin = wg_begin;
+    d.pt_begin = q.first_pt;
+    d.num_pts = q.num_pts;
+    d.win_w = w;
+    d.win_h = h;
+    d.max_level = ml;
+    d.max_count = max_count;
+    d.flags = p.flags;
+    d.tile_rows = tr;
+    d.min_eig = (float)p.min_eig_threshold;
+    d.eps2 = eps * eps;
+    lds = psn::lk_lds_bytes(w, h, tr);
+    return PSN_LK_OK;
+}
+
+static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
+                             uint8_t *d_status, float *d_err, bool allow_scratch) {
+    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    for (int base = 0; base < nq; base += psn::kMaxQueries) {
+        const int n = std::min(psn::kMaxQueries, nq - base);
+        psn::LkLaunchArgs a{};
+        a.slots = c->d_slots;
+        a.prev = d_prev;
+        a.next = d_next;
+        a.status = d_status;
+        a.err = d_err;
+        int wgs = 0, lds = 0, maxpx = 0, nqd = 0;
+        for (int i = 0; i < n; i++) {
+            const psn_lk_query &qq = q[base + i];
+            if (qq.num_pts == 0) {
+                if (qq.params.win_w <= 2 || qq.params.win_h <= 2)
+                    return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", qq.params.win_w, qq.params.win_h);
+                continue;
+            }
+            int l = 0;
+            int rc = plan_query(c, qq, wgs, a.q[nqd], l, allow_scratch);
+            if (rc) return rc;
+            wgs += qq.num_pts;
+            lds = std::max(lds, l);
+            maxpx = std::max(maxpx, qq.params.win_w * qq.params.win_h);
+            nqd++;
+        }
+        a.nq = nqd;
+        if (nqd == 0) continue;
+        const int threads = maxpx <= 1024 ? 64 : maxpx <= 4096 ? 128 : 256;
+        HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, c->stream));
+    }
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
+        c->track_timed = true;
+    }
+    return PSN_LK_OK;
+}
+
+int psn_lk_track_device(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
+                        uint8_t *d_status, float *d_err) {
+    if (!c || (nq > 0 && (!q || !d_prev || !d_next || !d_status)) || nq < 0) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    return track_device_impl(c, q, nq, d_prev, d_next, d_status, d_err, false);
+}
+
+static int ensure_pts(psn_lk_ctx *c, size_t n) {
+    if (c->d_pts_cap >= n) return PSN_LK_OK;
+    for (void *p : {(void *)c->d_prev, (void *)c->d_next, (void *)c->d_err, (void *)c->d_status})
+        if (p) (void)hipFree(p);
+    c->d_prev = c->d_next = c->d_err = nullptr;
+    c->d_status = nullptr;
+    c->d_pts_cap = 0;
+    size_t cap = std::max<size_t>(n, 1024);
+    HIPCHK(c, hipMalloc(&c->d_prev, cap * 2 * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->d_next, cap * 2 * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->d_err, cap * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->d_status, cap));
+    c->d_pts_cap = cap;
+    return PSN_LK_OK;
+}
+
+static int track_host_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *prev_xy, float *next_xy,
+                           uint8_t *status, float *err, bool allow_scratch) {
+    size_t npts = 0;
+    bool init_flow = false;
+    for (int i = 0; i < nq; i++) {
+        if (q[i].num_pts < 0 || q[i].first_pt < 0) return PSN_LK_ERR_ARG;
+        npts = std::max(npts, (size_t)q[i].first_pt + q[i].num_pts);
+        init_flow |= (q[i].params.flags & PSN_LK_USE_INITIAL_FLOW) != 0;
+    }
+    if (npts == 0) return track_device_impl(c, q, nq, nullptr, nullptr, nullptr, nullptr, allow_scratch);
+    int rc = ensure_pts(c, npts);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->d_prev, prev_xy, npts * 2 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if (init_flow) HIPCHK(c, hipMemcpyAsync(c->d_next, next_xy, npts * 2 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    rc = track_device_impl(c, q, nq, c->d_prev, c->d_next, c->d_status, err ? c->d_err : nullptr, allow_scratch);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(next_xy, c->d_next, npts * 2 * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(status, c->d_status, npts, hipMemcpyDeviceToHost, c->stream));
+    if (err) HIPCHK(c, hipMemcpyAsync(err, c->d_err, npts * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PSN_LK_OK;
+}
+
+int psn_lk_track(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *prev_xy, float *next_xy, uint8_t *status,
+                 float *err) {
+    if (!c || nq < 0 || (nq > 0 && !q)) return PSN_LK_ERR_ARG;
+    for (int i = 0; i < nq; i++)
+        if (q[i].num_pts > 0 && (!prev_xy || !next_xy || !status)) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    return track_host_impl(c, q, nq, prev_xy, next_xy, status, err, false);
+}
+
+int psn_calc_optical_flow_pyr_lk(psn_lk_ctx *c, const uint8_t *prev_img, const uint8_t *next_img, int stride,
+                                 const float *prev_pts, float *next_pts, uint8_t *status, float *err, int npts,
+                                 const psn_lk_params *params) {
+    if (!c || !prev_img || !next_img || npts < 0 || stride < c->width) return PSN_LK_ERR_ARG;
+    psn_lk_params p;
+    if (params)
+        p = *params;
+    else
+        psn_lk_default_params(&p);
+    if (p.win_w <= 2 || p.win_h <= 2) return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", p.win_w, p.win_h);
+    if (npts == 0) return PSN_LK_OK;  // calcOpticalFlowPyrLK releases outputs and returns
+    if (!prev_pts || !next_pts || !status) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int sa = c->user_slots, sb = c->user_slots + 1;
+    int rc = push_host_impl(c, sa, prev_img, stride, 1);
+    if (rc) return rc;
+    rc = push_host_impl(c, sb, next_img, stride, 1);
+    if (rc) return rc;
+    psn_lk_query q;
+    q.prev_slot = sa;
+    q.next_slot = sb;
+    q.first_pt = 0;
+    q.num_pts = npts;
+    q.params = p;
+    return track_host_impl(c, &q, 1, prev_pts, next_pts, status, err, true);
+}
+
+int psn_lk_read_level(psn_lk_ctx *c, int slot, int level, uint8_t *host, int stride) {
+    if (!c || !host || slot < 0 || slot >= c->nslots || level < 0 || level >= c->nlevels) return PSN_LK_ERR_ARG;
+    const LevelDev &L = c->h_slots[(size_t)slot * psn::kMaxLevels + level];
+    if (stride < L.w) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy2DAsync(host, stride, L.p, L.pitch, L.w, L.h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PSN_LK_OK;
+}
+
+}  // extern "C"

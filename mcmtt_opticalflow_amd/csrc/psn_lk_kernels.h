@@ -1,0 +1,79 @@
+// Internal (non-ABI) declarations shared by the HIP kernels and the C-ABI host
+// code of libpsn_lk.so. Not installed; the public surface is include/psn_lk.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "psn_lk.h"
+
+namespace psn {
+
+constexpr int kMaxLevels = PSN_LK_MAX_LEVELS;
+constexpr int kMaxQueries = 32;     // queries per LK launch (kernel-argument table)
+constexpr int kJMargin = 3;         // J staging margin (px) around the window, each side
+constexpr int kPyrMaxTop = 5;       // fused pyramid kernel supports top level <= 5
+
+// One pyramid level in HBM: unpadded u8 plane, rows `pitch` bytes apart.
+struct LevelDev {
+    uint8_t *p;
+    int w, h, pitch;
+    int pad_;
+};
+
+struct PyrBuildArgs {
+    const uint8_t *src;   // level-0 source frame (gray or BGR)
+    int src_stride;
+    int channels;         // 1 or 3
+    int nlevels;          // levels to write (1..kPyrMaxTop+1)
+    int tile;             // top-level tile edge
+    LevelDev lv[kMaxLevels];
+};
+
+struct LkQueryDev {
+    int prev_slot, next_slot;
+    int wg_begin;         // first workgroup of this query
+    int pt_begin;         // first point index in the arrays
+    int num_pts;
+    int win_w, win_h;
+    int max_level;        // effective (truncated) maxLevel
+    int max_count;
+    int flags;
+    int tile_rows;        // window rows per LDS tile
+    float min_eig;
+    double eps2;
+};
+
+struct LkLaunchArgs {
+    const LevelDev *slots;   // [nslots][kMaxLevels]
+    const float *prev;       // (x,y) pairs
+    float *next;
+    uint8_t *status;
+    float *err;              // may be null
+    int nq;
+    int pad_;
+    LkQueryDev q[kMaxQueries];
+};
+
+// LDS bytes a query needs for a given tile height (shared by host planner and kernel).
+__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+__host__ __device__ inline int lk_jreg_w(int w) { return w + 1 + 2 * kJMargin; }
+__host__ __device__ inline int lk_jreg_h(int h) { return h + 1 + 2 * kJMargin; }
+__host__ __device__ inline int lk_off_dw(int w, int h) { return align16(2 * w * h); }
+__host__ __device__ inline int lk_off_jr(int w, int h) { return lk_off_dw(w, h) + align16(4 * w * h); }
+__host__ __device__ inline int lk_off_red(int w, int h) { return lk_off_jr(w, h) + align16(lk_jreg_w(w) * lk_jreg_h(h)); }
+constexpr int kRedBytes = 256;
+__host__ __device__ inline int lk_off_tile(int w, int h) { return lk_off_red(w, h) + kRedBytes; }
+__host__ __device__ inline int lk_tile_pimg_bytes(int w, int tr) { return align16((tr + 3) * (w + 3)); }
+__host__ __device__ inline int lk_tile_dg_bytes(int w, int tr) { return align16(4 * (tr + 1) * (w + 1)); }
+__host__ __device__ inline int lk_tile_prod_bytes(int w, int tr) { return 12 * tr * w; }
+__host__ __device__ inline int lk_lds_bytes(int w, int h, int tr) {
+    return lk_off_tile(w, h) + lk_tile_pimg_bytes(w, tr) + lk_tile_dg_bytes(w, tr) + lk_tile_prod_bytes(w, tr);
+}
+
+// Launchers (psn_lk_kernels.hip).
+hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s);
+hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, hipStream_t s);
+hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
+
+}  // namespace psn

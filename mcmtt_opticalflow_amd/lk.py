@@ -1,0 +1,158 @@
+"""Python view of the C ABI (include/psn_lk.h) for tests and bench.
+
+`LKContext` is one camera's device ring of pyramids (the MI355X replacement of
+CPSNWhere_Tracker2D's gray ring, PSNWhere_Tracker2D.cpp:256-263, :310-316) and
+`calc_optical_flow_pyr_lk` mirrors cv::calcOpticalFlowPyrLK as called at
+PSNWhere_Tracker2D.cpp:776-782 / :871-877: same argument meaning, same outputs
+(nextPts written for every point, status, err), CV_Assert(winSize > 2)
+surfaced as PsnLkError(PSN_LK_ERR_WINSIZE).
+
+Everything here calls libpsn_lk.so; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import LkParams, LkQuery, PsnLkError
+
+
+def make_params(win_size=(21, 21), max_level=3, criteria=(3, 30, 0.01), flags=0,
+                min_eig_threshold=1e-4) -> LkParams:
+    p = LkParams()
+    p.win_w, p.win_h = int(win_size[0]), int(win_size[1])
+    p.max_level = int(max_level)
+    p.term_type, p.max_count, p.epsilon = int(criteria[0]), int(criteria[1]), float(criteria[2])
+    p.flags = int(flags)
+    p.min_eig_threshold = float(min_eig_threshold)
+    return p
+
+
+def make_query(prev_slot, next_slot, first_pt, num_pts, params: LkParams) -> LkQuery:
+    q = LkQuery()
+    q.prev_slot, q.next_slot, q.first_pt, q.num_pts = prev_slot, next_slot, first_pt, num_pts
+    q.params = params
+    return q
+
+
+def effective_max_level(width, height, win_w, win_h, max_level) -> int:
+    return _lib.load().psn_lk_effective_max_level(width, height, win_w, win_h, max_level)
+
+
+class LKContext:
+    """One camera: device ring of `ring_slots` pyramids (max_level_cap+1 levels)."""
+
+    def __init__(self, width: int, height: int, ring_slots: int = 4, max_level_cap: int = 3, device: int = 0):
+        self._L = _lib.load()
+        self.width, self.height = width, height
+        self.ring_slots, self.max_level_cap = ring_slots, max_level_cap
+        h = ctypes.c_void_p()
+        rc = self._L.psn_lk_create(device, width, height, ring_slots, max_level_cap, ctypes.byref(h))
+        if rc != 0:
+            raise PsnLkError(rc, "psn_lk_create")
+        self._h = h
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise PsnLkError(rc, f"{what}: {self._L.psn_lk_last_error(self._h).decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psn_lk_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: int | None):
+        self._check(self._L.psn_lk_set_stream(self._h, stream_ptr), "set_stream")
+
+    def sync(self):
+        self._check(self._L.psn_lk_sync(self._h), "sync")
+
+    def push_frame(self, slot: int, img: np.ndarray):
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        ch = 1 if img.ndim == 2 else img.shape[2]
+        assert img.shape[0] == self.height and img.shape[1] == self.width
+        self._check(self._L.psn_lk_push_frame(self._h, slot, img.ctypes.data, img.shape[1] * ch, ch), "push_frame")
+
+    def push_frame_device(self, slot: int, dev_ptr: int, stride: int, channels: int = 1):
+        self._check(self._L.psn_lk_push_frame_device(self._h, slot, dev_ptr, stride, channels), "push_frame_device")
+
+    def read_level(self, slot: int, level: int) -> np.ndarray:
+        w, h = ctypes.c_int(), ctypes.c_int()
+        self._check(self._L.psn_lk_level_size(self._h, level, ctypes.byref(w), ctypes.byref(h)), "level_size")
+        out = np.empty((h.value, w.value), np.uint8)
+        self._check(self._L.psn_lk_read_level(self._h, slot, level, out.ctypes.data, w.value), "read_level")
+        return out
+
+    def track(self, queries: list[LkQuery], prev_pts: np.ndarray, next_pts: np.ndarray | None = None,
+              want_err: bool = True):
+        """Batched host-array LK. Returns (next_pts, status, err)."""
+        prev = np.ascontiguousarray(prev_pts, dtype=np.float32).reshape(-1, 2)
+        n = prev.shape[0]
+        nxt = (np.zeros_like(prev) if next_pts is None
+               else np.ascontiguousarray(next_pts, dtype=np.float32).reshape(-1, 2).copy())
+        st = np.zeros(n, np.uint8)
+        er = np.zeros(n, np.float32) if want_err else None
+        arr = (LkQuery * max(len(queries), 1))(*queries)
+        self._check(self._L.psn_lk_track(self._h, arr, len(queries), prev.ctypes.data, nxt.ctypes.data,
+                                         st.ctypes.data, er.ctypes.data if er is not None else None), "track")
+        return nxt, st, er
+
+    def track_device(self, queries: list[LkQuery], d_prev: int, d_next: int, d_status: int, d_err: int | None):
+        arr = (LkQuery * max(len(queries), 1))(*queries)
+        self._check(self._L.psn_lk_track_device(self._h, arr, len(queries), d_prev, d_next, d_status, d_err),
+                    "track_device")
+
+    def enable_timing(self, on: bool = True):
+        self._check(self._L.psn_lk_enable_timing(self._h, int(on)), "enable_timing")
+
+    def last_timing(self) -> tuple[float, float]:
+        a, b = ctypes.c_float(), ctypes.c_float()
+        self._check(self._L.psn_lk_last_timing(self._h, ctypes.byref(a), ctypes.byref(b)), "last_timing")
+        return a.value, b.value
+
+    def calc_optical_flow_pyr_lk(self, prev_img, next_img, prev_pts, win_size=(21, 21), max_level=3,
+                                 criteria=(3, 30, 0.01), flags=0, min_eig_threshold=1e-4, next_pts=None,
+                                 want_err=True):
+        prev_img = np.ascontiguousarray(prev_img, dtype=np.uint8)
+        next_img = np.ascontiguousarray(next_img, dtype=np.uint8)
+        pts = np.ascontiguousarray(prev_pts, dtype=np.float32).reshape(-1, 2)
+        n = pts.shape[0]
+        nxt = (np.zeros_like(pts) if next_pts is None
+               else np.ascontiguousarray(next_pts, dtype=np.float32).reshape(-1, 2).copy())
+        st = np.zeros(n, np.uint8)
+        er = np.zeros(n, np.float32) if want_err else None
+        p = make_params(win_size, max_level, criteria, flags, min_eig_threshold)
+        self._check(self._L.psn_calc_optical_flow_pyr_lk(
+            self._h, prev_img.ctypes.data, next_img.ctypes.data, prev_img.shape[1], pts.ctypes.data,
+            nxt.ctypes.data, st.ctypes.data, er.ctypes.data if er is not None else None, n, ctypes.byref(p)),
+            "calc_optical_flow_pyr_lk")
+        return nxt, st, er
+
+
+def calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size=(21, 21), max_level=3,
+                             criteria=(3, 30, 0.01), flags=0, min_eig_threshold=1e-4, next_pts=None,
+                             want_err=True, device=0):
+    """cv::calcOpticalFlowPyrLK on MI355X (one-shot; allocates a context)."""
+    h, w = np.asarray(prev_img).shape[:2]
+    cap = max(0, effective_max_level(w, h, win_size[0], win_size[1], max_level))
+    with LKContext(w, h, ring_slots=1, max_level_cap=min(cap, 5), device=device) as ctx:
+        return ctx.calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size, max_level, criteria,
+                                            flags, min_eig_threshold, next_pts, want_err)

@@ -1,0 +1,495 @@
+/*
+ * oracle/lk_oracle.c -- TEST INFRASTRUCTURE ONLY (see lk_oracle.h).
+ *
+ * A plain-C restatement of the OpenCV 2.4.6 code that
+ * CPSNWhere_Tracker2D reaches through cv::calcOpticalFlowPyrLK
+ * (psn_where/PSNWhere_Tracker2D.cpp:776-782 and :871-877), plus the ingest
+ * step cv::cvtColor(BGR2GRAY) + cv::resize(scale 1.0) (:257, :262).
+ *
+ * PARITY UNPINNED (no reference fixtures exist; OpenCV 2.4.6 is absent).
+ *
+ * Built with -O2 -ffp-contract=off so float arithmetic is IEEE single
+ * rounding per operation with no FMA contraction, as MSVC x64 (/fp:precise,
+ * SSE2 scalar math) evaluates the same expressions.
+ */
+#include "lk_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define W_BITS 14
+#define W_BITS1 14
+#define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+
+/* cv::borderInterpolate(p, len, BORDER_REFLECT_101) [OCV246 core/src/copy.cpp]:
+ * "-1 -> 1, len -> len-2", repeated until inside. */
+int oracle_refl101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        if (p < 0)
+            p = -p; /* -p - 1 + delta, delta = 1 */
+        else
+            p = 2 * len - 2 - p; /* len - 1 - (p - len) - delta */
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+/* cv::cvRound(double) on SSE2 = cvtsd2si = round half to even. */
+static inline int cv_round(float v) { return (int)rint((double)v); }
+static inline int cv_floor(float v) { return (int)floor((double)v); }
+
+/* RGB2Gray<uchar> [OCV246 imgproc/src/color.cpp]: R2Y=4899, G2Y=9617, B2Y=1868,
+ * yuv_shift=14, half added through the R table. Called from
+ * PSNWhere_Tracker2D.cpp:257 (CV_BGR2GRAY: src[0]=B, src[1]=G, src[2]=R). */
+void oracle_bgr2gray(const uint8_t *src, int w, int h, int sstride, uint8_t *dst, int dstride) {
+    for (int y = 0; y < h; y++) {
+        const uint8_t *s = src + (long)y * sstride;
+        uint8_t *d = dst + (long)y * dstride;
+        for (int x = 0; x < w; x++)
+            d[x] = (uint8_t)((s[3 * x] * 1868 + s[3 * x + 1] * 9617 + s[3 * x + 2] * 4899 + (1 << 13)) >> 14);
+    }
+}
+
+/* pyrDown_<FixPtCast<uchar,8>> [OCV246 imgproc/src/pyramids.cpp]: separable
+ * [1 4 6 4 1]^2, (sum + 128) >> 8, reflect-101 on the SOURCE size. Integer,
+ * so the row ring buffer / SSE2 vecOp order is immaterial. */
+void oracle_pyr_down(const uint8_t *src, int sw, int sh, int sstride, uint8_t *dst, int dstride) {
+    static const int k[5] = {1, 4, 6, 4, 1};
+    int dw = (sw + 1) / 2, dh = (sh + 1) / 2;
+    int *cx = (int *)malloc(sizeof(int) * 5 * dw);
+    for (int x = 0; x < dw; x++)
+        for (int j = 0; j < 5; j++) cx[x * 5 + j] = oracle_refl101(2 * x + j - 2, sw);
+    for (int y = 0; y < dh; y++) {
+        const uint8_t *rows[5];
+        for (int i = 0; i < 5; i++) rows[i] = src + (long)oracle_refl101(2 * y + i - 2, sh) * sstride;
+        for (int x = 0; x < dw; x++) {
+            int acc = 0;
+            for (int i = 0; i < 5; i++) {
+                int r = 0;
+                for (int j = 0; j < 5; j++) r += k[j] * rows[i][cx[x * 5 + j]];
+                acc += k[i] * r;
+            }
+            dst[(long)y * dstride + x] = (uint8_t)((acc + 128) >> 8);
+        }
+    }
+    free(cx);
+}
+
+/* calcSharrDeriv [OCV246 video/src/lkpyramid.cpp]: vertical (3,10,3) / (-1,0,1)
+ * pass with reflect-101 rows, horizontal pass with reflect-101 columns of the
+ * filtered rows; interleaved int16 (Ix, Iy). */
+void oracle_scharr(const uint8_t *src, int w, int h, int sstride, int16_t *dst, int dstride) {
+    int *t0 = (int *)malloc(sizeof(int) * (w + 2));
+    int *t1 = (int *)malloc(sizeof(int) * (w + 2));
+    for (int y = 0; y < h; y++) {
+        const uint8_t *s0 = src + (long)(y > 0 ? y - 1 : h > 1 ? 1 : 0) * sstride;
+        const uint8_t *s1 = src + (long)y * sstride;
+        const uint8_t *s2 = src + (long)(y < h - 1 ? y + 1 : h > 1 ? h - 2 : 0) * sstride;
+        for (int x = 0; x < w; x++) {
+            t0[x + 1] = (s0[x] + s2[x]) * 3 + s1[x] * 10;
+            t1[x + 1] = s2[x] - s0[x];
+        }
+        int x0 = w > 1 ? 1 : 0, x1 = w > 1 ? w - 2 : 0;
+        t0[0] = t0[x0 + 1];
+        t0[w + 1] = t0[x1 + 1];
+        t1[0] = t1[x0 + 1];
+        t1[w + 1] = t1[x1 + 1];
+        int16_t *d = dst + (long)y * dstride;
+        for (int x = 0; x < w; x++) {
+            d[2 * x] = (int16_t)(t0[x + 2] - t0[x]);
+            d[2 * x + 1] = (int16_t)((t1[x + 2] + t1[x]) * 3 + t1[x + 1] * 10);
+        }
+    }
+    free(t0);
+    free(t1);
+}
+
+/* buildOpticalFlowPyramid's stop rule [OCV246 video/src/lkpyramid.cpp]: after
+ * level `l` is built, sz = ((w+1)/2, (h+1)/2); stop (maxLevel = l) when
+ * sz.width <= winW || sz.height <= winH. */
+int oracle_effective_max_level(int w, int h, int win_w, int win_h, int max_level) {
+    int sw = w, sh = h;
+    for (int level = 0; level <= max_level; level++) {
+        sw = (sw + 1) / 2;
+        sh = (sh + 1) / 2;
+        if (sw <= win_w || sh <= win_h) return level;
+    }
+    return max_level;
+}
+
+void oracle_level_size(int w, int h, int level, int *lw, int *lh) {
+    for (int l = 0; l < level; l++) {
+        w = (w + 1) / 2;
+        h = (h + 1) / 2;
+    }
+    *lw = w;
+    *lh = h;
+}
+
+long oracle_level_offset(int w, int h, int level) {
+    long off = 0;
+    for (int l = 0; l < level; l++) {
+        off += (long)w * h;
+        w = (w + 1) / 2;
+        h = (h + 1) / 2;
+    }
+    return off;
+}
+
+/* Level 0 = the image (its reflect-101 border is applied on read), level l+1 =
+ * pyrDown(level l) on the level's own ROI (BORDER_ISOLATED in 2.4.6). */
+void oracle_build_pyramid(const uint8_t *img, int w, int h, int stride, int nlevels, uint8_t *pyr) {
+    for (int y = 0; y < h; y++) memcpy(pyr + (long)y * w, img + (long)y * stride, (size_t)w);
+    int lw = w, lh = h;
+    long off = 0;
+    for (int l = 1; l < nlevels; l++) {
+        int nw = (lw + 1) / 2, nh = (lh + 1) / 2;
+        oracle_pyr_down(pyr + off, lw, lh, lw, pyr + off + (long)lw * lh, nw);
+        off += (long)lw * lh;
+        lw = nw;
+        lh = nh;
+    }
+}
+
+/* A level as calcOpticalFlowPyrLK sees it: I and J padded by winSize with
+ * reflect-101 (copyMakeBorder(..., BORDER_REFLECT_101), buildOpticalFlowPyramid)
+ * and the Scharr plane of I padded by winSize with zeros
+ * (copyMakeBorder(derivI, ..., BORDER_CONSTANT|BORDER_ISOLATED)). Pointers
+ * address the ROI origin; strides are in elements. */
+typedef struct {
+    const uint8_t *I, *J;
+    const int16_t *dI;
+    int stepI, dstep; /* dstep in int16 elements (2 per pixel) */
+    int cols, rows;
+} level_view;
+
+/* copyMakeBorder(src, dst, bh, bh, bw, bw, BORDER_REFLECT_101) */
+static void pad_reflect(const uint8_t *src, int cols, int rows, int bw, int bh, uint8_t *dst) {
+    int dcols = cols + 2 * bw;
+    int *tab = (int *)malloc(sizeof(int) * dcols);
+    for (int x = 0; x < dcols; x++) tab[x] = oracle_refl101(x - bw, cols);
+    for (int y = 0; y < rows + 2 * bh; y++) {
+        const uint8_t *s = src + (long)oracle_refl101(y - bh, rows) * cols;
+        uint8_t *d = dst + (long)y * dcols;
+        memcpy(d + bw, s, (size_t)cols);
+        for (int x = 0; x < bw; x++) d[x] = s[tab[x]];
+        for (int x = bw + cols; x < dcols; x++) d[x] = s[tab[x]];
+    }
+    free(tab);
+}
+
+/* Scharr of `src` into a zero-bordered interleaved int16 buffer. */
+static void scharr_padded(const uint8_t *src, int cols, int rows, int bw, int bh, int16_t *dst) {
+    int dcols = cols + 2 * bw;
+    memset(dst, 0, sizeof(int16_t) * 2 * (size_t)dcols * (rows + 2 * bh));
+    oracle_scharr(src, cols, rows, cols, dst + ((long)bh * dcols + bw) * 2, 2 * dcols);
+}
+
+#define BILIN(p, s, w00, w01, w10, w11) ((p)[0] * (w00) + (p)[1] * (w01) + (p)[s] * (w10) + (p)[(s) + 1] * (w11))
+#define BILIN_D(p, s, c, w00, w01, w10, w11) \
+    ((p)[c] * (w00) + (p)[2 + (c)] * (w01) + (p)[(s) + (c)] * (w10) + (p)[(s) + 2 + (c)] * (w11))
+
+/* LKTrackerInvoker::operator() [OCV246 video/src/lkpyramid.cpp] for one point at
+ * one level. nextPts/status/err are the shared output arrays. The SSE2 build
+ * keeps 4 float lanes for A (4-pixel steps) and 2x4 lanes for b (8-pixel
+ * steps) next to a scalar tail; both are reproduced literally (accum == SSE2). */
+static void lk_point_level(const level_view *lv, int level, int max_level, const float *prev_pts,
+                           float *next_pts, uint8_t *status, float *err, int i, int win_w,
+                           int win_h, int max_count, double eps2, int flags, float min_eig_thr,
+                           int accum, int16_t *ibuf /* 3*win_w*win_h */) {
+    const float hwx = (float)(win_w - 1) * 0.5f, hwy = (float)(win_h - 1) * 0.5f;
+    const float scale = (float)(1. / (1 << level));
+    const int cols = lv->cols, rows = lv->rows;
+    const int sse = accum == ORACLE_ACCUM_SSE2;
+    const int stepI = lv->stepI, dstep = lv->dstep;
+    int16_t *Iw = ibuf, *dIw = ibuf + win_w * win_h; /* dIw interleaved (Ix, Iy) */
+
+    float px = prev_pts[2 * i] * scale, py = prev_pts[2 * i + 1] * scale;
+    float nx, ny;
+    if (level == max_level) {
+        if (flags & ORACLE_USE_INITIAL_FLOW) {
+            nx = next_pts[2 * i] * scale;
+            ny = next_pts[2 * i + 1] * scale;
+        } else {
+            nx = px;
+            ny = py;
+        }
+    } else {
+        nx = next_pts[2 * i] * 2.f;
+        ny = next_pts[2 * i + 1] * 2.f;
+    }
+    next_pts[2 * i] = nx;
+    next_pts[2 * i + 1] = ny;
+
+    px -= hwx;
+    py -= hwy;
+    int ipx = cv_floor(px), ipy = cv_floor(py);
+    if (ipx < -win_w || ipx >= cols || ipy < -win_h || ipy >= rows) {
+        if (level == 0) {
+            status[i] = 0;
+            if (err) err[i] = 0;
+        }
+        return;
+    }
+
+    float a = px - (float)ipx, b = py - (float)ipy;
+    int iw00 = cv_round((1.f - a) * (1.f - b) * (float)(1 << W_BITS));
+    int iw01 = cv_round(a * (1.f - b) * (float)(1 << W_BITS));
+    int iw10 = cv_round((1.f - a) * b * (float)(1 << W_BITS));
+    int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+
+    float A11 = 0, A12 = 0, A22 = 0;
+    float qA11[4] = {0, 0, 0, 0}, qA12[4] = {0, 0, 0, 0}, qA22[4] = {0, 0, 0, 0};
+    for (int y = 0; y < win_h; y++) {
+        const uint8_t *src = lv->I + (long)(y + ipy) * stepI + ipx;
+        const int16_t *dsrc = lv->dI + (long)(y + ipy) * dstep + 2 * ipx;
+        int16_t *Iptr = Iw + y * win_w, *dIptr = dIw + 2 * y * win_w;
+        int x = 0;
+        if (sse) {
+            for (; x <= win_w - 4; x += 4) {
+                int ixv[4], iyv[4];
+                for (int k = 0; k < 4; k++) {
+                    Iptr[x + k] = (int16_t)DESCALE(BILIN(src + x + k, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5);
+                    ixv[k] = DESCALE(BILIN_D(dsrc + 2 * (x + k), dstep, 0, iw00, iw01, iw10, iw11), W_BITS1);
+                    iyv[k] = DESCALE(BILIN_D(dsrc + 2 * (x + k), dstep, 1, iw00, iw01, iw10, iw11), W_BITS1);
+                    dIptr[2 * (x + k)] = (int16_t)ixv[k];
+                    dIptr[2 * (x + k) + 1] = (int16_t)iyv[k];
+                }
+                for (int k = 0; k < 4; k++) {
+                    float fx = (float)ixv[k], fy = (float)iyv[k];
+                    qA22[k] += fy * fy;
+                    qA12[k] += fx * fy;
+                    qA11[k] += fx * fx;
+                }
+            }
+        }
+        for (; x < win_w; x++) {
+            int ival = DESCALE(BILIN(src + x, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5);
+            int ixval = DESCALE(BILIN_D(dsrc + 2 * x, dstep, 0, iw00, iw01, iw10, iw11), W_BITS1);
+            int iyval = DESCALE(BILIN_D(dsrc + 2 * x, dstep, 1, iw00, iw01, iw10, iw11), W_BITS1);
+            Iptr[x] = (int16_t)ival;
+            dIptr[2 * x] = (int16_t)ixval;
+            dIptr[2 * x + 1] = (int16_t)iyval;
+            A11 += (float)(ixval * ixval);
+            A12 += (float)(ixval * iyval);
+            A22 += (float)(iyval * iyval);
+        }
+    }
+    if (sse) {
+        A11 += qA11[0] + qA11[1] + qA11[2] + qA11[3];
+        A12 += qA12[0] + qA12[1] + qA12[2] + qA12[3];
+        A22 += qA22[0] + qA22[1] + qA22[2] + qA22[3];
+    }
+
+    const float FLT_SCALE = 1.f / (1 << 20);
+    A11 *= FLT_SCALE;
+    A12 *= FLT_SCALE;
+    A22 *= FLT_SCALE;
+
+    float D = A11 * A22 - A12 * A12;
+    float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * win_w * win_h);
+
+    if (err && (flags & ORACLE_GET_MIN_EIGENVALS) != 0) err[i] = minEig;
+
+    if (minEig < min_eig_thr || D < FLT_EPSILON) {
+        if (level == 0) status[i] = 0;
+        return;
+    }
+
+    D = 1.f / D;
+    nx -= hwx;
+    ny -= hwy;
+    float pdx = 0.f, pdy = 0.f;
+
+    for (int j = 0; j < max_count; j++) {
+        int inx = cv_floor(nx), iny = cv_floor(ny);
+        if (inx < -win_w || inx >= cols || iny < -win_h || iny >= rows) {
+            if (level == 0) status[i] = 0;
+            break;
+        }
+        a = nx - (float)inx;
+        b = ny - (float)iny;
+        iw00 = cv_round((1.f - a) * (1.f - b) * (float)(1 << W_BITS));
+        iw01 = cv_round(a * (1.f - b) * (float)(1 << W_BITS));
+        iw10 = cv_round((1.f - a) * b * (float)(1 << W_BITS));
+        iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+
+        float b1 = 0, b2 = 0;
+        float qb0[4] = {0, 0, 0, 0}, qb1[4] = {0, 0, 0, 0};
+        for (int y = 0; y < win_h; y++) {
+            const uint8_t *Jptr = lv->J + (long)(y + iny) * stepI + inx;
+            const int16_t *Iptr = Iw + y * win_w, *dIptr = dIw + 2 * y * win_w;
+            int x = 0;
+            if (sse) {
+                for (; x <= win_w - 8; x += 8) {
+                    int d[8];
+                    for (int k = 0; k < 8; k++)
+                        d[k] = DESCALE(BILIN(Jptr + x + k, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5) - Iptr[x + k];
+                    const int16_t *g = dIptr + 2 * x;
+                    /* diff0 = pixels 0..3: lanes qb0 <- (0,1), qb1 <- (2,3) */
+                    qb0[0] += (float)(g[0] * d[0]);
+                    qb0[1] += (float)(g[1] * d[0]);
+                    qb0[2] += (float)(g[2] * d[1]);
+                    qb0[3] += (float)(g[3] * d[1]);
+                    qb1[0] += (float)(g[4] * d[2]);
+                    qb1[1] += (float)(g[5] * d[2]);
+                    qb1[2] += (float)(g[6] * d[3]);
+                    qb1[3] += (float)(g[7] * d[3]);
+                    /* diff1 = pixels 4..7: qb0 <- (4,5), qb1 <- (6,7) */
+                    qb0[0] += (float)(g[8] * d[4]);
+                    qb0[1] += (float)(g[9] * d[4]);
+                    qb0[2] += (float)(g[10] * d[5]);
+                    qb0[3] += (float)(g[11] * d[5]);
+                    qb1[0] += (float)(g[12] * d[6]);
+                    qb1[1] += (float)(g[13] * d[6]);
+                    qb1[2] += (float)(g[14] * d[7]);
+                    qb1[3] += (float)(g[15] * d[7]);
+                }
+            }
+            for (; x < win_w; x++) {
+                int diff = DESCALE(BILIN(Jptr + x, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5) - Iptr[x];
+                b1 += (float)(diff * dIptr[2 * x]);
+                b2 += (float)(diff * dIptr[2 * x + 1]);
+            }
+        }
+        if (sse) {
+            float bb[4];
+            for (int k = 0; k < 4; k++) bb[k] = qb0[k] + qb1[k];
+            b1 += bb[0] + bb[2];
+            b2 += bb[1] + bb[3];
+        }
+        b1 *= FLT_SCALE;
+        b2 *= FLT_SCALE;
+
+        float dx = (float)((A12 * b2 - A22 * b1) * D);
+        float dy = (float)((A12 * b1 - A11 * b2) * D);
+        nx += dx;
+        ny += dy;
+        next_pts[2 * i] = nx + hwx;
+        next_pts[2 * i + 1] = ny + hwy;
+
+        if ((double)dx * (double)dx + (double)dy * (double)dy <= eps2) break;
+        if (j > 0 && fabsf(dx + pdx) < 0.01 && fabsf(dy + pdy) < 0.01) {
+            next_pts[2 * i] -= dx * 0.5f;
+            next_pts[2 * i + 1] -= dy * 0.5f;
+            break;
+        }
+        pdx = dx;
+        pdy = dy;
+    }
+
+    if (status[i] && err && level == 0 && (flags & ORACLE_GET_MIN_EIGENVALS) == 0) {
+        float qx = next_pts[2 * i] - hwx, qy = next_pts[2 * i + 1] - hwy;
+        int iqx = cv_floor(qx), iqy = cv_floor(qy);
+        if (iqx < -win_w || iqx >= cols || iqy < -win_h || iqy >= rows) {
+            status[i] = 0;
+            return;
+        }
+        float aa = qx - (float)iqx, bb = qy - (float)iqy;
+        iw00 = cv_round((1.f - aa) * (1.f - bb) * (float)(1 << W_BITS));
+        iw01 = cv_round(aa * (1.f - bb) * (float)(1 << W_BITS));
+        iw10 = cv_round((1.f - aa) * bb * (float)(1 << W_BITS));
+        iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+        float errval = 0.f;
+        for (int y = 0; y < win_h; y++) {
+            const uint8_t *Jptr = lv->J + (long)(y + iqy) * stepI + iqx;
+            const int16_t *Iptr = Iw + y * win_w;
+            for (int x = 0; x < win_w; x++) {
+                int diff = DESCALE(BILIN(Jptr + x, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5) - Iptr[x];
+                errval += fabsf((float)diff);
+            }
+        }
+        err[i] = errval * 1.f / (float)(32 * win_w * win_h);
+    }
+}
+
+/* calcOpticalFlowPyrLK body [OCV246]: criteria clamp, status=1, then for
+ * level = maxLevel..0 { calcSharrDeriv(prevPyr[level]) + zero border;
+ * parallel_for_ over points (LKTrackerInvoker) }. */
+int oracle_lk_track_pyr(const uint8_t *prev_pyr, const uint8_t *next_pyr, int w, int h,
+                        const float *prev_pts, float *next_pts, uint8_t *status, float *err,
+                        int npts, int win_w, int win_h, int max_level, int term_type,
+                        int max_count, double epsilon, int flags, double min_eig_threshold,
+                        int accum_mode, int nthreads) {
+    if (win_w <= 2 || win_h <= 2 || max_level < 0) return -2;
+    if (npts <= 0) return 0;
+    if ((term_type & 1) == 0)
+        max_count = 30;
+    else
+        max_count = max_count < 0 ? 0 : max_count > 100 ? 100 : max_count;
+    if ((term_type & 2) == 0)
+        epsilon = 0.01;
+    else
+        epsilon = epsilon < 0. ? 0. : epsilon > 10. ? 10. : epsilon;
+    double eps2 = epsilon * epsilon;
+    float min_eig_thr = (float)min_eig_threshold;
+
+    for (int i = 0; i < npts; i++) status[i] = 1;
+    if (err)
+        for (int i = 0; i < npts; i++) err[i] = 0.f;
+
+    size_t pad_px = (size_t)(w + 2 * win_w) * (h + 2 * win_h);
+    uint8_t *Ipad = (uint8_t *)malloc(pad_px), *Jpad = (uint8_t *)malloc(pad_px);
+    int16_t *Dpad = (int16_t *)malloc(sizeof(int16_t) * 2 * pad_px);
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+    (void)nthreads;
+#endif
+    for (int level = max_level; level >= 0; level--) {
+        int cols, rows;
+        oracle_level_size(w, h, level, &cols, &rows);
+        const uint8_t *I = prev_pyr + oracle_level_offset(w, h, level);
+        const uint8_t *J = next_pyr + oracle_level_offset(w, h, level);
+        int pc = cols + 2 * win_w;
+        pad_reflect(I, cols, rows, win_w, win_h, Ipad);
+        pad_reflect(J, cols, rows, win_w, win_h, Jpad);
+        scharr_padded(I, cols, rows, win_w, win_h, Dpad);
+        level_view lv = {Ipad + (long)win_h * pc + win_w, Jpad + (long)win_h * pc + win_w,
+                         Dpad + ((long)win_h * pc + win_w) * 2, pc, 2 * pc, cols, rows};
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads)
+#endif
+        {
+            int16_t *ibuf = (int16_t *)malloc(sizeof(int16_t) * 3 * (size_t)win_w * win_h);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+            for (int i = 0; i < npts; i++)
+                lk_point_level(&lv, level, max_level, prev_pts, next_pts, status, err, i, win_w, win_h,
+                               max_count, eps2, flags, min_eig_thr, accum_mode, ibuf);
+            free(ibuf);
+        }
+    }
+    free(Ipad);
+    free(Jpad);
+    free(Dpad);
+    return 0;
+}
+
+int oracle_calc_optical_flow_pyr_lk(const uint8_t *prev_img, const uint8_t *next_img, int w, int h,
+                                    int stride, const float *prev_pts, float *next_pts,
+                                    uint8_t *status, float *err, int npts, int win_w, int win_h,
+                                    int max_level, int term_type, int max_count, double epsilon,
+                                    int flags, double min_eig_threshold, int accum_mode,
+                                    int nthreads) {
+    if (win_w <= 2 || win_h <= 2 || max_level < 0) return -2;
+    if (npts <= 0) return 0;
+    int ml = oracle_effective_max_level(w, h, win_w, win_h, max_level);
+    long total = oracle_level_offset(w, h, ml + 1);
+    uint8_t *pp = (uint8_t *)malloc((size_t)total), *np = (uint8_t *)malloc((size_t)total);
+    oracle_build_pyramid(prev_img, w, h, stride, ml + 1, pp);
+    oracle_build_pyramid(next_img, w, h, stride, ml + 1, np);
+    int rc = oracle_lk_track_pyr(pp, np, w, h, prev_pts, next_pts, status, err, npts, win_w, win_h, ml,
+                                 term_type, max_count, epsilon, flags, min_eig_threshold, accum_mode,
+                                 nthreads);
+    free(pp);
+    free(np);
+    return rc;
+}

@@ -1,0 +1,79 @@
+/*
+ * oracle/lk_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the OpenCV 2.4.6 pyramidal Lucas-Kanade path that
+ * CPSNWhere_Tracker2D calls (psn_where/PSNWhere_Tracker2D.cpp:776-782 backward,
+ * :871-877 forward). Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library; the product path never does.
+ *
+ * PARITY UNPINNED: the arithmetic lives in OpenCV 2.4.6 (pinned by
+ * $(OPENCV_246) and the *246.lib names, psn_where/PSN_Where.vcxproj:97,104,
+ * 124-125,151,175-176), which is not vendored in the reference and is absent
+ * from this image; the reference ships no tests, fixtures or golden vectors.
+ * The restatement follows OpenCV 2.4.6's published algorithm
+ * (modules/video/src/lkpyramid.cpp, modules/imgproc/src/pyramids.cpp,
+ * color.cpp) and is pinned by self-made known-answer tests (tests/).
+ */
+#ifndef PSN_LK_ORACLE_H
+#define PSN_LK_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Accumulation order of the float normal-equation sums.
+ * 0 = the SSE2 build of OpenCV 2.4.6 (x64/x86 prebuilt libs the reference
+ *     links): 4-lane partial sums for A, 8-pixel/2x4-lane for b, scalar tail.
+ * 1 = the scalar (no-SIMD) build: one sequential float chain per sum. */
+#define ORACLE_ACCUM_SSE2 0
+#define ORACLE_ACCUM_SCALAR 1
+
+/* cv::OPTFLOW_* flag values (OpenCV 2.4.6 video/tracking.hpp) */
+#define ORACLE_USE_INITIAL_FLOW 4
+#define ORACLE_GET_MIN_EIGENVALS 8
+
+int oracle_refl101(int p, int len);
+
+/* cv::cvtColor(CV_BGR2GRAY) for CV_8UC3 (PSNWhere_Tracker2D.cpp:257). */
+void oracle_bgr2gray(const uint8_t *src, int w, int h, int sstride, uint8_t *dst, int dstride);
+
+/* cv::pyrDown, BORDER_REFLECT_101, dst size ((w+1)/2, (h+1)/2). */
+void oracle_pyr_down(const uint8_t *src, int sw, int sh, int sstride, uint8_t *dst, int dstride);
+
+/* calcSharrDeriv: interleaved int16 (Ix, Iy), reflect-101 inside the image. */
+void oracle_scharr(const uint8_t *src, int w, int h, int sstride, int16_t *dst, int dstride_elems);
+
+/* Level truncation of buildOpticalFlowPyramid: effective maxLevel. */
+int oracle_effective_max_level(int w, int h, int win_w, int win_h, int max_level);
+
+/* Pyramid of `nlevels` u8 planes packed contiguously (level l at offset
+ * oracle_level_offset(w,h,l), pitch = level width). */
+long oracle_level_offset(int w, int h, int level);
+void oracle_level_size(int w, int h, int level, int *lw, int *lh);
+void oracle_build_pyramid(const uint8_t *img, int w, int h, int stride, int nlevels, uint8_t *pyr);
+
+/* LK over prebuilt pyramids (packed as above); derivatives are computed per
+ * level inside, as calcOpticalFlowPyrLK does. `max_level` must already be the
+ * effective (truncated) level; both pyramids must hold >= max_level+1 levels.
+ * Returns 0, or -2 when winSize <= 2 (CV_Assert). */
+int oracle_lk_track_pyr(const uint8_t *prev_pyr, const uint8_t *next_pyr, int w, int h,
+                        const float *prev_pts, float *next_pts, uint8_t *status, float *err,
+                        int npts, int win_w, int win_h, int max_level, int term_type,
+                        int max_count, double epsilon, int flags, double min_eig_threshold,
+                        int accum_mode, int nthreads);
+
+/* One-shot cv::calcOpticalFlowPyrLK(prev, next, ...) with the reference call
+ * schedule: both pyramids (and the Scharr planes) rebuilt inside the call. */
+int oracle_calc_optical_flow_pyr_lk(const uint8_t *prev_img, const uint8_t *next_img, int w, int h,
+                                    int stride, const float *prev_pts, float *next_pts,
+                                    uint8_t *status, float *err, int npts, int win_w, int win_h,
+                                    int max_level, int term_type, int max_count, double epsilon,
+                                    int flags, double min_eig_threshold, int accum_mode,
+                                    int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

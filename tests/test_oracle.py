@@ -1,0 +1,173 @@
+"""CPU tests of the oracle (oracle/lk_oracle.c) -- known-answer tests that pin
+the restatement of OpenCV 2.4.6's LK stack, which the reference reaches via
+cv::calcOpticalFlowPyrLK (psn_where/PSNWhere_Tracker2D.cpp:776-782, :871-877).
+
+Parity with OpenCV itself is UNPINNED (OpenCV 2.4.6 absent, no reference
+fixtures); these tests pin the arithmetic rules by exact expected values
+derived by hand from the published algorithm, plus analytic-flow recovery.
+"""
+import numpy as np
+import pytest
+
+from mcmtt_opticalflow_amd import synth
+
+
+def test_refl101(oracle_mod):
+    r = oracle_mod.refl101
+    assert [r(p, 5) for p in (-3, -2, -1, 0, 4, 5, 6, 7)] == [3, 2, 1, 0, 4, 3, 2, 1]
+    assert r(-1, 1) == 0 and r(7, 1) == 0
+    assert r(-1, 2) == 1 and r(2, 2) == 0 and r(3, 2) == 1
+    # repeated reflection when the border exceeds the length
+    assert r(-9, 4) == oracle_mod.refl101(r(-9 + 6, 4), 4) or 0 <= r(-9, 4) < 4
+
+
+def test_bgr2gray_known_values(oracle_mod):
+    px = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255], [10, 20, 30]]], np.uint8)
+    g = oracle_mod.bgr2gray(px)[0]
+    exp = [(b * 1868 + gg * 9617 + r * 4899 + 8192) >> 14 for b, gg, r in px[0].tolist()]
+    assert g.tolist() == exp == [29, 150, 76, 255, 22]
+
+
+def _pyr_down_ref(img):
+    """Direct 5x5 reflect-101 definition, pure numpy (independent of the C)."""
+    h, w = img.shape
+    k = np.array([1, 4, 6, 4, 1])
+    dh, dw = (h + 1) // 2, (w + 1) // 2
+
+    def refl(p, n):
+        if n == 1:
+            return 0
+        while p < 0 or p >= n:
+            p = -p if p < 0 else 2 * n - 2 - p
+        return p
+
+    out = np.zeros((dh, dw), np.uint8)
+    for y in range(dh):
+        for x in range(dw):
+            s = 0
+            for i in range(5):
+                for j in range(5):
+                    s += k[i] * k[j] * int(img[refl(2 * y + i - 2, h), refl(2 * x + j - 2, w)])
+            out[y, x] = (s + 128) >> 8
+    return out
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (1, 7), (2, 2), (3, 5), (7, 9), (16, 13)])
+def test_pyr_down_matches_definition(oracle_mod, shape):
+    rng = np.random.default_rng(shape[0] * 31 + shape[1])
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    np.testing.assert_array_equal(oracle_mod.pyr_down(img), _pyr_down_ref(img))
+
+
+def test_pyr_down_constant_and_size(oracle_mod):
+    img = np.full((11, 15), 77, np.uint8)
+    d = oracle_mod.pyr_down(img)
+    assert d.shape == (6, 8) and np.all(d == 77)
+
+
+def test_scharr_ramp_exact(oracle_mod):
+    # I = 3x + 5y: interior Ix = 2*16*3 = 96 (t0 scale 16, central difference 2)
+    h, w = 9, 12
+    yy, xx = np.mgrid[0:h, 0:w]
+    img = (3 * xx + 5 * yy).astype(np.uint8)
+    d = oracle_mod.scharr(img)
+    assert np.all(d[1:-1, 1:-1, 0] == 96)
+    assert np.all(d[1:-1, 1:-1, 1] == 160)
+    # reflect-101 borders: derivative across the border is zero
+    assert np.all(d[:, 0, 0] == 0) and np.all(d[:, -1, 0] == 0)
+    assert np.all(d[0, :, 1] == 0) and np.all(d[-1, :, 1] == 0)
+
+
+def test_scharr_single_pixel(oracle_mod):
+    d = oracle_mod.scharr(np.array([[200]], np.uint8))
+    assert d.tolist() == [[[0, 0]]]
+
+
+@pytest.mark.parametrize("w,h,win,ml,exp", [
+    (1920, 1080, 21, 3, 3), (640, 480, 21, 3, 3), (640, 480, 32, 3, 3), (640, 480, 60, 3, 2),
+    (1920, 1080, 64, 3, 3), (1920, 1080, 160, 3, 2), (100, 100, 60, 3, 0), (30, 30, 21, 5, 0),
+])
+def test_effective_max_level(oracle_mod, w, h, win, ml, exp):
+    assert oracle_mod.effective_max_level(w, h, win, win, ml) == exp
+
+
+def _textured(w, h, seed):
+    return synth.texture(w, h, seed)
+
+
+@pytest.mark.parametrize("shift", [(0, 0), (2, 0), (0, -3), (1, 1)])
+def test_lk_integer_shift(oracle_mod, shift):
+    img = _textured(160, 120, 5)
+    dx, dy = shift
+    nxt_img = np.roll(np.roll(img, dy, axis=0), dx, axis=1)
+    pts = np.array([[80.0, 60.0], [50.5, 40.25], [100.0, 70.0]], np.float32)
+    nxt, st, err = oracle_mod.calc_optical_flow_pyr_lk(img, nxt_img, pts, (15, 15), 2)
+    assert st.tolist() == [1, 1, 1]
+    np.testing.assert_allclose(nxt - pts, np.array([[dx, dy]] * 3, np.float32), atol=0.05)
+    assert np.all(err >= 0)
+    if shift == (0, 0):
+        np.testing.assert_array_equal(nxt, pts)
+        assert np.all(err == 0)
+
+
+def test_lk_analytic_subpixel_flow(oracle_mod):
+    sc = synth.make_scene(3, 320, 240, 64, nboxes=2, box_w=48, box_h=96, max_speed=3.0)
+    f0, f1 = sc.frame(0), sc.frame(1)
+    p0 = sc.points_at(0)
+    gt = sc.points_at(1)
+    # keep points well inside their box so the window sees one motion
+    inner = np.all((p0 - sc.boxes0[sc.pt_box] > 14) & (sc.boxes0[sc.pt_box] + [48, 96] - p0 > 14), axis=1)
+    nxt, st, _ = oracle_mod.calc_optical_flow_pyr_lk(f0, f1, p0, (11, 11), 3)
+    e = np.linalg.norm(nxt - gt, axis=1)[inner & (st == 1)]
+    assert inner.sum() >= 10 and np.median(e) < 0.05
+
+
+def test_lk_out_of_image_point_status(oracle_mod):
+    img = _textured(64, 48, 1)
+    pts = np.array([[-40.0, 10.0], [10.0, 500.0], [30.0, 20.0]], np.float32)
+    nxt, st, err = oracle_mod.calc_optical_flow_pyr_lk(img, img, pts, (9, 9), 1)
+    assert st.tolist() == [0, 0, 1]
+    assert err[0] == 0 and err[1] == 0
+
+
+def test_lk_flat_image_min_eig_fails(oracle_mod):
+    img = np.full((40, 40), 90, np.uint8)
+    pts = np.array([[20.0, 20.0]], np.float32)
+    nxt, st, _ = oracle_mod.calc_optical_flow_pyr_lk(img, img, pts, (7, 7), 2)
+    assert st[0] == 0
+    np.testing.assert_array_equal(nxt, pts)  # nextPts still written (= initial guess)
+
+
+def test_lk_winsize_assert(oracle_mod):
+    img = np.zeros((20, 20), np.uint8)
+    with pytest.raises(ValueError):
+        oracle_mod.calc_optical_flow_pyr_lk(img, img, np.zeros((1, 2), np.float32), (2, 5), 1)
+
+
+def test_lk_accum_orders_close(oracle_mod):
+    sc = synth.make_scene(7, 320, 240, 128)
+    f0, f1 = sc.frame(0), sc.frame(1)
+    p0 = sc.points_at(0)
+    a, sa, _ = oracle_mod.calc_optical_flow_pyr_lk(f0, f1, p0, (21, 21), 3, accum=oracle_mod.ACCUM_SSE2)
+    b, sb, _ = oracle_mod.calc_optical_flow_pyr_lk(f0, f1, p0, (21, 21), 3, accum=oracle_mod.ACCUM_SCALAR)
+    ok = (sa == 1) & (sb == 1)
+    # the two OpenCV builds differ only in float summation order
+    assert np.median(np.linalg.norm(a - b, axis=1)[ok]) < 1e-3
+
+
+def test_lk_threads_deterministic(oracle_mod):
+    sc = synth.make_scene(2, 320, 240, 96)
+    f0, f1 = sc.frame(0), sc.frame(1)
+    p0 = sc.points_at(0)
+    r1 = oracle_mod.calc_optical_flow_pyr_lk(f0, f1, p0, (21, 21), 3, nthreads=1)
+    r4 = oracle_mod.calc_optical_flow_pyr_lk(f0, f1, p0, (21, 21), 3, nthreads=4)
+    for x, y in zip(r1, r4):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_lk_min_eigenvals_flag(oracle_mod):
+    sc = synth.make_scene(4, 160, 120, 16, nboxes=1)
+    f0 = sc.frame(0)
+    p0 = sc.points_at(0)
+    _, st, err = oracle_mod.calc_optical_flow_pyr_lk(f0, f0, p0, (9, 9), 1, flags=oracle_mod.GET_MIN_EIGENVALS)
+    assert np.all(err[st == 1] > 1e-4)
