@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Tracker2D LK hot-path benchmark (BASELINE.json metric) on MI355X.
+
+One step = one camera-frame of the per-camera hot path on every rank:
+  1. ingest frame t into the camera's device ring + build its 4-level pyramid
+     (pyramid_kernel; replaces cvtColor/resize + buildOpticalFlowPyramid,
+     PSNWhere_Tracker2D.cpp:257-262, :776-782, :871-877),
+  2. pyramidal LK of the camera's 512 tracked points from frame t-1 to t
+     (lk_kernel; the calcOpticalFlowPyrLK call), outputs written in place into
+     the camera's tracklet slot; the tracked points of t are the inputs of t+1
+     (tracklet propagation, no host round trip),
+  3. N>1: one RCCL all-gather of the per-camera slots (the hand-off into
+     Associator3D, PSNWhere.cpp:264-269).
+Workload (BASELINE.json configs[1]): 1 camera per GPU, 1920x1080 gray, 512
+points, 4-level pyramid, 21x21 window, default criteria. Inputs are synthetic
+(mcmtt_opticalflow_amd/synth.py) and resident in HBM before timing.
+
+Single GPU:  python bench.py --steps 200 --warmup 10
+Multi GPU:   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Tracker2D frames/sec (all cameras) + achieved HBM GB/s fraction, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def level_sizes(w, h, nlev):
+    out = []
+    for _ in range(nlev):
+        out.append((w, h))
+        w, h = (w + 1) // 2, (h + 1) // 2
+    return out
+
+
+def algorithmic_bytes(w, h, nlev, npts, c_in=1):
+    """B = c_in*S0 + 4*S_pyr - S_{L-1} + 21*N per camera-frame,
+    split per kernel: pyramid = c_in*S0 + S_pyr (write) + (S_pyr - S_{L-1})
+    (pyrDown reads); LK = 2*S_pyr (I and J pyramids read once) + 21*N."""
+    sz = [a * b for a, b in level_sizes(w, h, nlev)]
+    s_pyr = sum(sz)
+    pyr = c_in * sz[0] + s_pyr + (s_pyr - sz[-1])
+    lk = 2 * s_pyr + 21 * npts
+    return pyr, lk
+
+
+def ping_pong(t, period):
+    """Frame index of step t in a 0..P-1..0 sequence (keeps boxes in view)."""
+    m = t % (2 * (period - 1))
+    return m if m < period else 2 * (period - 1) - m
+
+
+def render_frames_torch(scene, period, device):
+    import numpy as np
+    import torch
+
+    from mcmtt_opticalflow_amd import synth
+
+    frames = torch.empty((period, scene.height, scene.width), dtype=torch.uint8, device=device)
+    for t in range(period):
+        frames[t].copy_(torch.from_numpy(scene.frame(t)))
+    return frames
+
+
+def cpu_baseline(scene, period, npts, win, max_level, budget_s, max_frames):
+    """The oracle (reference call schedule: both pyramids + Scharr rebuilt in
+    every calcOpticalFlowPyrLK call) on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # cpu_baseline leg only
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    frames = [scene.frame(t) for t in range(period)]
+    pts = scene.points_at(0)
+    oracle.calc_optical_flow_pyr_lk(frames[0], frames[1], pts, win, max_level, nthreads=threads)  # warm
+    n = 0
+    t0 = time.perf_counter()
+    while n < max_frames:
+        a, b = frames[ping_pong(n, period)], frames[ping_pong(n + 1, period)]
+        pts, _, _ = oracle.calc_optical_flow_pyr_lk(a, b, pts, win, max_level, nthreads=threads)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} camera-frames of the same workload (1920x1080, {npts} pts, 21x21, 4 levels), "
+                      f"oracle/lk_oracle.c with OpenMP over points, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--points", type=int, default=512)
+    ap.add_argument("--levels", type=int, default=4)
+    ap.add_argument("--win", type=int, default=21)
+    ap.add_argument("--period", type=int, default=10)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from mcmtt_opticalflow_amd import dist as pdist
+    from mcmtt_opticalflow_amd import lk, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    cam = rank
+    W, H, N, L, win = args.width, args.height, args.points, args.levels, args.win
+    R = 4  # ring slots, PSN_2D_BACKTRACKING_INTERVAL (PSNWhere_Tracker2D.cpp:16)
+
+    scene = synth.make_scene(cam, W, H, N)
+    frames = render_frames_torch(scene, args.period, device)
+    # one explicit stream for the library kernels and the torch ops around them
+    stream = torch.cuda.Stream(device)
+    torch.cuda.set_stream(stream)
+    ctx = lk.LKContext(W, H, ring_slots=R, max_level_cap=L - 1, device=local_rank)
+    ctx.set_stream(stream.cuda_stream)
+
+    sb = pdist.slot_bytes(N)
+    slots = [torch.zeros(sb, dtype=torch.uint8, device=device) for _ in range(2)]
+    views = [pdist.slot_views(s, N) for s in slots]
+    for hdr, nxt, _, _ in views:
+        hdr.copy_(torch.tensor([cam, 0, N, 0], dtype=torch.int32))
+    views[0][1].copy_(torch.from_numpy(scene.points_at(0)))
+    gathered = torch.empty((world, sb), dtype=torch.uint8, device=device)
+    params = lk.make_params((win, win), L - 1)
+    ctx.push_frame_device(0, frames[0].data_ptr(), W, 1)
+
+    def step(t):
+        cur, prv = views[t % 2], views[(t - 1) % 2]
+        f = frames[ping_pong(t, args.period)]
+        ctx.push_frame_device(t % R, f.data_ptr(), W, 1)
+        q = lk.make_query((t - 1) % R, t % R, 0, N, params)
+        ctx.track_device([q], prv[1].data_ptr(), cur[1].data_ptr(), cur[3].data_ptr(), cur[2].data_ptr())
+        cur[0][1].fill_(t)
+        if world > 1:
+            pdist.allgather_slots(slots[t % 2], world, out=gathered)
+
+    t = 1
+    for _ in range(args.warmup):
+        step(t)
+        t += 1
+    ctx.enable_timing(args.steps + 1)  # syncs the stream
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(t)
+        t += 1
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = pdist.max_over_ranks(elapsed, device)
+    ts = ctx.timing_stats()
+    tracked = int(views[(t - 1) % 2][3].sum().item())
+
+    pyr_bytes, lk_bytes = algorithmic_bytes(W, H, L, N)
+    pyr_us = 1e3 * ts["push_ms"] / max(ts["n_push"], 1)
+    lk_us = 1e3 * ts["track_ms"] / max(ts["n_track"], 1)
+    fps_all = world * args.steps / elapsed
+    per_gpu_fps = args.steps / elapsed
+    frame_bytes = pyr_bytes + lk_bytes
+
+    if rank == 0:
+        dom = ("lk_kernel", lk_bytes, lk_us) if lk_us >= pyr_us else ("pyramid_kernel", pyr_bytes, pyr_us)
+        achieved = dom[1] / (dom[2] * 1e-6) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": round(fps_all, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8+f32",
+            "data": "synthetic",
+            "config": {
+                "workload": "BASELINE.json configs[1]: 1 camera per GPU, 1920x1080 gray, 512 points, "
+                            "4-level pyramid, 21x21 window, per-frame pyramid build + LK + tracklet propagation"
+                            + (", RCCL all-gather of per-camera slots" if world > 1 else ""),
+                "cameras": world, "width": W, "height": H, "points_per_camera": N, "levels": L,
+                "win": [win, win], "parallelism": f"camera-per-GPU x{world}",
+            },
+            "roofline": {
+                "kernel": dom[0], "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                "bytes_per_launch": dom[1], "avg_launch_us": round(dom[2], 3),
+            },
+            "kernels_us": {"pyramid_kernel": round(pyr_us, 3), "lk_kernel": round(lk_us, 3)},
+            "frame_level": {
+                "algorithmic_bytes_per_camera_frame": frame_bytes,
+                "achieved_GBps_per_gpu": round(frame_bytes * per_gpu_fps / 1e9, 2),
+                "hbm_fraction": round(frame_bytes * per_gpu_fps / 1e9 / HBM_PEAK_GBPS, 5),
+            },
+            "tracked_points_last_frame": tracked,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene, args.period, N, (win, win), L - 1, args.cpu_budget, 2000)
+            out["speedup_vs_cpu"] = round(fps_all / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

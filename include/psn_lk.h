@@ -128,10 +128,18 @@ int psn_calc_optical_flow_pyr_lk(psn_lk_ctx *ctx, const uint8_t *prev_img, const
 int psn_lk_read_level(psn_lk_ctx *ctx, int slot, int level, uint8_t *host, int stride);
 int psn_lk_level_size(psn_lk_ctx *ctx, int level, int *w, int *h);
 
-/* Device-side timing of the last psn_lk_push_frame / psn_lk_track calls
- * (HIP events on the context stream) when enabled. Milliseconds. */
-int psn_lk_enable_timing(psn_lk_ctx *ctx, int on);
-int psn_lk_last_timing(psn_lk_ctx *ctx, float *push_ms, float *track_ms);
+/* Device-side kernel timing with HIP events recorded on the context stream
+ * around every psn_lk_push_frame* (pyramid kernel) and psn_lk_track* (LK
+ * kernel) call. `capacity` = calls of each kind kept in an event ring
+ * (0 disables). psn_lk_timing_stats waits for the recorded events, returns
+ * the number of timed calls and their summed milliseconds, and resets. */
+int psn_lk_enable_timing(psn_lk_ctx *ctx, int capacity);
+int psn_lk_timing_stats(psn_lk_ctx *ctx, int *n_push, double *push_ms, int *n_track, double *track_ms);
+
+/* Diagnostic builds only (libpsn_lk_stamps.so, -DPSN_LK_STAMPS): record
+ * shader-clock stamps of every LK workgroup's phases into a device buffer of
+ * 64 u64 per workgroup. Returns PSN_LK_ERR_UNSUPPORTED in product builds. */
+int psn_lk_debug_set_stamps(psn_lk_ctx *ctx, void *d_stamps);
 
 /* ---- multi-GPU: per-camera tracklet slots all-gathered over RCCL/xGMI ----
  * Replaces the in-process std::vector<stTrack2DResult> hand-off into

@@ -11,7 +11,7 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpsn_lk.so")
+LIB_PATH = os.environ.get("PSN_LK_LIB") or os.path.join(_HERE, "lib", "libpsn_lk.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psn_lk.h")
 
 PSN_LK_OK = 0
@@ -102,7 +102,9 @@ def load():
     L.psn_lk_read_level.argtypes = [vp, ip, ip, u8p, ip]
     L.psn_lk_level_size.argtypes = [vp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]
     L.psn_lk_enable_timing.argtypes = [vp, ip]
-    L.psn_lk_last_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    L.psn_lk_timing_stats.argtypes = [vp, ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double)]
+    L.psn_lk_debug_set_stamps.argtypes = [vp, vp]
     L.psn_comm_get_unique_id.argtypes = [vp]
     L.psn_comm_init.argtypes = [ip, ip, ip, vp, ctypes.POINTER(vp)]
     L.psn_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -36,10 +37,15 @@ struct psn_lk_ctx {
     float *d_prev = nullptr, *d_next = nullptr, *d_err = nullptr;
     uint8_t *d_status = nullptr;
     size_t d_pts_cap = 0;
-    // timing
-    bool timing = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    bool push_timed = false, track_timed = false;
+    // tuning / test overrides read at create time: PSN_LK_THREADS=64|128|256,
+    // PSN_LK_GENERIC=1 (always the tiled kernel)
+    int force_threads = 0;
+    bool force_generic = false;
+    unsigned long long *d_stamps = nullptr;  // diagnostic build only
+    // timing: event ring, 2 events per timed call
+    int tcap = 0;
+    std::vector<hipEvent_t> ev_push, ev_track;
+    long n_push = 0, n_track = 0;
     std::string err;
 };
 
@@ -103,6 +109,8 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     c->user_slots = ring_slots;
     c->nslots = ring_slots + 2;
     c->nlevels = max_level_cap + 1;
+    if (const char *e = getenv("PSN_LK_THREADS")) c->force_threads = atoi(e);
+    if (const char *e = getenv("PSN_LK_GENERIC")) c->force_generic = atoi(e) != 0;
     auto fail = [&](int rc) {
         psn_lk_destroy(c);
         return rc;
@@ -138,8 +146,6 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (hipMemcpy(c->d_slots, c->h_slots.data(), sizeof(LevelDev) * c->h_slots.size(), hipMemcpyHostToDevice) != hipSuccess)
         return fail(PSN_LK_ERR_HIP);
     c->filled.assign(c->nslots, 0);
-    for (auto &e : c->ev)
-        if (hipEventCreate(&e) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     *out = c;
     return PSN_LK_OK;
 }
@@ -148,8 +154,9 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-    for (auto &e : c->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto *v : {&c->ev_push, &c->ev_track})
+        for (auto e : *v)
+            if (e) (void)hipEventDestroy(e);
     for (void *p : {(void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status})
         if (p) (void)hipFree(p);
@@ -173,24 +180,46 @@ int psn_lk_sync(psn_lk_ctx *c) {
     return PSN_LK_OK;
 }
 
-int psn_lk_enable_timing(psn_lk_ctx *c, int on) {
-    if (!c) return PSN_LK_ERR_ARG;
-    c->timing = on != 0;
-    c->push_timed = c->track_timed = false;
+int psn_lk_enable_timing(psn_lk_ctx *c, int capacity) {
+    if (!c || capacity < 0) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (auto *v : {&c->ev_push, &c->ev_track}) {
+        for (auto e : *v)
+            if (e) (void)hipEventDestroy(e);
+        v->assign(2 * (size_t)capacity, nullptr);
+        for (auto &e : *v) HIPCHK(c, hipEventCreate(&e));
+    }
+    c->tcap = capacity;
+    c->n_push = c->n_track = 0;
     return PSN_LK_OK;
 }
 
-int psn_lk_last_timing(psn_lk_ctx *c, float *push_ms, float *track_ms) {
+static int sum_events(psn_lk_ctx *c, std::vector<hipEvent_t> &ev, long n, double *ms) {
+    *ms = 0.0;
+    const long k = std::min<long>(n, c->tcap);
+    for (long i = 0; i < k; i++) {
+        HIPCHK(c, hipEventSynchronize(ev[2 * i + 1]));
+        float t = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
+        *ms += t;
+    }
+    return PSN_LK_OK;
+}
+
+int psn_lk_timing_stats(psn_lk_ctx *c, int *n_push, double *push_ms, int *n_track, double *track_ms) {
     if (!c) return PSN_LK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    if (push_ms) {
-        *push_ms = -1.f;
-        if (c->push_timed) HIPCHK(c, hipEventElapsedTime(push_ms, c->ev[0], c->ev[1]));
-    }
-    if (track_ms) {
-        *track_ms = -1.f;
-        if (c->track_timed) HIPCHK(c, hipEventElapsedTime(track_ms, c->ev[2], c->ev[3]));
-    }
+    double pm = 0, tm = 0;
+    int rc = sum_events(c, c->ev_push, c->n_push, &pm);
+    if (rc) return rc;
+    rc = sum_events(c, c->ev_track, c->n_track, &tm);
+    if (rc) return rc;
+    if (n_push) *n_push = (int)std::min<long>(c->n_push, c->tcap);
+    if (n_track) *n_track = (int)std::min<long>(c->n_track, c->tcap);
+    if (push_ms) *push_ms = pm;
+    if (track_ms) *track_ms = tm;
+    c->n_push = c->n_track = 0;
     return PSN_LK_OK;
 }
 
@@ -209,11 +238,12 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
     a.nlevels = c->nlevels;
     a.tile = (c->nlevels - 1) <= 4 ? 8 : 4;
     for (int l = 0; l < c->nlevels; l++) a.lv[l] = c->h_slots[(size_t)slot * psn::kMaxLevels + l];
-    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+    const long ti = c->tcap ? (c->n_push % c->tcap) : 0;
+    if (c->tcap) HIPCHK(c, hipEventRecord(c->ev_push[2 * ti], c->stream));
     HIPCHK(c, psn::launch_pyramid(a, c->stream));
-    if (c->timing) {
-        HIPCHK(c, hipEventRecord(c->ev[1], c->stream));
-        c->push_timed = true;
+    if (c->tcap) {
+        HIPCHK(c, hipEventRecord(c->ev_push[2 * ti + 1], c->stream));
+        c->n_push++;
     }
     c->filled[slot] = 1;
     return PSN_LK_OK;
@@ -250,7 +280,9 @@ int psn_lk_push_frame(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, 
 }
 
 // Validate and plan one query into its device descriptor.
-static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::LkQueryDev &d, int &lds, bool allow_scratch) {
+static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::LkQueryDev &d, int &lds, bool &single,
+                      bool allow_scratch) {
+    single = false;
     const psn_lk_params &p = q.params;
     const int limit = allow_scratch ? c->nslots : c->user_slots;
     if (q.prev_slot < 0 || q.prev_slot >= limit || q.next_slot < 0 || q.next_slot >= limit)
@@ -267,9 +299,12 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     int max_count = (p.term_type & PSN_LK_TERM_COUNT) ? std::min(std::max(p.max_count, 0), 100) : 30;
     double eps = (p.term_type & PSN_LK_TERM_EPS) ? std::min(std::max(p.epsilon, 0.), 10.) : 0.01;
     const int w = p.win_w, h = p.win_h;
+    const psn::LkStLayout st(w, h, (p.flags & PSN_LK_ACCUM_SCALAR) == 0, ml + 1);
     int tr = h;
     const int budget = 160 * 1024 - 1024;
-    if (psn::lk_lds_bytes(w, h, tr) > 64 * 1024) {
+    if (w * h <= 256 * psn::kStEPT && st.total <= psn::kStMaxLds) {
+        single = true;
+    } else if (psn::lk_lds_bytes(w, h, tr) > 64 * 1024) {
         while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
         if (psn::lk_lds_bytes(w, h, tr) > budget)
             return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d does not fit LDS", w, h);
@@ -287,13 +322,14 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     d.tile_rows = tr;
     d.min_eig = (float)p.min_eig_threshold;
     d.eps2 = eps * eps;
-    lds = psn::lk_lds_bytes(w, h, tr);
+    lds = single ? st.total : psn::lk_lds_bytes(w, h, tr);
     return PSN_LK_OK;
 }
 
 static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
                              uint8_t *d_status, float *d_err, bool allow_scratch) {
-    if (c->timing) HIPCHK(c, hipEventRecord(c->ev[2], c->stream));
+    const long ti = c->tcap ? (c->n_track % c->tcap) : 0;
+    if (c->tcap) HIPCHK(c, hipEventRecord(c->ev_track[2 * ti], c->stream));
     for (int base = 0; base < nq; base += psn::kMaxQueries) {
         const int n = std::min(psn::kMaxQueries, nq - base);
         psn::LkLaunchArgs a{};
@@ -302,7 +338,9 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         a.next = d_next;
         a.status = d_status;
         a.err = d_err;
+        a.stamps = c->d_stamps;
         int wgs = 0, lds = 0, maxpx = 0, nqd = 0;
+        bool all_single = true;
         for (int i = 0; i < n; i++) {
             const psn_lk_query &qq = q[base + i];
             if (qq.num_pts == 0) {
@@ -311,8 +349,10 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                 continue;
             }
             int l = 0;
-            int rc = plan_query(c, qq, wgs, a.q[nqd], l, allow_scratch);
+            bool single = false;
+            int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch);
             if (rc) return rc;
+            all_single &= single;
             wgs += qq.num_pts;
             lds = std::max(lds, l);
             maxpx = std::max(maxpx, qq.params.win_w * qq.params.win_h);
@@ -320,12 +360,30 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         }
         a.nq = nqd;
         if (nqd == 0) continue;
-        const int threads = maxpx <= 1024 ? 64 : maxpx <= 4096 ? 128 : 256;
-        HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, c->stream));
+        int threads = maxpx <= 1024 ? 64 : maxpx <= 4096 ? 128 : 256;
+        if (all_single)  // single-tile kernel: kStEPT window pixels per thread
+            threads = maxpx <= 64 * psn::kStEPT ? 64 : maxpx <= 128 * psn::kStEPT ? 128 : 256;
+        const int forced = c->force_threads;
+        if (c->force_generic) all_single = false;
+        if ((forced == 64 || forced == 128 || forced == 256) && (!all_single || forced * psn::kStEPT >= maxpx))
+            threads = forced;
+        if (!all_single) {  // the generic kernel runs every query of this launch: re-plan its LDS
+            lds = 0;
+            for (int i = 0; i < nqd; i++) {
+                psn::LkQueryDev &d = a.q[i];
+                if (d.tile_rows >= d.win_h) {
+                    int tr = d.win_h;
+                    while (tr > 1 && psn::lk_lds_bytes(d.win_w, d.win_h, tr) > 160 * 1024 - 1024) tr--;
+                    d.tile_rows = tr;
+                }
+                lds = std::max(lds, psn::lk_lds_bytes(d.win_w, d.win_h, d.tile_rows));
+            }
+        }
+        HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, all_single, c->stream));
     }
-    if (c->timing) {
-        HIPCHK(c, hipEventRecord(c->ev[3], c->stream));
-        c->track_timed = true;
+    if (c->tcap) {
+        HIPCHK(c, hipEventRecord(c->ev_track[2 * ti + 1], c->stream));
+        c->n_track++;
     }
     return PSN_LK_OK;
 }
@@ -410,6 +468,17 @@ int psn_calc_optical_flow_pyr_lk(psn_lk_ctx *c, const uint8_t *prev_img, const u
     q.num_pts = npts;
     q.params = p;
     return track_host_impl(c, &q, 1, prev_pts, next_pts, status, err, true);
+}
+
+int psn_lk_debug_set_stamps(psn_lk_ctx *c, void *d_stamps) {
+    if (!c) return PSN_LK_ERR_ARG;
+#ifdef PSN_LK_STAMPS
+    c->d_stamps = (unsigned long long *)d_stamps;
+    return PSN_LK_OK;
+#else
+    (void)d_stamps;
+    return PSN_LK_ERR_UNSUPPORTED;
+#endif
 }
 
 int psn_lk_read_level(psn_lk_ctx *c, int slot, int level, uint8_t *host, int stride) {

@@ -39,7 +39,7 @@ struct LkQueryDev {
     int max_level;        // effective (truncated) maxLevel
     int max_count;
     int flags;
-    int tile_rows;        // window rows per LDS tile
+    int tile_rows;        // window rows per LDS tile (>= win_h: single-tile kernel)
     float min_eig;
     double eps2;
 };
@@ -50,6 +50,7 @@ struct LkLaunchArgs {
     float *next;
     uint8_t *status;
     float *err;              // may be null
+    unsigned long long *stamps;  // diagnostic build only (PSN_LK_STAMPS): [wg][64] s_memtime
     int nq;
     int pad_;
     LkQueryDev q[kMaxQueries];
@@ -66,14 +67,48 @@ constexpr int kRedBytes = 256;
 __host__ __device__ inline int lk_off_tile(int w, int h) { return lk_off_red(w, h) + kRedBytes; }
 __host__ __device__ inline int lk_tile_pimg_bytes(int w, int tr) { return align16((tr + 3) * (w + 3)); }
 __host__ __device__ inline int lk_tile_dg_bytes(int w, int tr) { return align16(4 * (tr + 1) * (w + 1)); }
-__host__ __device__ inline int lk_tile_prod_bytes(int w, int tr) { return 12 * tr * w; }
+// 3 planes, each = 5 chain regions rounded up to 4 floats (16-B aligned vector reads)
+__host__ __device__ inline int lk_tile_prod_bytes(int w, int tr) { return 12 * (tr * w + 20); }
 __host__ __device__ inline int lk_lds_bytes(int w, int h, int tr) {
     return lk_off_tile(w, h) + lk_tile_pimg_bytes(w, tr) + lk_tile_dg_bytes(w, tr) + lk_tile_prod_bytes(w, tr);
 }
 
+// Single-tile kernel layout (whole window LDS-resident, double-buffered b products).
+__host__ __device__ inline int round16i(int x) { return (x + 15) & ~15; }
+__host__ __device__ inline int lk_st_planeA(int w, int h, bool sse) {
+    const int n = sse ? w / 4 : 0;
+    return 4 * round16i(h * n) + round16i(h * (w - 4 * n));
+}
+__host__ __device__ inline int lk_st_planeB(int w, int h, bool sse) {
+    const int n = sse ? w / 8 : 0;
+    return 4 * round16i(h * 2 * n) + round16i(h * (w - 8 * n));
+}
+// Single-tile kernel LDS layout. Staged u8 patches are held one pixel per
+// dword (LDS-DMA global_load_lds_ubyte writes a zero-extended dword per lane).
+struct LkStLayout {
+    int tbl, ri, jr, pim, pim_stride, dg, pa, pb, total;
+    __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev) {
+        const int wh = w * h;
+        tbl = 0;                                   // 2 pyramids x kMaxLevels x 8 ints
+        ri = tbl + 2 * kMaxLevels * 8 * 4;         // 4 x 16 ints of reduce scratch
+        jr = ri + 256;
+        pim = jr + align16(4 * lk_jreg_w(w) * lk_jreg_h(h));
+        pim_stride = align16(4 * (h + 3) * (w + 3));
+        dg = pim + nlev * pim_stride;
+        pa = dg + align16(4 * (h + 1) * (w + 1));
+        int pa_bytes = 12 * lk_st_planeA(w, h, sse);
+        const int err_bytes = 4 * round16i(wh);  // row-major |diff| plane of the err pass
+        if (pa_bytes < err_bytes) pa_bytes = err_bytes;
+        pb = pa + pa_bytes;
+        total = pb + 16 * lk_st_planeB(w, h, sse);
+    }
+};
+constexpr int kStEPT = 4;  // window pixels per thread held in registers by the single-tile kernel
+constexpr int kStMaxLds = 96 * 1024;
+
 // Launchers (psn_lk_kernels.hip).
 hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s);
-hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, hipStream_t s);
+hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, bool single_tile, hipStream_t s);
 hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
 
 }  // namespace psn

@@ -120,13 +120,16 @@ class LKContext:
         self._check(self._L.psn_lk_track_device(self._h, arr, len(queries), d_prev, d_next, d_status, d_err),
                     "track_device")
 
-    def enable_timing(self, on: bool = True):
-        self._check(self._L.psn_lk_enable_timing(self._h, int(on)), "enable_timing")
+    def enable_timing(self, capacity: int = 1024):
+        """HIP-event timing of every push (pyramid kernel) / track (LK kernel) call."""
+        self._check(self._L.psn_lk_enable_timing(self._h, int(capacity)), "enable_timing")
 
-    def last_timing(self) -> tuple[float, float]:
-        a, b = ctypes.c_float(), ctypes.c_float()
-        self._check(self._L.psn_lk_last_timing(self._h, ctypes.byref(a), ctypes.byref(b)), "last_timing")
-        return a.value, b.value
+    def timing_stats(self) -> dict:
+        np_, nt = ctypes.c_int(), ctypes.c_int()
+        pm, tm = ctypes.c_double(), ctypes.c_double()
+        self._check(self._L.psn_lk_timing_stats(self._h, ctypes.byref(np_), ctypes.byref(pm), ctypes.byref(nt),
+                                                ctypes.byref(tm)), "timing_stats")
+        return {"n_push": np_.value, "push_ms": pm.value, "n_track": nt.value, "track_ms": tm.value}
 
     def calc_optical_flow_pyr_lk(self, prev_img, next_img, prev_pts, win_size=(21, 21), max_level=3,
                                  criteria=(3, 30, 0.01), flags=0, min_eig_threshold=1e-4, next_pts=None,

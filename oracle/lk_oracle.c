@@ -22,6 +22,11 @@
 #include <omp.h>
 #endif
 
+/* Optional per-point statistics (analysis only): iterations run per level and
+ * how many b-sums / A-sums stayed within the exact-integer bound 2^24. */
+static int *g_iter_log = 0; /* [npts][8] iterations at level l */
+void oracle_set_iter_log(int *buf) { g_iter_log = buf; }
+
 #define W_BITS 14
 #define W_BITS1 14
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
@@ -308,6 +313,7 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
     float pdx = 0.f, pdy = 0.f;
 
     for (int j = 0; j < max_count; j++) {
+        if (g_iter_log) g_iter_log[i * 8 + level]++;
         int inx = cv_floor(nx), iny = cv_floor(ny);
         if (inx < -win_w || inx >= cols || iny < -win_h || iny >= rows) {
             if (level == 0) status[i] = 0;

@@ -73,6 +73,10 @@ int oracle_calc_optical_flow_pyr_lk(const uint8_t *prev_img, const uint8_t *next
                                     int flags, double min_eig_threshold, int accum_mode,
                                     int nthreads);
 
+/* Analysis hook: when set, counts LK iterations per point and level into
+ * buf[i*8 + level] (caller zeroes it). Single-threaded use only. */
+void oracle_set_iter_log(int *buf);
+
 #ifdef __cplusplus
 }
 #endif

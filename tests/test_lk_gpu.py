@@ -243,3 +243,19 @@ def test_lk_config5_4k_5level(oracle_mod):
     ref = oracle_ref(oracle_mod, f0, f1, pts, (21, 21), 4)
     gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, (21, 21), 4)
     assert_same(gpu, ref, "4k")
+
+
+@pytest.mark.parametrize("env", [{"PSN_LK_GENERIC": "1"}, {"PSN_LK_THREADS": "64"}, {"PSN_LK_THREADS": "128"},
+                                 {"PSN_LK_GENERIC": "1", "PSN_LK_THREADS": "64"}])
+@pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
+def test_lk_kernel_variants(oracle_mod, monkeypatch, env, flags):
+    """The single-tile and the tiled kernel, at every workgroup size, give the
+    same bits (both are checked against the oracle)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc, f0, f1 = scene_pair(10, 640, 480, 96)
+    pts = sc.points_at(0)
+    for win in [(21, 21), (9, 15), (32, 32)]:
+        ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
+        gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
+        assert_same(gpu, ref, f"{env} {win}")
