@@ -107,6 +107,14 @@ int psn_lk_sync(psn_lk_ctx *ctx);
 int psn_lk_push_frame(psn_lk_ctx *ctx, int slot, const uint8_t *host, int stride, int channels);
 int psn_lk_push_frame_device(psn_lk_ctx *ctx, int slot, const uint8_t *dev, int stride, int channels);
 
+/* Ingest overlap (default off). When on, psn_lk_push_frame* builds the
+ * pyramid on the context's internal ingest stream, ordered only against
+ * earlier LK launches that read the same slot; LK launches wait for the builds
+ * of the slots they read. A device source frame must then already be complete
+ * when psn_lk_push_frame_device is called (it is not ordered after the
+ * context stream). Lets frame t+1's pyramid run concurrently with frame t's LK. */
+int psn_lk_set_ingest_overlap(psn_lk_ctx *ctx, int on);
+
 /* Batched LK (replaces cv::calcOpticalFlowPyrLK at PSNWhere_Tracker2D.cpp:776-782
  * and :871-877). next_xy is written for EVERY point, including status==0 ones,
  * as OpenCV does (the backward path feeds all of them to LocalSearchKLT,

@@ -105,6 +105,7 @@ def load():
     L.psn_lk_timing_stats.argtypes = [vp, ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double)]
     L.psn_lk_debug_set_stamps.argtypes = [vp, vp]
+    L.psn_lk_set_ingest_overlap.argtypes = [vp, ip]
     L.psn_comm_get_unique_id.argtypes = [vp]
     L.psn_comm_init.argtypes = [ip, ip, ip, vp, ctypes.POINTER(vp)]
     L.psn_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]

@@ -27,6 +27,12 @@ struct psn_lk_ctx {
     int user_slots = 0, nslots = 0;  // user ring + 2 scratch slots (one-shot API)
     int nlevels = 0;                 // max_level_cap + 1
     hipStream_t own_stream = nullptr, stream = nullptr;
+    // ingest overlap: pyramid builds on their own stream, ordered against the
+    // LK launches by per-slot events (ready after a build, free after a read)
+    hipStream_t ingest_stream = nullptr;
+    bool overlap = false;
+    std::vector<hipEvent_t> slot_ready, slot_free;
+    std::vector<char> ready_rec, free_rec;
     uint8_t *d_pyr = nullptr;
     LevelDev *d_slots = nullptr;
     std::vector<LevelDev> h_slots;  // [nslots][kMaxLevels]
@@ -119,6 +125,7 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (psn::lk_kernels_init() != hipSuccess) return fail(PSN_LK_ERR_HIP);
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     c->stream = c->own_stream;
+    if (hipStreamCreateWithFlags(&c->ingest_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     // slot layout: levels back to back, rows padded to 256 B (one HBM burst / 4 x 64-B lines)
     size_t slot_bytes = 0;
     std::vector<size_t> lv_off(c->nlevels);
@@ -136,8 +143,10 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
         }
     }
     slot_bytes = (slot_bytes + 4095) & ~(size_t)4095;
-    if (hipMalloc(&c->d_pyr, slot_bytes * c->nslots) != hipSuccess) return fail(PSN_LK_ERR_NOMEM);
-    if (hipMemset(c->d_pyr, 0, slot_bytes * c->nslots) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    // +256 B slack: the LK kernel's aligned dword staging loads may read up to
+    // 3 bytes past the last row of a level
+    if (hipMalloc(&c->d_pyr, slot_bytes * c->nslots + 256) != hipSuccess) return fail(PSN_LK_ERR_NOMEM);
+    if (hipMemset(c->d_pyr, 0, slot_bytes * c->nslots + 256) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     c->h_slots.assign((size_t)c->nslots * psn::kMaxLevels, LevelDev{nullptr, 0, 0, 0, 0});
     for (int s = 0; s < c->nslots; s++)
         for (int l = 0; l < c->nlevels; l++)
@@ -146,6 +155,14 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (hipMemcpy(c->d_slots, c->h_slots.data(), sizeof(LevelDev) * c->h_slots.size(), hipMemcpyHostToDevice) != hipSuccess)
         return fail(PSN_LK_ERR_HIP);
     c->filled.assign(c->nslots, 0);
+    c->slot_ready.assign(c->nslots, nullptr);
+    c->slot_free.assign(c->nslots, nullptr);
+    c->ready_rec.assign(c->nslots, 0);
+    c->free_rec.assign(c->nslots, 0);
+    for (int i = 0; i < c->nslots; i++) {
+        if (hipEventCreateWithFlags(&c->slot_ready[i], hipEventDisableTiming) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+        if (hipEventCreateWithFlags(&c->slot_free[i], hipEventDisableTiming) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    }
     *out = c;
     return PSN_LK_OK;
 }
@@ -154,13 +171,15 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-    for (auto *v : {&c->ev_push, &c->ev_track})
+    if (c->ingest_stream) (void)hipStreamSynchronize(c->ingest_stream);
+    for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready, &c->slot_free})
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
     for (void *p : {(void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status})
         if (p) (void)hipFree(p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->ingest_stream) (void)hipStreamDestroy(c->ingest_stream);
     delete c;
 }
 
@@ -176,7 +195,15 @@ void *psn_lk_get_stream(psn_lk_ctx *c) { return c ? (void *)c->stream : nullptr;
 
 int psn_lk_sync(psn_lk_ctx *c) {
     if (!c) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PSN_LK_OK;
+}
+
+int psn_lk_set_ingest_overlap(psn_lk_ctx *c, int on) {
+    if (!c) return PSN_LK_ERR_ARG;
+    c->overlap = on != 0;
     return PSN_LK_OK;
 }
 
@@ -238,12 +265,23 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
     a.nlevels = c->nlevels;
     a.tile = (c->nlevels - 1) <= 4 ? 8 : 4;
     for (int l = 0; l < c->nlevels; l++) a.lv[l] = c->h_slots[(size_t)slot * psn::kMaxLevels + l];
+    hipStream_t s = c->stream;
+    if (c->overlap) {  // build on the ingest stream once the slot's last readers are done
+        s = c->ingest_stream;
+        if (c->free_rec[slot]) HIPCHK(c, hipStreamWaitEvent(s, c->slot_free[slot], 0));
+    }
     const long ti = c->tcap ? (c->n_push % c->tcap) : 0;
-    if (c->tcap) HIPCHK(c, hipEventRecord(c->ev_push[2 * ti], c->stream));
-    HIPCHK(c, psn::launch_pyramid(a, c->stream));
+    if (c->tcap) HIPCHK(c, hipEventRecord(c->ev_push[2 * ti], s));
+    HIPCHK(c, psn::launch_pyramid(a, s));
     if (c->tcap) {
-        HIPCHK(c, hipEventRecord(c->ev_push[2 * ti + 1], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_push[2 * ti + 1], s));
         c->n_push++;
+    }
+    if (c->overlap) {
+        HIPCHK(c, hipEventRecord(c->slot_ready[slot], s));
+        c->ready_rec[slot] = 1;
+    } else {
+        c->ready_rec[slot] = 0;
     }
     c->filled[slot] = 1;
     return PSN_LK_OK;
@@ -265,10 +303,11 @@ static int push_host_impl(psn_lk_ctx *c, int slot, const uint8_t *host, int stri
         HIPCHK(c, hipMalloc(&c->d_src, need));
         c->d_src_cap = need;
     }
-    HIPCHK(c, hipMemcpy2DAsync(c->d_src, row, host, stride, row, c->height, hipMemcpyHostToDevice, c->stream));
+    hipStream_t s = c->overlap ? c->ingest_stream : c->stream;  // the stream the build runs on
+    HIPCHK(c, hipMemcpy2DAsync(c->d_src, row, host, stride, row, c->height, hipMemcpyHostToDevice, s));
     int rc = push_device_impl(c, slot, c->d_src, (int)row, channels);
     if (rc) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // the host frame belongs to the caller after return
+    HIPCHK(c, hipStreamSynchronize(s));  // the host frame belongs to the caller after return
     return PSN_LK_OK;
 }
 
@@ -302,7 +341,7 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     const psn::LkStLayout st(w, h, (p.flags & PSN_LK_ACCUM_SCALAR) == 0, ml + 1);
     int tr = h;
     const int budget = 160 * 1024 - 1024;
-    if (w * h <= 256 * psn::kStEPT && st.total <= psn::kStMaxLds) {
+    if (w * h <= 256 * psn::kStEPTMax && st.total <= psn::kStMaxLds) {
         single = true;
     } else if (psn::lk_lds_bytes(w, h, tr) > 64 * 1024) {
         while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
@@ -328,6 +367,13 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
 
 static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
                              uint8_t *d_status, float *d_err, bool allow_scratch) {
+    // slots built on the ingest stream must be complete before the LK reads them
+    for (int i = 0; i < nq; i++)
+        for (int sl : {q[i].prev_slot, q[i].next_slot})
+            if (sl >= 0 && sl < c->nslots && c->ready_rec[sl]) {
+                HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot_ready[sl], 0));
+                c->ready_rec[sl] = 0;
+            }
     const long ti = c->tcap ? (c->n_track % c->tcap) : 0;
     if (c->tcap) HIPCHK(c, hipEventRecord(c->ev_track[2 * ti], c->stream));
     for (int base = 0; base < nq; base += psn::kMaxQueries) {
@@ -361,12 +407,15 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         a.nq = nqd;
         if (nqd == 0) continue;
         int threads = maxpx <= 1024 ? 64 : maxpx <= 4096 ? 128 : 256;
-        if (all_single)  // single-tile kernel: kStEPT window pixels per thread
-            threads = maxpx <= 64 * psn::kStEPT ? 64 : maxpx <= 128 * psn::kStEPT ? 128 : 256;
         const int forced = c->force_threads;
         if (c->force_generic) all_single = false;
-        if ((forced == 64 || forced == 128 || forced == 256) && (!all_single || forced * psn::kStEPT >= maxpx))
-            threads = forced;
+        if (forced == 64 || forced == 128 || forced == 256) threads = forced;
+        if (all_single) {  // single-tile kernel: (workgroup size, window pixels per thread)
+            int nt = maxpx <= 128 ? 64 : maxpx <= 256 ? 128 : 256;
+            if ((forced == 64 || forced == 128 || forced == 256) && forced * psn::kStEPTMax >= maxpx) nt = forced;
+            const int ept = maxpx <= 2 * nt ? 2 : 4;
+            threads = nt * 10 + ept;
+        }
         if (!all_single) {  // the generic kernel runs every query of this launch: re-plan its LDS
             lds = 0;
             for (int i = 0; i < nqd; i++) {
@@ -385,6 +434,13 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         HIPCHK(c, hipEventRecord(c->ev_track[2 * ti + 1], c->stream));
         c->n_track++;
     }
+    if (c->overlap)  // the next build into these slots waits for this launch
+        for (int i = 0; i < nq; i++)
+            for (int sl : {q[i].prev_slot, q[i].next_slot})
+                if (sl >= 0 && sl < c->nslots) {
+                    HIPCHK(c, hipEventRecord(c->slot_free[sl], c->stream));
+                    c->free_rec[sl] = 1;
+                }
     return PSN_LK_OK;
 }
 

@@ -77,11 +77,11 @@ __host__ __device__ inline int lk_lds_bytes(int w, int h, int tr) {
 __host__ __device__ inline int round16i(int x) { return (x + 15) & ~15; }
 __host__ __device__ inline int lk_st_planeA(int w, int h, bool sse) {
     const int n = sse ? w / 4 : 0;
-    return 4 * round16i(h * n) + round16i(h * (w - 4 * n));
+    return 4 * round16i(h * n) + round16i(h * (w - 4 * n) + 1);  // +1: a zero slot for idle lanes
 }
 __host__ __device__ inline int lk_st_planeB(int w, int h, bool sse) {
     const int n = sse ? w / 8 : 0;
-    return 4 * round16i(h * 2 * n) + round16i(h * (w - 8 * n));
+    return 4 * round16i(h * 2 * n) + round16i(h * (w - 8 * n) + 1);
 }
 // Single-tile kernel LDS layout. Staged u8 patches are held one pixel per
 // dword (LDS-DMA global_load_lds_ubyte writes a zero-extended dword per lane).
@@ -103,7 +103,7 @@ struct LkStLayout {
         total = pb + 16 * lk_st_planeB(w, h, sse);
     }
 };
-constexpr int kStEPT = 4;  // window pixels per thread held in registers by the single-tile kernel
+constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel
 constexpr int kStMaxLds = 96 * 1024;
 
 // Launchers (psn_lk_kernels.hip).

@@ -854,7 +854,7 @@ __device__ __forceinline__ ChainGeo chain_geo_A(int w, int h, bool sse) {
     g.lenL = h * nA;
     g.lenT = h * g.tL;
     g.S = round16i(g.lenL);
-    g.T = round16i(g.lenT);
+    g.T = round16i(g.lenT + 1);
     g.P = lk_st_planeA(w, h, sse);
     return g;
 }
@@ -866,7 +866,7 @@ __device__ __forceinline__ ChainGeo chain_geo_B(int w, int h, bool sse) {
     g.lenL = h * 2 * nB;
     g.lenT = h * g.tL;
     g.S = round16i(g.lenL);
-    g.T = round16i(g.lenT);
+    g.T = round16i(g.lenT + 1);
     g.P = lk_st_planeB(w, h, sse);
     return g;
 }
@@ -992,10 +992,80 @@ __device__ __forceinline__ LevelDev tbl_level(const int *tbl, int pyr, int level
     return L;
 }
 
+// Register-staged load of a PW x PH u8 region into LDS (one dword per pixel,
+// row stride PW): the loads are issued by load() and written by store(), so
+// the memory latency overlaps whatever the caller does in between. Interior
+// regions move aligned dwords (4 pixels per load); regions that cross the
+// image border gather single bytes through reflect-101. Up to KJ*NT elements
+// are in flight; any remainder is moved synchronously by store().
+constexpr int KJ = 8;
 template <int NT>
+struct JStage {
+    int v[KJ];
+    const uint8_t *src;
+    int pitch, lw, lh, gy0, gx0, PW, PH, ax0, ndw, n;
+    bool interior;
+    __device__ __forceinline__ void fetch(int e, int &out) const {
+        if (interior) {  // element = aligned dword d of row y
+            const int y = e / ndw, d = e - y * ndw;
+            out = *(const __attribute__((address_space(1))) int *)(src + (size_t)(gy0 + y) * pitch + ax0 + 4 * d);
+        } else {
+            const int y = e / PW, x = e - y * PW;
+            out = src[(size_t)refl101(gy0 + y, lh) * pitch + refl101(gx0 + x, lw)];
+        }
+    }
+    __device__ __forceinline__ void put(uint32_t *dst, int e, int val) const {
+        if (interior) {
+            const int y = e / ndw, d = e - y * ndw;
+            const int x0 = ax0 + 4 * d - gx0;  // region column of byte 0
+            uint32_t *row = dst + y * PW;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int x = x0 + b;
+                if (x >= 0 && x < PW) row[x] = (uint32_t)(val >> (8 * b)) & 0xff;
+            }
+        } else {
+            dst[e] = (uint32_t)val;
+        }
+    }
+    __device__ __forceinline__ void load(const LevelDev &L, int y0, int x0, int pw, int ph) {
+        src = L.p;
+        pitch = L.pitch;
+        lw = L.w;
+        lh = L.h;
+        gy0 = y0;
+        gx0 = x0;
+        PW = pw;
+        PH = ph;
+        interior = y0 >= 0 && x0 >= 0 && y0 + ph <= lh && x0 + pw <= lw;
+        ax0 = x0 & ~3;
+        ndw = (x0 - ax0 + pw + 3) >> 2;
+        n = interior ? ph * ndw : ph * pw;
+        // dword loads may read up to 3 bytes past the region's row end: they stay
+        // inside the row's 256-B padded pitch or the next row, never past the slot
+#pragma unroll
+        for (int k = 0; k < KJ; k++) {
+            const int e = threadIdx.x + k * NT;
+            if (e < n) fetch(e, v[k]);
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t *dst) const {
+#pragma unroll
+        for (int k = 0; k < KJ; k++) {
+            const int e = threadIdx.x + k * NT;
+            if (e < n) put(dst, e, v[k]);
+        }
+        for (int e = threadIdx.x + KJ * NT; e < n; e += NT) {
+            int t;
+            fetch(e, t);
+            put(dst, e, t);
+        }
+    }
+};
+
+template <int NT, int EPT>
 __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    constexpr int EPT = kStEPT;
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = blockIdx.x;
     int qi = 0;
@@ -1018,19 +1088,23 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     float *PB = (float *)(smem + lay.pb);
     const ChainGeo GA = chain_geo_A(w, h, sse), GB = chain_geo_B(w, h, sse);
 
-    // ---- per-thread window pixels (fixed for the whole kernel) ----
-    int ofsJ[EPT], ofsP[EPT], ofsD[EPT], posA_[EPT], posB_[EPT];
+    // ---- per-thread window pixels (fixed for the whole kernel). Idle lanes
+    // (pixel index >= w*h) read pixel 0, carry zero gradients and write their
+    // zero products into a pad slot of the chain planes: branch-free loops.
+    int ofsJ[EPT], ofsP[EPT], ofsD[EPT], posA_[EPT], posB_[EPT], ofsE[EPT];
     bool ev[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; k++) {
         const int idx = tid + k * NT;
         ev[k] = idx < wh;
-        const int y = idx / w, x = idx - (idx / w) * w;
+        const int i = ev[k] ? idx : 0;
+        const int y = i / w, x = i - (i / w) * w;
         ofsJ[k] = y * JRW + x;
         ofsP[k] = (y + 1) * PW + x + 1;
         ofsD[k] = y * DW + x;
-        posA_[k] = ev[k] ? posA(GA, y, x) : 0;
-        posB_[k] = ev[k] ? posB(GB, y, x) : 0;
+        posA_[k] = ev[k] ? posA(GA, y, x) : 4 * GA.S + GA.lenT;
+        posB_[k] = ev[k] ? posB(GB, y, x) : 4 * GB.S + GB.lenT;
+        ofsE[k] = ev[k] ? idx : round16i(wh);  // err plane (row-major): idle lanes write past the end
     }
 
     // ---- prologue: level table -> LDS, zero chain padding once ----
@@ -1053,7 +1127,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         NPy = A.next[2 * pi + 1];
     }
 
-    // ---- prologue DMA: the I patch of EVERY level + the coarsest J region ----
+    // ---- prologue LDS-DMA: the I patch of EVERY level + the coarsest J region ----
     for (int l = 0; l <= maxL; l++) {
         const LevelDev I = tbl_level(TBL, 0, l);
         const float sc = ldexpf(1.f, -l);
@@ -1080,18 +1154,25 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
 #ifdef PSN_LK_STAMPS
     unsigned long long acc_ph[6] = {0, 0, 0, 0, 0, 0}, t_ph = 0;
 #define PH_BEGIN() t_ph = __builtin_amdgcn_s_memtime()
-#define PH_MARK(i)                                           \
-    do {                                                     \
+#define PH_MARK(i)                                                  \
+    do {                                                            \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        acc_ph[i] += t_ - t_ph;                              \
-        t_ph = t_;                                           \
+        acc_ph[i] += t_ - t_ph;                                     \
+        t_ph = t_;                                                  \
     } while (0)
 #define PH_COUNT(i) acc_ph[i]++
 #else
-#define PH_BEGIN() do {} while (0)
-#define PH_MARK(i) do {} while (0)
-#define PH_COUNT(i) do {} while (0)
+#define PH_BEGIN() \
+    do {           \
+    } while (0)
+#define PH_MARK(i) \
+    do {           \
+    } while (0)
+#define PH_COUNT(i) \
+    do {            \
+    } while (0)
 #endif
+    JStage<NT> js;
 
     for (int level = maxL; level >= 0; level--) {
         LK_STAMP(level * 10 + 0);
@@ -1129,10 +1210,11 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         bilin_weights(__fsub_rn(px, (float)ipx), __fsub_rn(py, (float)ipy), iw00, iw01, iw10, iw11);
         nx = __fsub_rn(nx, hwx);
         ny = __fsub_rn(ny, hwy);
-        if (level < maxL) {  // J region of this level, in flight during the A-phase
+        const bool new_jr = level < maxL;
+        if (new_jr) {  // J region of this level: loads in flight during the A-phase
             jr_x0 = cv_floor(nx) - kJMargin;
             jr_y0 = cv_floor(ny) - kJMargin;
-            dma_region<NT>(JR, J, jr_y0, jr_x0, JRW, JRH);
+            js.load(J, jr_y0, jr_x0, JRW, JRH);
         }
         LK_STAMP(level * 10 + 1);
 
@@ -1162,25 +1244,24 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         unsigned aA = 0;  // saturating sum of |every A term|
 #pragma unroll
         for (int k = 0; k < EPT; k++) {
-            Iw_[k] = Ix_[k] = Iy_[k] = 0;
-            if (ev[k]) {
-                const uint32_t *p = P + ofsP[k];
-                Iw_[k] = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[PW] * iw10 + (int)p[PW + 1] * iw11, 9);
-                const short2 *d = Dg + ofsD[k];
-                const short2 d00 = d[0], d01 = d[1], d10 = d[DW], d11 = d[DW + 1];
-                Ix_[k] = PSN_DESCALE(d00.x * iw00 + d01.x * iw01 + d10.x * iw10 + d11.x * iw11, 14);
-                Iy_[k] = PSN_DESCALE(d00.y * iw00 + d01.y * iw01 + d10.y * iw10 + d11.y * iw11, 14);
-                const int xx2 = Ix_[k] * Ix_[k], xy = Ix_[k] * Iy_[k], yy2 = Iy_[k] * Iy_[k];
-                PA[posA_[k]] = (float)xx2;
-                PA[GA.P + posA_[k]] = (float)xy;
-                PA[2 * GA.P + posA_[k]] = (float)yy2;
-                sA11 += xx2;
-                sA12 += xy;
-                sA22 += yy2;
-                aA = sat_add(aA, sat_add(sat_add((unsigned)xx2, (unsigned)abs(xy)), (unsigned)yy2));
-            }
+            const uint32_t *p = P + ofsP[k];
+            Iw_[k] = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[PW] * iw10 + (int)p[PW + 1] * iw11, 9);
+            const short2 *d = Dg + ofsD[k];
+            const short2 d00 = d[0], d01 = d[1], d10 = d[DW], d11 = d[DW + 1];
+            const int ix = PSN_DESCALE(d00.x * iw00 + d01.x * iw01 + d10.x * iw10 + d11.x * iw11, 14);
+            const int iy = PSN_DESCALE(d00.y * iw00 + d01.y * iw01 + d10.y * iw10 + d11.y * iw11, 14);
+            Ix_[k] = ev[k] ? ix : 0;
+            Iy_[k] = ev[k] ? iy : 0;
+            const int xx2 = Ix_[k] * Ix_[k], xy = Ix_[k] * Iy_[k], yy2 = Iy_[k] * Iy_[k];
+            PA[posA_[k]] = (float)xx2;
+            PA[GA.P + posA_[k]] = (float)xy;
+            PA[2 * GA.P + posA_[k]] = (float)yy2;
+            sA11 += xx2;
+            sA12 += xy;
+            sA22 += yy2;
+            aA = sat_add(aA, sat_add(sat_add((unsigned)xx2, (unsigned)abs(xy)), (unsigned)yy2));
         }
-        dma_wait();  // this wave's J-region DMA (published by the barrier below)
+        if (new_jr) js.store(JR);  // published by the barrier below
         LK_STAMP(level * 10 + 3);
         block_sums4<NT>(sA11, sA12, sA22, aA, RI + 32);
         LK_STAMP(level * 10 + 4);
@@ -1248,8 +1329,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 // barrier, which this wave has passed
                 jr_x0 = inx - kJMargin;
                 jr_y0 = iny - kJMargin;
-                dma_region<NT>(JR, J, jr_y0, jr_x0, JRW, JRH);
-                dma_wait();
+                js.load(J, jr_y0, jr_x0, JRW, JRH);
+                js.store(JR);
                 __syncthreads();
                 PH_COUNT(5);
             }
@@ -1259,17 +1340,15 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             unsigned a = 0;
 #pragma unroll
             for (int k = 0; k < EPT; k++) {
-                if (ev[k]) {
-                    const uint32_t *p = jb + ofsJ[k];
-                    const int jv = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[JRW] * iw10 + (int)p[JRW + 1] * iw11, 9);
-                    const int diff = jv - Iw_[k];
-                    const int t1 = diff * Ix_[k], t2 = diff * Iy_[k];
-                    pb[posB_[k]] = (float)t1;
-                    pb[GB.P + posB_[k]] = (float)t2;
-                    s1 += t1;
-                    s2 += t2;
-                    a = sat_add(a, sat_add((unsigned)abs(t1), (unsigned)abs(t2)));
-                }
+                const uint32_t *p = jb + ofsJ[k];
+                const int jv = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[JRW] * iw10 + (int)p[JRW + 1] * iw11, 9);
+                const int diff = jv - Iw_[k];
+                const int t1 = diff * Ix_[k], t2 = diff * Iy_[k];
+                pb[posB_[k]] = (float)t1;
+                pb[GB.P + posB_[k]] = (float)t2;
+                s1 += t1;
+                s2 += t2;
+                a = sat_add(a, sat_add((unsigned)abs(t1), (unsigned)abs(t2)));
             }
             PH_MARK(0);
             block_sums3<NT>(s1, s2, a, RI + 16 * (j & 1));  // the iteration's barrier
@@ -1335,8 +1414,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             if (!(iqx >= jr_x0 && iqy >= jr_y0 && iqx + w + 1 <= jr_x0 + JRW && iqy + h + 1 <= jr_y0 + JRH)) {
                 jr_x0 = iqx - kJMargin;
                 jr_y0 = iqy - kJMargin;
-                dma_region<NT>(JR, J, jr_y0, jr_x0, JRW, JRH);
-                dma_wait();
+                js.load(J, jr_y0, jr_x0, JRW, JRH);
+                js.store(JR);
                 __syncthreads();
             }
             const uint32_t *jb = JR + (iqy - jr_y0) * JRW + (iqx - jr_x0);
@@ -1344,13 +1423,11 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             unsigned ea = 0;
 #pragma unroll
             for (int k = 0; k < EPT; k++) {
-                if (ev[k]) {
-                    const uint32_t *p = jb + ofsJ[k];
-                    const int jv = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[JRW] * iw10 + (int)p[JRW + 1] * iw11, 9);
-                    const int ad = abs(jv - Iw_[k]);
-                    PA[tid + k * NT] = (float)ad;  // row-major, for the sequential fallback
-                    ea = sat_add(ea, (unsigned)ad);
-                }
+                const uint32_t *p = jb + ofsJ[k];
+                const int jv = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[JRW] * iw10 + (int)p[JRW + 1] * iw11, 9);
+                const int ad = ev[k] ? abs(jv - Iw_[k]) : 0;
+                PA[ofsE[k]] = (float)ad;  // row-major, for the sequential fallback
+                ea = sat_add(ea, (unsigned)ad);
             }
             for (int k = wh + tid; k < round16i(wh); k += NT) PA[k] = 0.f;
             block_sums3<NT>(e1, e2, ea, RI + 48);
@@ -1377,15 +1454,22 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         if (A.err) A.err[pi] = errv;
     }
 }
+#undef PH_BEGIN
+#undef PH_MARK
+#undef PH_COUNT
 
 hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, bool single_tile, hipStream_t s) {
     if (total_wgs <= 0) return hipSuccess;
     const dim3 grid(total_wgs);
     if (single_tile) {
+        // threads encodes (workgroup size, pixels per thread): NT * 10 + EPT
         switch (threads) {
-            case 64: hipLaunchKernelGGL(lk_kernel_st<64>, grid, dim3(64), lds_bytes, s, a); break;
-            case 128: hipLaunchKernelGGL(lk_kernel_st<128>, grid, dim3(128), lds_bytes, s, a); break;
-            default: hipLaunchKernelGGL(lk_kernel_st<256>, grid, dim3(256), lds_bytes, s, a); break;
+            case 642: hipLaunchKernelGGL((lk_kernel_st<64, 2>), grid, dim3(64), lds_bytes, s, a); break;
+            case 644: hipLaunchKernelGGL((lk_kernel_st<64, 4>), grid, dim3(64), lds_bytes, s, a); break;
+            case 1282: hipLaunchKernelGGL((lk_kernel_st<128, 2>), grid, dim3(128), lds_bytes, s, a); break;
+            case 1284: hipLaunchKernelGGL((lk_kernel_st<128, 4>), grid, dim3(128), lds_bytes, s, a); break;
+            case 2562: hipLaunchKernelGGL((lk_kernel_st<256, 2>), grid, dim3(256), lds_bytes, s, a); break;
+            default: hipLaunchKernelGGL((lk_kernel_st<256, 4>), grid, dim3(256), lds_bytes, s, a); break;
         }
     } else {
         switch (threads) {
@@ -1403,9 +1487,11 @@ hipError_t lk_kernels_init() {
     if ((e = hipFuncSetAttribute((const void *)lk_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)lk_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)lk_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
-    if ((e = hipFuncSetAttribute((const void *)lk_kernel_st<64>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
-    if ((e = hipFuncSetAttribute((const void *)lk_kernel_st<128>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
-    if ((e = hipFuncSetAttribute((const void *)lk_kernel_st<256>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
+    const void *st[] = {(const void *)lk_kernel_st<64, 2>,  (const void *)lk_kernel_st<64, 4>,
+                        (const void *)lk_kernel_st<128, 2>, (const void *)lk_kernel_st<128, 4>,
+                        (const void *)lk_kernel_st<256, 2>, (const void *)lk_kernel_st<256, 4>};
+    for (const void *f : st)
+        if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)pyramid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     return hipSuccess;
 }

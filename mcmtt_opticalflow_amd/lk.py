@@ -82,6 +82,10 @@ class LKContext:
     def set_stream(self, stream_ptr: int | None):
         self._check(self._L.psn_lk_set_stream(self._h, stream_ptr), "set_stream")
 
+    def set_ingest_overlap(self, on: bool = True):
+        """Build pyramids on the internal ingest stream (overlapping earlier LK work)."""
+        self._check(self._L.psn_lk_set_ingest_overlap(self._h, int(on)), "set_ingest_overlap")
+
     def sync(self):
         self._check(self._L.psn_lk_sync(self._h), "sync")
 

@@ -1,0 +1,77 @@
+"""N>1 path on CPU: camera-per-rank tracklet slots all-gathered with gloo
+(world_size 2), ordered by rank == camera index as Associator3D requires
+(psn_where/PSNWhere_Associator3D.cpp:1105-1116), and the bench's
+max-over-ranks timing reduction."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, npts, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mcmtt_opticalflow_amd import dist as pdist
+
+        slot = torch.zeros(pdist.slot_bytes(npts), dtype=torch.uint8)
+        hdr, nxt, err, st = pdist.slot_views(slot, npts)
+        hdr.copy_(torch.tensor([rank, 7, npts, 0], dtype=torch.int32))
+        nxt.copy_(torch.arange(2 * npts, dtype=torch.float32).view(npts, 2) + 1000 * rank)
+        err.fill_(0.5 * rank)
+        st.copy_(torch.tensor([(i + rank) % 2 for i in range(npts)], dtype=torch.uint8))
+        gathered = pdist.allgather_slots(slot, world)
+        t = pdist.max_over_ranks(0.1 * (rank + 1))
+        rows = []
+        for r in range(world):
+            h, n, e, s = pdist.slot_views(gathered[r].contiguous(), npts)
+            rows.append((h.tolist(), n.numpy().copy(), e.numpy().copy(), s.numpy().copy()))
+        q.put((rank, rows, t))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allgather_slots_gloo_world2():
+    world, npts = 2, 37
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, npts, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, rows, t in results:
+        assert t == pytest.approx(0.2)
+        for cam, (h, n, e, s) in enumerate(rows):
+            assert h == [cam, 7, npts, 0]  # row index == camera index
+            np.testing.assert_array_equal(n, np.arange(2 * npts, dtype=np.float32).reshape(npts, 2) + 1000 * cam)
+            assert np.all(e == 0.5 * cam)
+            assert s.tolist() == [(i + cam) % 2 for i in range(npts)]
+
+
+def test_slot_layout_alignment():
+    from mcmtt_opticalflow_amd import dist as pdist
+
+    for n in (1, 3, 512, 2048, 4096):
+        b = pdist.slot_bytes(n)
+        assert b % 64 == 0 and b >= 16 + 13 * n
+        slot = torch.zeros(b, dtype=torch.uint8)
+        hdr, nxt, err, st = pdist.slot_views(slot, n)
+        assert nxt.shape == (n, 2) and err.shape == (n,) and st.shape == (n,)

@@ -200,13 +200,16 @@ def test_lk_batched_queries_ring(oracle_mod):
         assert_same((gn[first:first + n], gs[first:first + n], ge[first:first + n]), ref, f"query {win}")
 
 
-def test_lk_propagation_sequence(oracle_mod):
-    """Tracklet propagation: frame t's outputs are frame t+1's inputs."""
+@pytest.mark.parametrize("overlap", [False, True])
+def test_lk_propagation_sequence(oracle_mod, overlap):
+    """Tracklet propagation: frame t's outputs are frame t+1's inputs (with and
+    without the ingest stream overlapping pyramid builds with LK)."""
     sc = synth.make_scene(8, 640, 480, 128)
     frames = [sc.frame(t) for t in range(6)]
     p_ref = sc.points_at(0)
     p_gpu = p_ref.copy()
     with glk.LKContext(640, 480, ring_slots=2, max_level_cap=3) as ctx:
+        ctx.set_ingest_overlap(overlap)
         ctx.push_frame(0, frames[0])
         for t in range(1, 6):
             ctx.push_frame(t % 2, frames[t])
@@ -217,7 +220,8 @@ def test_lk_propagation_sequence(oracle_mod):
             p_gpu, p_ref = g[0], r[0]
 
 
-def test_lk_device_pointer_path(oracle_mod):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_lk_device_pointer_path(oracle_mod, overlap):
     import hiprt
 
     sc, f0, f1 = scene_pair(9, 640, 480, 200)
@@ -227,6 +231,7 @@ def test_lk_device_pointer_path(oracle_mod):
     d_p = hiprt.DeviceBuffer.from_array(pts)
     d_n, d_s, d_e = hiprt.DeviceBuffer(pts.nbytes), hiprt.DeviceBuffer(len(pts)), hiprt.DeviceBuffer(4 * len(pts))
     with glk.LKContext(640, 480, ring_slots=2, max_level_cap=3) as ctx:
+        ctx.set_ingest_overlap(overlap)
         ctx.push_frame_device(0, d_f0.addr, 640, 1)
         ctx.push_frame_device(1, d_f1.addr, 640, 1)
         q = glk.make_query(0, 1, 0, len(pts), glk.make_params((21, 21), 3))
