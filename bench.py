@@ -28,7 +28,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Tracker2D frames/sec (all cameras) + achieved HBM GB/s fraction, 1/2/4/8 GPU"
-HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBPS = 8000.0
+TIMING_EVERY = 8  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
 def level_sizes(w, h, nlev):
@@ -105,7 +106,9 @@ def main():
     ap.add_argument("--period", type=int, default=10)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true", help="build pyramids on the LK stream (serial)")
+    ap.add_argument("--overlap", choices=["off", "stream", "fused"], default="fused",
+                    help="ingest of frame t+1: serial on the LK stream, on a second stream, or fused "
+                         "into the tail of frame t's LK launch (default)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"),
                     help="rocprofv3 FETCH/WRITE_SIZE summary (tools/profile_round.sh) for roofline.traffic")
     args = ap.parse_args()
@@ -134,9 +137,10 @@ def main():
     torch.cuda.set_stream(stream)
     ctx = lk.LKContext(W, H, ring_slots=R, max_level_cap=L - 1, device=local_rank)
     ctx.set_stream(stream.cuda_stream)
-    # frame t+1's pyramid (internal ingest stream) overlaps frame t's LK; the
-    # frames are resident and complete before timing starts
-    ctx.set_ingest_overlap(not args.no_overlap)
+    # frame t+1's pyramid overlaps frame t's LK (fused: built by the LK launch's
+    # tail workgroups); the frames are resident and complete before timing starts
+    mode = {"off": 0, "stream": 1, "fused": 2}[args.overlap]
+    ctx.set_ingest_overlap(mode)
 
     sb = pdist.slot_bytes(N)
     slots = [torch.zeros(sb, dtype=torch.uint8, device=device) for _ in range(2)]
@@ -147,12 +151,18 @@ def main():
     gathered = torch.empty((world, sb), dtype=torch.uint8, device=device)
     params = lk.make_params((win, win), L - 1)
     ctx.push_frame_device(0, frames[0].data_ptr(), W, 1)
+    if mode == 2:
+        ctx.push_frame_device(1, frames[ping_pong(1, args.period)].data_ptr(), W, 1)
+        ctx.sync()
+    queries = [lk.make_query((t - 1) % R, t % R, 0, N, params) for t in range(R)]
 
     def step(t):
         cur, prv = views[t % 2], views[(t - 1) % 2]
-        f = frames[ping_pong(t, args.period)]
-        ctx.push_frame_device(t % R, f.data_ptr(), W, 1)
-        q = lk.make_query((t - 1) % R, t % R, 0, N, params)
+        if mode == 2:  # ingest frame t+1 (deferred into this step's LK launch)
+            ctx.push_frame_device((t + 1) % R, frames[ping_pong(t + 1, args.period)].data_ptr(), W, 1)
+        else:  # ingest frame t
+            ctx.push_frame_device(t % R, frames[ping_pong(t, args.period)].data_ptr(), W, 1)
+        q = queries[t % R]
         ctx.track_device([q], prv[1].data_ptr(), cur[1].data_ptr(), cur[3].data_ptr(), cur[2].data_ptr())
         cur[0][1].fill_(t)
         if world > 1:
@@ -162,7 +172,9 @@ def main():
     for _ in range(args.warmup):
         step(t)
         t += 1
-    ctx.enable_timing(args.steps + 1)  # syncs the stream
+    # HIP events around every TIMING_EVERY-th LK launch (an event pair costs GPU
+    # time, so sampling keeps it from slowing the measured loop)
+    ctx.enable_timing(args.steps + 1, TIMING_EVERY)  # syncs the stream
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
@@ -179,19 +191,24 @@ def main():
     tracked = int(views[(t - 1) % 2][3].sum().item())
 
     pyr_bytes, lk_bytes = algorithmic_bytes(W, H, L, N)
-    pyr_us = 1e3 * ts["push_ms"] / max(ts["n_push"], 1)
+    pyr_us = 1e3 * ts["push_ms"] / max(ts["n_push"], 1) if ts["n_push"] else None
     lk_us = 1e3 * ts["track_ms"] / max(ts["n_track"], 1)
     fps_all = world * args.steps / elapsed
     per_gpu_fps = args.steps / elapsed
     frame_bytes = pyr_bytes + lk_bytes
 
     if rank == 0:
-        dom = ("lk_kernel", lk_bytes, lk_us) if lk_us >= pyr_us else ("pyramid_kernel", pyr_bytes, pyr_us)
+        if mode == 2:  # one launch per frame: LK of frame t + pyramid of frame t+1
+            dom = ("lk_kernel_st+fused_pyramid", lk_bytes + pyr_bytes, lk_us)
+        elif pyr_us is None or lk_us >= pyr_us:
+            dom = ("lk_kernel", lk_bytes, lk_us)
+        else:
+            dom = ("pyramid_kernel", pyr_bytes, pyr_us)
         achieved = dom[1] / (dom[2] * 1e-6) / 1e9
         traffic, traffic_src = None, None
         if args.pmc_summary and os.path.exists(args.pmc_summary):
             ks = json.load(open(args.pmc_summary)).get("kernels", {})
-            key = "lk_kernel_st" if dom[0] == "lk_kernel" and "lk_kernel_st" in ks else dom[0]
+            key = "lk_kernel_st" if dom[0].startswith("lk_kernel") and "lk_kernel_st" in ks else dom[0]
             if key in ks:
                 traffic = ks[key]["hbm_bytes_per_launch"]
                 traffic_src = os.path.relpath(args.pmc_summary, ROOT)
@@ -221,7 +238,9 @@ def main():
                 "traffic_source": traffic_src,
                 "bytes_per_launch": dom[1], "avg_launch_us": round(dom[2], 3),
             },
-            "kernels_us": {"pyramid_kernel": round(pyr_us, 3), "lk_kernel": round(lk_us, 3)},
+            "kernels_us": {"pyramid_kernel": None if pyr_us is None else round(pyr_us, 3),
+                           "lk_kernel": round(lk_us, 3)},
+            "ingest_overlap": args.overlap,
             "frame_level": {
                 "algorithmic_bytes_per_camera_frame": frame_bytes,
                 "achieved_GBps_per_gpu": round(frame_bytes * per_gpu_fps / 1e9, 2),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PSN_LK_ABI_VERSION 1
+#define PSN_LK_ABI_VERSION 2
 
 #define PSN_LK_OK 0
 #define PSN_LK_ERR_ARG (-1)
@@ -107,13 +107,24 @@ int psn_lk_sync(psn_lk_ctx *ctx);
 int psn_lk_push_frame(psn_lk_ctx *ctx, int slot, const uint8_t *host, int stride, int channels);
 int psn_lk_push_frame_device(psn_lk_ctx *ctx, int slot, const uint8_t *dev, int stride, int channels);
 
-/* Ingest overlap (default off). When on, psn_lk_push_frame* builds the
- * pyramid on the context's internal ingest stream, ordered only against
- * earlier LK launches that read the same slot; LK launches wait for the builds
- * of the slots they read. A device source frame must then already be complete
- * when psn_lk_push_frame_device is called (it is not ordered after the
- * context stream). Lets frame t+1's pyramid run concurrently with frame t's LK. */
-int psn_lk_set_ingest_overlap(psn_lk_ctx *ctx, int on);
+/* Ingest overlap modes (default OFF: builds run on the context stream).
+ * STREAM: psn_lk_push_frame* builds the pyramid on the context's internal
+ *   ingest stream, ordered only against earlier LK launches that read the same
+ *   slot; LK launches wait for the builds of the slots they read. A device
+ *   source frame must already be complete when psn_lk_push_frame_device is
+ *   called (it is not ordered after the context stream).
+ * FUSED: psn_lk_push_frame_device defers the build; the next psn_lk_track*
+ *   launch that does not read that slot runs it in its own tail (workgroups
+ *   whose point has converged pull pyramid tiles), so frame t+1's ingest costs
+ *   no extra launch and no cross-stream wait. Any other call (a track reading
+ *   the slot, another push, read_level, sync, set_stream, destroy) runs a
+ *   pending build first as its own launch. The device source frame must stay
+ *   valid until then. Host-frame pushes are never deferred.
+ * Results are identical in every mode. */
+#define PSN_LK_OVERLAP_OFF 0
+#define PSN_LK_OVERLAP_STREAM 1
+#define PSN_LK_OVERLAP_FUSED 2
+int psn_lk_set_ingest_overlap(psn_lk_ctx *ctx, int mode);
 
 /* Batched LK (replaces cv::calcOpticalFlowPyrLK at PSNWhere_Tracker2D.cpp:776-782
  * and :871-877). next_xy is written for EVERY point, including status==0 ones,
@@ -137,11 +148,14 @@ int psn_lk_read_level(psn_lk_ctx *ctx, int slot, int level, uint8_t *host, int s
 int psn_lk_level_size(psn_lk_ctx *ctx, int level, int *w, int *h);
 
 /* Device-side kernel timing with HIP events recorded on the context stream
- * around every psn_lk_push_frame* (pyramid kernel) and psn_lk_track* (LK
- * kernel) call. `capacity` = calls of each kind kept in an event ring
- * (0 disables). psn_lk_timing_stats waits for the recorded events, returns
- * the number of timed calls and their summed milliseconds, and resets. */
-int psn_lk_enable_timing(psn_lk_ctx *ctx, int capacity);
+ * around every `every`-th psn_lk_push_frame* build launch (pyramid kernel)
+ * and psn_lk_track* call (LK launch, including a fused build). `capacity` =
+ * timed calls of each kind kept in an event ring (0 disables); every >= 1
+ * (each event pair costs a few microseconds of GPU time, so sampling keeps
+ * the measurement from slowing the measured loop). psn_lk_timing_stats waits
+ * for the recorded events, returns the number of timed calls and their summed
+ * milliseconds, and resets. */
+int psn_lk_enable_timing(psn_lk_ctx *ctx, int capacity, int every);
 int psn_lk_timing_stats(psn_lk_ctx *ctx, int *n_push, double *push_ms, int *n_track, double *track_ms);
 
 /* Diagnostic builds only (libpsn_lk_stamps.so, -DPSN_LK_STAMPS): record

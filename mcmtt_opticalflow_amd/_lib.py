@@ -28,6 +28,7 @@ ERRORS = {
 USE_INITIAL_FLOW = 4
 GET_MIN_EIGENVALS = 8
 ACCUM_SCALAR = 0x100
+OVERLAP_OFF, OVERLAP_STREAM, OVERLAP_FUSED = 0, 1, 2  # psn_lk_set_ingest_overlap modes
 TERM_COUNT = 1
 TERM_EPS = 2
 MAX_WIN_PIXELS = 16384
@@ -101,7 +102,7 @@ def load():
     L.psn_calc_optical_flow_pyr_lk.argtypes = [vp, u8p, u8p, ip, fp, fp, u8p, fp, ip, ctypes.POINTER(LkParams)]
     L.psn_lk_read_level.argtypes = [vp, ip, ip, u8p, ip]
     L.psn_lk_level_size.argtypes = [vp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]
-    L.psn_lk_enable_timing.argtypes = [vp, ip]
+    L.psn_lk_enable_timing.argtypes = [vp, ip, ip]
     L.psn_lk_timing_stats.argtypes = [vp, ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double)]
     L.psn_lk_debug_set_stamps.argtypes = [vp, vp]

@@ -30,7 +30,13 @@ struct psn_lk_ctx {
     // ingest overlap: pyramid builds on their own stream, ordered against the
     // LK launches by per-slot events (ready after a build, free after a read)
     hipStream_t ingest_stream = nullptr;
-    bool overlap = false;
+    int overlap = PSN_LK_OVERLAP_OFF;
+    // PSN_LK_OVERLAP_FUSED: the last pushed build is deferred and run inside
+    // the next LK launch that does not read its slot (tail workgroups)
+    bool pend = false;
+    int pend_slot = -1;
+    psn::PyrBuildArgs pend_args{};
+    unsigned *d_ctr = nullptr;  // [2] fused-build work counter + finished workgroups
     std::vector<hipEvent_t> slot_ready, slot_free;
     std::vector<char> ready_rec, free_rec;
     uint8_t *d_pyr = nullptr;
@@ -51,9 +57,21 @@ struct psn_lk_ctx {
     // timing: event ring, 2 events per timed call
     int tcap = 0;
     std::vector<hipEvent_t> ev_push, ev_track;
-    long n_push = 0, n_track = 0;
+    long n_push = 0, n_track = 0;          // timed calls
+    long calls_push = 0, calls_track = 0;  // all calls since enable_timing
+    int every = 1;                         // time every `every`-th call of each kind
     std::string err;
 };
+
+static int set_err(psn_lk_ctx *c, int code, const char *fmt, ...);
+static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s);
+
+// Run a deferred (fused-mode) build now, as its own launch on the LK stream.
+static int flush_pending(psn_lk_ctx *c) {
+    if (!c->pend) return PSN_LK_OK;
+    c->pend = false;
+    return launch_build(c, c->pend_args, c->stream);
+}
 
 static int set_err(psn_lk_ctx *c, int code, const char *fmt, ...) {
     if (c) {
@@ -123,6 +141,8 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     };
     if (hipSetDevice(device) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     if (psn::lk_kernels_init() != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    if (hipMalloc(&c->d_ctr, 2 * sizeof(unsigned)) != hipSuccess) return fail(PSN_LK_ERR_NOMEM);
+    if (hipMemset(c->d_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     c->stream = c->own_stream;
     if (hipStreamCreateWithFlags(&c->ingest_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
@@ -159,9 +179,11 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     c->slot_free.assign(c->nslots, nullptr);
     c->ready_rec.assign(c->nslots, 0);
     c->free_rec.assign(c->nslots, 0);
+    // slot events only order two streams of one device: a device-scope release suffices
+    const unsigned evf = hipEventDisableTiming | hipEventReleaseToDevice;
     for (int i = 0; i < c->nslots; i++) {
-        if (hipEventCreateWithFlags(&c->slot_ready[i], hipEventDisableTiming) != hipSuccess) return fail(PSN_LK_ERR_HIP);
-        if (hipEventCreateWithFlags(&c->slot_free[i], hipEventDisableTiming) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+        if (hipEventCreateWithFlags(&c->slot_ready[i], evf) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+        if (hipEventCreateWithFlags(&c->slot_free[i], evf) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     }
     *out = c;
     return PSN_LK_OK;
@@ -170,12 +192,14 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
 void psn_lk_destroy(psn_lk_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->pend && c->stream) (void)flush_pending(c);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->ingest_stream) (void)hipStreamSynchronize(c->ingest_stream);
     for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready, &c->slot_free})
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
-    for (void *p : {(void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
+    for (void *p : {(void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status})
         if (p) (void)hipFree(p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -187,6 +211,9 @@ const char *psn_lk_last_error(psn_lk_ctx *c) { return c ? c->err.c_str() : "null
 
 int psn_lk_set_stream(psn_lk_ctx *c, void *s) {
     if (!c) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = flush_pending(c);  // a deferred build belongs to the old stream's order
+    if (rc) return rc;
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return PSN_LK_OK;
 }
@@ -196,29 +223,40 @@ void *psn_lk_get_stream(psn_lk_ctx *c) { return c ? (void *)c->stream : nullptr;
 int psn_lk_sync(psn_lk_ctx *c) {
     if (!c) return PSN_LK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    int rc = flush_pending(c);
+    if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PSN_LK_OK;
 }
 
-int psn_lk_set_ingest_overlap(psn_lk_ctx *c, int on) {
-    if (!c) return PSN_LK_ERR_ARG;
-    c->overlap = on != 0;
+int psn_lk_set_ingest_overlap(psn_lk_ctx *c, int mode) {
+    if (!c || mode < PSN_LK_OVERLAP_OFF || mode > PSN_LK_OVERLAP_FUSED) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = flush_pending(c);
+    if (rc) return rc;
+    c->overlap = mode;
     return PSN_LK_OK;
 }
 
-int psn_lk_enable_timing(psn_lk_ctx *c, int capacity) {
-    if (!c || capacity < 0) return PSN_LK_ERR_ARG;
+int psn_lk_enable_timing(psn_lk_ctx *c, int capacity, int every) {
+    if (!c || capacity < 0 || every < 1) return PSN_LK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    int rc = flush_pending(c);
+    if (rc) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (auto *v : {&c->ev_push, &c->ev_track}) {
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
         v->assign(2 * (size_t)capacity, nullptr);
-        for (auto &e : *v) HIPCHK(c, hipEventCreate(&e));
+        // timing-only events: no system-scope fence (cache writeback/invalidate) per record
+        for (auto &e : *v) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     }
     c->tcap = capacity;
+    c->every = every;
     c->n_push = c->n_track = 0;
+    c->calls_push = c->calls_track = 0;
     return PSN_LK_OK;
 }
 
@@ -247,6 +285,7 @@ int psn_lk_timing_stats(psn_lk_ctx *c, int *n_push, double *push_ms, int *n_trac
     if (push_ms) *push_ms = pm;
     if (track_ms) *track_ms = tm;
     c->n_push = c->n_track = 0;
+    c->calls_push = c->calls_track = 0;
     return PSN_LK_OK;
 }
 
@@ -257,7 +296,31 @@ int psn_lk_level_size(psn_lk_ctx *c, int level, int *w, int *h) {
     return PSN_LK_OK;
 }
 
+// One standalone pyramid launch on stream s (timed when timing is enabled).
+static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s) {
+    const bool timed = c->tcap && (c->calls_push++ % c->every) == 0;
+    const long ti = timed ? (c->n_push % c->tcap) : 0;
+    if (timed) HIPCHK(c, hipEventRecord(c->ev_push[2 * ti], s));
+    HIPCHK(c, psn::launch_pyramid(a, s));
+    if (timed) {
+        HIPCHK(c, hipEventRecord(c->ev_push[2 * ti + 1], s));
+        c->n_push++;
+    }
+    return PSN_LK_OK;
+}
+
+// Make the LK stream wait for a build of `slot` running on the ingest stream.
+static int wait_slot_ready(psn_lk_ctx *c, int slot) {
+    if (slot >= 0 && slot < c->nslots && c->ready_rec[slot]) {
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot_ready[slot], 0));
+        c->ready_rec[slot] = 0;
+    }
+    return PSN_LK_OK;
+}
+
 static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
+    int rc = flush_pending(c);  // at most one deferred build
+    if (rc) return rc;
     psn::PyrBuildArgs a{};
     a.src = dev;
     a.src_stride = stride;
@@ -265,25 +328,27 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
     a.nlevels = c->nlevels;
     a.tile = (c->nlevels - 1) <= 4 ? 8 : 4;
     for (int l = 0; l < c->nlevels; l++) a.lv[l] = c->h_slots[(size_t)slot * psn::kMaxLevels + l];
+    c->filled[slot] = 1;
+    if (c->overlap == PSN_LK_OVERLAP_FUSED && c->nlevels > 1) {
+        c->ready_rec[slot] = 0;
+        c->pend = true;
+        c->pend_slot = slot;
+        c->pend_args = a;
+        return PSN_LK_OK;
+    }
     hipStream_t s = c->stream;
-    if (c->overlap) {  // build on the ingest stream once the slot's last readers are done
+    if (c->overlap == PSN_LK_OVERLAP_STREAM) {  // build on the ingest stream once the slot's last readers are done
         s = c->ingest_stream;
         if (c->free_rec[slot]) HIPCHK(c, hipStreamWaitEvent(s, c->slot_free[slot], 0));
     }
-    const long ti = c->tcap ? (c->n_push % c->tcap) : 0;
-    if (c->tcap) HIPCHK(c, hipEventRecord(c->ev_push[2 * ti], s));
-    HIPCHK(c, psn::launch_pyramid(a, s));
-    if (c->tcap) {
-        HIPCHK(c, hipEventRecord(c->ev_push[2 * ti + 1], s));
-        c->n_push++;
-    }
-    if (c->overlap) {
+    rc = launch_build(c, a, s);
+    if (rc) return rc;
+    if (c->overlap == PSN_LK_OVERLAP_STREAM) {
         HIPCHK(c, hipEventRecord(c->slot_ready[slot], s));
         c->ready_rec[slot] = 1;
     } else {
         c->ready_rec[slot] = 0;
     }
-    c->filled[slot] = 1;
     return PSN_LK_OK;
 }
 
@@ -296,6 +361,8 @@ int psn_lk_push_frame_device(psn_lk_ctx *c, int slot, const uint8_t *dev, int st
 
 static int push_host_impl(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, int channels) {
     const size_t row = (size_t)c->width * channels, need = row * c->height;
+    int rc0 = flush_pending(c);  // a deferred build may still read d_src's predecessor frame
+    if (rc0) return rc0;
     if (c->d_src_cap < need) {
         if (c->d_src) (void)hipFree(c->d_src);
         c->d_src = nullptr;
@@ -303,9 +370,15 @@ static int push_host_impl(psn_lk_ctx *c, int slot, const uint8_t *host, int stri
         HIPCHK(c, hipMalloc(&c->d_src, need));
         c->d_src_cap = need;
     }
-    hipStream_t s = c->overlap ? c->ingest_stream : c->stream;  // the stream the build runs on
-    HIPCHK(c, hipMemcpy2DAsync(c->d_src, row, host, stride, row, c->height, hipMemcpyHostToDevice, s));
-    int rc = push_device_impl(c, slot, c->d_src, (int)row, channels);
+    // the stream the build runs on (a fused-mode build of a host frame is not deferred)
+    const int mode = c->overlap;
+    if (mode == PSN_LK_OVERLAP_FUSED) c->overlap = PSN_LK_OVERLAP_OFF;
+    hipStream_t s = c->overlap == PSN_LK_OVERLAP_STREAM ? c->ingest_stream : c->stream;
+    if (c->overlap == PSN_LK_OVERLAP_STREAM && c->free_rec[slot]) HIPCHK(c, hipStreamWaitEvent(s, c->slot_free[slot], 0));
+    hipError_t ce = hipMemcpy2DAsync(c->d_src, row, host, stride, row, c->height, hipMemcpyHostToDevice, s);
+    int rc = ce == hipSuccess ? push_device_impl(c, slot, c->d_src, (int)row, channels)
+                              : set_err(c, PSN_LK_ERR_HIP, "hipMemcpy2DAsync: %s", hipGetErrorString(ce));
+    c->overlap = mode;
     if (rc) return rc;
     HIPCHK(c, hipStreamSynchronize(s));  // the host frame belongs to the caller after return
     return PSN_LK_OK;
@@ -367,15 +440,20 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
 
 static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
                              uint8_t *d_status, float *d_err, bool allow_scratch) {
-    // slots built on the ingest stream must be complete before the LK reads them
+    // slots built on the ingest stream must be complete before the LK reads them;
+    // a deferred build of a slot this call reads runs first, as its own launch
     for (int i = 0; i < nq; i++)
-        for (int sl : {q[i].prev_slot, q[i].next_slot})
-            if (sl >= 0 && sl < c->nslots && c->ready_rec[sl]) {
-                HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot_ready[sl], 0));
-                c->ready_rec[sl] = 0;
+        for (int sl : {q[i].prev_slot, q[i].next_slot}) {
+            if (c->pend && sl == c->pend_slot) {
+                int rc = flush_pending(c);
+                if (rc) return rc;
             }
-    const long ti = c->tcap ? (c->n_track % c->tcap) : 0;
-    if (c->tcap) HIPCHK(c, hipEventRecord(c->ev_track[2 * ti], c->stream));
+            int rc = wait_slot_ready(c, sl);
+            if (rc) return rc;
+        }
+    const bool timed = c->tcap && (c->calls_track++ % c->every) == 0;
+    const long ti = timed ? (c->n_track % c->tcap) : 0;
+    if (timed) HIPCHK(c, hipEventRecord(c->ev_track[2 * ti], c->stream));
     for (int base = 0; base < nq; base += psn::kMaxQueries) {
         const int n = std::min(psn::kMaxQueries, nq - base);
         psn::LkLaunchArgs a{};
@@ -416,6 +494,20 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             const int ept = maxpx <= 2 * nt ? 2 : 4;
             threads = nt * 10 + ept;
         }
+        if (c->pend && all_single) {  // fuse the deferred build into this launch's tail
+            int tx, ty, plds;
+            psn::pyramid_grid(c->pend_args, tx, ty, plds);
+            a.pyr = c->pend_args;
+            a.pyr_ntiles = tx * ty;
+            a.pyr_tiles_x = tx;
+            a.pyr_ctr = c->d_ctr;
+            a.total_wgs = wgs;
+            lds = std::max(lds, psn::kStScratchBytes + plds);
+            c->pend = false;
+        } else if (c->pend) {
+            int rc = flush_pending(c);
+            if (rc) return rc;
+        }
         if (!all_single) {  // the generic kernel runs every query of this launch: re-plan its LDS
             lds = 0;
             for (int i = 0; i < nqd; i++) {
@@ -430,11 +522,15 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         }
         HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, all_single, c->stream));
     }
-    if (c->tcap) {
+    if (c->pend) {  // no launch took it (no points)
+        int rc = flush_pending(c);
+        if (rc) return rc;
+    }
+    if (timed) {
         HIPCHK(c, hipEventRecord(c->ev_track[2 * ti + 1], c->stream));
         c->n_track++;
     }
-    if (c->overlap)  // the next build into these slots waits for this launch
+    if (c->overlap == PSN_LK_OVERLAP_STREAM)  // the next build into these slots waits for this launch
         for (int i = 0; i < nq; i++)
             for (int sl : {q[i].prev_slot, q[i].next_slot})
                 if (sl >= 0 && sl < c->nslots) {
@@ -542,6 +638,10 @@ int psn_lk_read_level(psn_lk_ctx *c, int slot, int level, uint8_t *host, int str
     const LevelDev &L = c->h_slots[(size_t)slot * psn::kMaxLevels + level];
     if (stride < L.w) return PSN_LK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    int rc = flush_pending(c);
+    if (rc) return rc;
+    rc = wait_slot_ready(c, slot);
+    if (rc) return rc;
     HIPCHK(c, hipMemcpy2DAsync(host, stride, L.p, L.pitch, L.w, L.h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PSN_LK_OK;

@@ -54,6 +54,14 @@ struct LkLaunchArgs {
     int nq;
     int pad_;
     LkQueryDev q[kMaxQueries];
+    // Deferred pyramid build fused into this launch (single-tile kernel only):
+    // workgroups that finish their point pull top-level tiles of `pyr` from
+    // the work counter pyr_ctr[0]; pyr_ctr[1] counts finished workgroups and
+    // the last one resets both. pyr_ntiles == 0: no fused build.
+    int pyr_ntiles, pyr_tiles_x;
+    int total_wgs, pad2_;
+    unsigned *pyr_ctr;
+    PyrBuildArgs pyr;
 };
 
 // LDS bytes a query needs for a given tile height (shared by host planner and kernel).
@@ -85,13 +93,14 @@ __host__ __device__ inline int lk_st_planeB(int w, int h, bool sse) {
 }
 // Single-tile kernel LDS layout. Staged u8 patches are held one pixel per
 // dword (LDS-DMA global_load_lds_ubyte writes a zero-extended dword per lane).
+constexpr int kStScratchBytes = 2 * kMaxLevels * 8 * 4 + 256;  // level table + reduce scratch
 struct LkStLayout {
     int tbl, ri, jr, pim, pim_stride, dg, pa, pb, total;
     __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev) {
         const int wh = w * h;
         tbl = 0;                                   // 2 pyramids x kMaxLevels x 8 ints
         ri = tbl + 2 * kMaxLevels * 8 * 4;         // 4 x 16 ints of reduce scratch
-        jr = ri + 256;
+        jr = ri + 256;                             // == kStScratchBytes (fused builds use LDS from here)
         pim = jr + align16(4 * lk_jreg_w(w) * lk_jreg_h(h));
         pim_stride = align16(4 * (h + 3) * (w + 3));
         dg = pim + nlev * pim_stride;
@@ -108,6 +117,7 @@ constexpr int kStMaxLds = 96 * 1024;
 
 // Launchers (psn_lk_kernels.hip).
 hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s);
+void pyramid_grid(const PyrBuildArgs &a, int &tiles_x, int &tiles_y, int &lds_bytes);
 hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, bool single_tile, hipStream_t s);
 hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
 

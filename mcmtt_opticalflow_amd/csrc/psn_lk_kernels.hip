@@ -88,23 +88,16 @@ __device__ __forceinline__ uint8_t load_src(const PyrBuildArgs &a, int y, int x)
     return (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
 }
 
-__global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+// One top-level tile (bx, by) of a multi-level build (top >= 1) by NT threads.
+// Called by pyramid_kernel and, for a deferred build fused into an LK launch,
+// by LK workgroups that have finished their point (lk_kernel_st epilogue).
+template <int NT>
+__device__ __forceinline__ void pyr_tile(const PyrBuildArgs &a, int bx, int by, uint8_t *smem) {
     const int tid = threadIdx.x;
     const int top = a.nlevels - 1;
     const int W0 = a.lv[0].w, H0 = a.lv[0].h;
-
-    if (top == 0) {  // single level: ingest only, 64x64 tiles
-        const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
-        for (int idx = tid; idx < 64 * 64; idx += 256) {
-            int gy = y0 + (idx >> 6), gx = x0 + (idx & 63);
-            if (gy < H0 && gx < W0) a.lv[0].p[(size_t)gy * a.lv[0].pitch + gx] = load_src(a, gy, gx);
-        }
-        return;
-    }
-
     const int T = a.tile;
-    const int topx = blockIdx.x * T, topy = blockIdx.y * T;
+    const int topx = bx * T, topy = by * T;
     const int n0 = pyr_region_n(top, 0, T);
     const int span = 1 << top;
     const int s0x = span * topx - 2 * (span - 1), s0y = span * topy - 2 * (span - 1);
@@ -114,7 +107,7 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
     {
         uint8_t *B0 = smem;
         const bool interior = s0x >= 0 && s0y >= 0 && s0x + n0 <= W0 && s0y + n0 <= H0;
-        for (int idx = tid; idx < n0 * n0; idx += 256) {
+        for (int idx = tid; idx < n0 * n0; idx += NT) {
             int yy = idx / n0, xx = idx - yy * n0;
             int gy = s0y + yy, gx = s0x + xx;
             if (!interior) {
@@ -129,7 +122,7 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
         const int ox = topx * span, oy = topy * span;
         uint8_t *dst = a.lv[0].p;
         const int pitch = a.lv[0].pitch;
-        for (int idx = tid; idx < own * own; idx += 256) {
+        for (int idx = tid; idx < own * own; idx += NT) {
             int yy = idx / own, xx = idx - yy * own;
             int gy = oy + yy, gx = ox + xx;
             if (gy < H0 && gx < W0) dst[(size_t)gy * pitch + gx] = B0[(yy + d) * n0 + xx + d];
@@ -144,7 +137,7 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
         const int Wl = a.lv[l].w, Hl = a.lv[l].h;
         const uint8_t *Bp = smem + pyr_lds_off(top, l - 1, T);
         // horizontal [1 4 6 4 1] over the previous region (rows np, cols nl)
-        for (int idx = tid; idx < np * nl; idx += 256) {
+        for (int idx = tid; idx < np * nl; idx += NT) {
             int r = idx / nl, c = idx - r * nl;
             const uint8_t *q = Bp + r * np + 2 * c;
             Ht[idx] = (int16_t)(q[0] + q[4] + 4 * (q[1] + q[3]) + 6 * q[2]);
@@ -152,7 +145,7 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
         __syncthreads();
         if (l < top) {
             uint8_t *Bl = smem + pyr_lds_off(top, l, T);
-            for (int idx = tid; idx < nl * nl; idx += 256) {
+            for (int idx = tid; idx < nl * nl; idx += NT) {
                 int yy = idx / nl, xx = idx - yy * nl;
                 int gy = sly + yy, gx = slx + xx;
                 if ((unsigned)gy < (unsigned)Hl && (unsigned)gx < (unsigned)Wl) {
@@ -164,7 +157,7 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
             __syncthreads();
             const bool border = slx < 0 || sly < 0 || slx + nl > Wl || sly + nl > Hl;
             if (border) {  // positions outside the level: copy their reflect-101 source
-                for (int idx = tid; idx < nl * nl; idx += 256) {
+                for (int idx = tid; idx < nl * nl; idx += NT) {
                     int yy = idx / nl, xx = idx - yy * nl;
                     int gy = sly + yy, gx = slx + xx;
                     if ((unsigned)gy >= (unsigned)Hl || (unsigned)gx >= (unsigned)Wl) {
@@ -178,7 +171,7 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
             const int ox = topx * sp, oy = topy * sp;
             uint8_t *dst = a.lv[l].p;
             const int pitch = a.lv[l].pitch;
-            for (int idx = tid; idx < own * own; idx += 256) {
+            for (int idx = tid; idx < own * own; idx += NT) {
                 int yy = idx / own, xx = idx - yy * own;
                 int gy = oy + yy, gx = ox + xx;
                 if (gy < Hl && gx < Wl) dst[(size_t)gy * pitch + gx] = Bl[(yy + d) * nl + xx + d];
@@ -186,7 +179,7 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
         } else {
             uint8_t *dst = a.lv[l].p;
             const int pitch = a.lv[l].pitch;
-            for (int idx = tid; idx < T * T; idx += 256) {
+            for (int idx = tid; idx < T * T; idx += NT) {
                 int yy = idx / T, xx = idx - yy * T;
                 int gy = topy + yy, gx = topx + xx;
                 if (gy < Hl && gx < Wl) {
@@ -200,17 +193,37 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
     }
 }
 
-hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s) {
-    const int top = a.nlevels - 1;
-    dim3 grid;
-    int lds = 0;
-    if (top == 0) {
-        grid = dim3((a.lv[0].w + 63) / 64, (a.lv[0].h + 63) / 64);
-    } else {
-        grid = dim3((a.lv[top].w + a.tile - 1) / a.tile, (a.lv[top].h + a.tile - 1) / a.tile);
-        lds = pyr_lds_bytes(top, a.tile);
+__global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.nlevels == 1) {  // single level: ingest only, 64x64 tiles
+        const int W0 = a.lv[0].w, H0 = a.lv[0].h;
+        const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
+        for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+            int gy = y0 + (idx >> 6), gx = x0 + (idx & 63);
+            if (gy < H0 && gx < W0) a.lv[0].p[(size_t)gy * a.lv[0].pitch + gx] = load_src(a, gy, gx);
+        }
+        return;
     }
-    hipLaunchKernelGGL(pyramid_kernel, grid, dim3(256), lds, s, a);
+    pyr_tile<256>(a, blockIdx.x, blockIdx.y, smem);
+}
+
+void pyramid_grid(const PyrBuildArgs &a, int &tiles_x, int &tiles_y, int &lds_bytes) {
+    const int top = a.nlevels - 1;
+    if (top == 0) {
+        tiles_x = (a.lv[0].w + 63) / 64;
+        tiles_y = (a.lv[0].h + 63) / 64;
+        lds_bytes = 0;
+    } else {
+        tiles_x = (a.lv[top].w + a.tile - 1) / a.tile;
+        tiles_y = (a.lv[top].h + a.tile - 1) / a.tile;
+        lds_bytes = pyr_lds_bytes(top, a.tile);
+    }
+}
+
+hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s) {
+    int tx, ty, lds;
+    pyramid_grid(a, tx, ty, lds);
+    hipLaunchKernelGGL(pyramid_kernel, dim3(tx, ty), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1452,6 +1465,32 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         A.next[2 * pi + 1] = NPy;
         A.status[pi] = (uint8_t)status;
         if (A.err) A.err[pi] = errv;
+    }
+    if (A.pyr_ntiles > 0) {
+        // fused next-frame ingest: this workgroup's point is done, so it pulls
+        // pyramid tiles while slower points keep iterating (fills the tail of
+        // the launch instead of a concurrent kernel on a second stream)
+        int *tile_slot = RI + 60;
+        for (;;) {
+            __syncthreads();  // every wave is done with LDS (LK state / previous tile)
+            if (tid == 0) tile_slot[0] = (int)atomicAdd(&A.pyr_ctr[0], 1u);
+            __syncthreads();
+            const int tile = tile_slot[0];
+            if (tile >= A.pyr_ntiles) break;
+            const int by = tile / A.pyr_tiles_x, bx = tile - by * A.pyr_tiles_x;
+            // the tile's LDS starts past the reduce scratch that holds tile_slot
+            pyr_tile<NT>(A.pyr, bx, by, smem + lay.jr);
+        }
+        if (tid == 0) {
+            // the last workgroup to finish resets the counters for the next launch;
+            // every workgroup has stopped pulling tiles before it counts itself done
+            __threadfence();
+            const unsigned done = atomicAdd(&A.pyr_ctr[1], 1u);
+            if (done == (unsigned)A.total_wgs - 1) {
+                A.pyr_ctr[0] = 0;
+                A.pyr_ctr[1] = 0;
+            }
+        }
     }
 }
 #undef PH_BEGIN

@@ -82,9 +82,10 @@ class LKContext:
     def set_stream(self, stream_ptr: int | None):
         self._check(self._L.psn_lk_set_stream(self._h, stream_ptr), "set_stream")
 
-    def set_ingest_overlap(self, on: bool = True):
-        """Build pyramids on the internal ingest stream (overlapping earlier LK work)."""
-        self._check(self._L.psn_lk_set_ingest_overlap(self._h, int(on)), "set_ingest_overlap")
+    def set_ingest_overlap(self, mode=True):
+        """Ingest overlap mode: False/0 off, True/1 internal ingest stream, 2 fused
+        into the next LK launch's tail (see psn_lk_set_ingest_overlap)."""
+        self._check(self._L.psn_lk_set_ingest_overlap(self._h, int(mode)), "set_ingest_overlap")
 
     def sync(self):
         self._check(self._L.psn_lk_sync(self._h), "sync")
@@ -124,9 +125,9 @@ class LKContext:
         self._check(self._L.psn_lk_track_device(self._h, arr, len(queries), d_prev, d_next, d_status, d_err),
                     "track_device")
 
-    def enable_timing(self, capacity: int = 1024):
-        """HIP-event timing of every push (pyramid kernel) / track (LK kernel) call."""
-        self._check(self._L.psn_lk_enable_timing(self._h, int(capacity)), "enable_timing")
+    def enable_timing(self, capacity: int = 1024, every: int = 1):
+        """HIP-event timing of every `every`-th push (pyramid launch) / track (LK launch) call."""
+        self._check(self._L.psn_lk_enable_timing(self._h, int(capacity), int(every)), "enable_timing")
 
     def timing_stats(self) -> dict:
         np_, nt = ctypes.c_int(), ctypes.c_int()

@@ -220,7 +220,7 @@ def test_lk_propagation_sequence(oracle_mod, overlap):
             p_gpu, p_ref = g[0], r[0]
 
 
-@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("overlap", [0, 1, 2])
 def test_lk_device_pointer_path(oracle_mod, overlap):
     import hiprt
 
@@ -239,6 +239,46 @@ def test_lk_device_pointer_path(oracle_mod, overlap):
         ctx.sync()
     gpu = (d_n.to_array(pts.shape, np.float32), d_s.to_array(len(pts), np.uint8), d_e.to_array(len(pts), np.float32))
     assert_same(gpu, ref, "device path")
+
+
+@pytest.mark.parametrize("env", [{}, {"PSN_LK_THREADS": "128"}, {"PSN_LK_THREADS": "64"}])
+@pytest.mark.parametrize("win", [(21, 21), (9, 9), (64, 64)])
+def test_lk_fused_ingest_pipeline(oracle_mod, monkeypatch, env, win):
+    """Fused ingest (PSN_LK_OVERLAP_FUSED): frame t+1 is pushed before frame t
+    is tracked, so its pyramid is built by the tail workgroups of the t-1 -> t
+    launch (or, for windows the single-tile kernel does not take, by its own
+    launch). Pyramids and propagated points must match the oracle bit for bit."""
+    import hiprt
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    W, H, R, T = 640, 480, 4, 7
+    sc = synth.make_scene(12, W, H, 96)
+    frames = [sc.frame(t) for t in range(T)]
+    d_frames = [hiprt.DeviceBuffer.from_array(f) for f in frames]
+    p_ref = sc.points_at(0)
+    n = len(p_ref)
+    d_pts = [hiprt.DeviceBuffer.from_array(p_ref), hiprt.DeviceBuffer(p_ref.nbytes)]
+    d_s, d_e = hiprt.DeviceBuffer(n), hiprt.DeviceBuffer(4 * n)
+    with glk.LKContext(W, H, ring_slots=R, max_level_cap=3) as ctx:
+        ctx.set_ingest_overlap(2)
+        ctx.push_frame_device(0, d_frames[0].addr, W, 1)
+        ctx.push_frame_device(1, d_frames[1].addr, W, 1)
+        ctx.sync()
+        for t in range(1, T):
+            if t + 1 < T:
+                ctx.push_frame_device((t + 1) % R, d_frames[t + 1].addr, W, 1)  # deferred
+            q = glk.make_query((t - 1) % R, t % R, 0, n, glk.make_params(win, 3))
+            ctx.track_device([q], d_pts[(t - 1) % 2].addr, d_pts[t % 2].addr, d_s.addr, d_e.addr)
+            ctx.sync()
+            gpu = (d_pts[t % 2].to_array(p_ref.shape, np.float32), d_s.to_array(n, np.uint8), d_e.to_array(n, np.float32))
+            r = oracle_ref(oracle_mod, frames[t - 1], frames[t], p_ref, win, 3)
+            assert_same(gpu, r, f"{env} {win} frame {t}")
+            p_ref = r[0]
+            if t + 1 < T:  # the pyramid built in this launch's tail
+                eff = oracle_mod.effective_max_level(W, H, 1, 1, 3)
+                for lvl, ref_l in enumerate(oracle_mod.build_pyramid(frames[t + 1], eff + 1)):
+                    np.testing.assert_array_equal(ctx.read_level((t + 1) % R, lvl), ref_l, f"pyr {t + 1} level {lvl}")
 
 
 def test_lk_config5_4k_5level(oracle_mod):
