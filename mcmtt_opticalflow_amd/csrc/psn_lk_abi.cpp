@@ -37,6 +37,8 @@ struct psn_lk_ctx {
     int pend_slot = -1;
     psn::PyrBuildArgs pend_args{};
     unsigned *d_ctr = nullptr;  // [2] fused-build work counter + finished workgroups
+    int fused_helpers = 0;      // PSN_LK_FUSED_HELPERS: tile-only workgroups per fused launch
+    psn::RingGeo ring{};        // slot/level geometry passed to the single-tile kernel
     std::vector<hipEvent_t> slot_ready, slot_free;
     std::vector<char> ready_rec, free_rec;
     uint8_t *d_pyr = nullptr;
@@ -135,6 +137,7 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     c->nlevels = max_level_cap + 1;
     if (const char *e = getenv("PSN_LK_THREADS")) c->force_threads = atoi(e);
     if (const char *e = getenv("PSN_LK_GENERIC")) c->force_generic = atoi(e) != 0;
+    if (const char *e = getenv("PSN_LK_FUSED_HELPERS")) c->fused_helpers = std::max(0, atoi(e));
     auto fail = [&](int rc) {
         psn_lk_destroy(c);
         return rc;
@@ -167,6 +170,14 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     // 3 bytes past the last row of a level
     if (hipMalloc(&c->d_pyr, slot_bytes * c->nslots + 256) != hipSuccess) return fail(PSN_LK_ERR_NOMEM);
     if (hipMemset(c->d_pyr, 0, slot_bytes * c->nslots + 256) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    c->ring.base = c->d_pyr;
+    c->ring.slot_bytes = (long long)slot_bytes;
+    for (int l = 0; l < c->nlevels; l++) {
+        c->ring.off[l] = (long long)lv_off[l];
+        c->ring.w[l] = lw[l];
+        c->ring.h[l] = lh[l];
+        c->ring.pitch[l] = lp[l];
+    }
     c->h_slots.assign((size_t)c->nslots * psn::kMaxLevels, LevelDev{nullptr, 0, 0, 0, 0});
     for (int s = 0; s < c->nslots; s++)
         for (int l = 0; l < c->nlevels; l++)
@@ -458,6 +469,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         const int n = std::min(psn::kMaxQueries, nq - base);
         psn::LkLaunchArgs a{};
         a.slots = c->d_slots;
+        a.ring = c->ring;
         a.prev = d_prev;
         a.next = d_next;
         a.status = d_status;
@@ -487,11 +499,14 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         int threads = maxpx <= 1024 ? 64 : maxpx <= 4096 ? 128 : 256;
         const int forced = c->force_threads;
         if (c->force_generic) all_single = false;
-        if (forced == 64 || forced == 128 || forced == 256) threads = forced;
+        if (forced == 64 || forced == 128 || forced == 256) threads = forced;  // tiled kernel sizes
         if (all_single) {  // single-tile kernel: (workgroup size, window pixels per thread)
             int nt = maxpx <= 128 ? 64 : maxpx <= 256 ? 128 : 256;
-            if ((forced == 64 || forced == 128 || forced == 256) && forced * psn::kStEPTMax >= maxpx) nt = forced;
-            const int ept = maxpx <= 2 * nt ? 2 : 4;
+            if (forced == 64 || forced == 128 || forced == 256 || forced == 512) {
+                const int max_ept = forced == 512 ? 2 : psn::kStEPTMax;
+                if (forced * max_ept >= maxpx) nt = forced;
+            }
+            const int ept = nt == 512 ? (maxpx <= 512 ? 1 : 2) : (maxpx <= 2 * nt ? 2 : 4);
             threads = nt * 10 + ept;
         }
         if (c->pend && all_single) {  // fuse the deferred build into this launch's tail
@@ -501,7 +516,12 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             a.pyr_ntiles = tx * ty;
             a.pyr_tiles_x = tx;
             a.pyr_ctr = c->d_ctr;
-            a.total_wgs = wgs;
+            // helpers start pulling tiles at once, so the build is done long before
+            // the slowest points finish (tiles taken late would extend the launch)
+            const int helpers = std::min(c->fused_helpers, a.pyr_ntiles);
+            a.lk_wgs = wgs;
+            a.total_wgs = wgs + helpers;
+            wgs += helpers;
             lds = std::max(lds, psn::kStScratchBytes + plds);
             c->pend = false;
         } else if (c->pend) {

@@ -44,8 +44,18 @@ struct LkQueryDev {
     double eps2;
 };
 
+// Ring geometry as kernel arguments (every slot has the same level layout):
+// level l of slot s starts at base + s * slot_bytes + off[l].
+struct RingGeo {
+    uint8_t *base;
+    long long slot_bytes;
+    long long off[kMaxLevels];
+    int w[kMaxLevels], h[kMaxLevels], pitch[kMaxLevels];
+};
+
 struct LkLaunchArgs {
     const LevelDev *slots;   // [nslots][kMaxLevels]
+    RingGeo ring;
     const float *prev;       // (x,y) pairs
     float *next;
     uint8_t *status;
@@ -58,8 +68,10 @@ struct LkLaunchArgs {
     // workgroups that finish their point pull top-level tiles of `pyr` from
     // the work counter pyr_ctr[0]; pyr_ctr[1] counts finished workgroups and
     // the last one resets both. pyr_ntiles == 0: no fused build.
+    // Helper workgroups (blockIdx >= lk_wgs) skip the LK part and pull tiles
+    // from the start; total_wgs = lk_wgs + helpers.
     int pyr_ntiles, pyr_tiles_x;
-    int total_wgs, pad2_;
+    int total_wgs, lk_wgs;
     unsigned *pyr_ctr;
     PyrBuildArgs pyr;
 };
@@ -91,29 +103,55 @@ __host__ __device__ inline int lk_st_planeB(int w, int h, bool sse) {
     const int n = sse ? w / 8 : 0;
     return 4 * round16i(h * 2 * n) + round16i(h * (w - 8 * n) + 1);
 }
-// Single-tile kernel LDS layout. Staged u8 patches are held one pixel per
-// dword (LDS-DMA global_load_lds_ubyte writes a zero-extended dword per lane).
-constexpr int kStScratchBytes = 2 * kMaxLevels * 8 * 4 + 256;  // level table + reduce scratch
+// Single-tile kernel LDS layout.
+//   scratch: level table (2 pyramids x kMaxLevels x 8 ints), reduce scratch
+//     RI (per-iteration regions for iteration parity 0/1 and the err pass: 4
+//     ints per wave for up to 8 waves; the fused-build tile index; the A-phase
+//     region: 4 sums x kStMaxLev levels x 8 waves), the per-level solver table
+//     LV (kStMaxLev x 8 floats);
+//   jp: the J region in PAIR format (dword x = J[x] | J[x+1] << 16, rows of
+//     st_jreg_w(w) dwords) for the packed-dot bilinear of the iterations;
+//   pim: the I patch of every level ((h+3) x (w+3), one dword per pixel as
+//     LDS-DMA writes them);
+//   dg: Scharr (Ix, Iy) short2 of every level ((h+1) x (w+1));
+//   iw: per level and window pixel {Iw, Ix | Iy << 16} (int2);
+//   r: A products of every level (3 chain-major planes per level); reused by
+//     the double-buffered b products of the iterations and the err plane.
+constexpr int kStMaxLev = kPyrMaxTop + 1;
+constexpr int kStJMargin = 4;  // J region margin (px) each side; prefetched at the predicted position
+constexpr int kStRiIt = 0, kStRiErr = 64, kStRiTile = 96, kStRiA = 128;           // ints
+constexpr int kStRiInts = kStRiA + 4 * kStMaxLev * 8;                             // 320
+constexpr int kStLvFloats = 8;
+constexpr int kStScratchBytes = 2 * kMaxLevels * 8 * 4 + kStRiInts * 4 + kStMaxLev * kStLvFloats * 4;  // 1984
+// J region: origin aligned down to 4 columns (one 8-byte load -> 4 pairs -> one
+// 16-B LDS write), width a multiple of 4 keeping >= kStJMargin columns each side
+__host__ __device__ inline int st_jreg_w(int w) { return (w + 2 * kStJMargin + 4 + 3) & ~3; }
+__host__ __device__ inline int st_jreg_h(int h) { return h + 1 + 2 * kStJMargin; }
 struct LkStLayout {
-    int tbl, ri, jr, pim, pim_stride, dg, pa, pb, total;
+    int tbl, ri, lv, jp, pim, pim_stride, dg, dg_stride, iw, iw_stride, r, total;
     __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev) {
         const int wh = w * h;
-        tbl = 0;                                   // 2 pyramids x kMaxLevels x 8 ints
-        ri = tbl + 2 * kMaxLevels * 8 * 4;         // 4 x 16 ints of reduce scratch
-        jr = ri + 256;                             // == kStScratchBytes (fused builds use LDS from here)
-        pim = jr + align16(4 * lk_jreg_w(w) * lk_jreg_h(h));
+        tbl = 0;
+        ri = tbl + 2 * kMaxLevels * 8 * 4;
+        lv = ri + kStRiInts * 4;
+        jp = kStScratchBytes;                      // fused builds use LDS from here
+        pim = jp + align16(4 * st_jreg_w(w) * st_jreg_h(h));
         pim_stride = align16(4 * (h + 3) * (w + 3));
         dg = pim + nlev * pim_stride;
-        pa = dg + align16(4 * (h + 1) * (w + 1));
-        int pa_bytes = 12 * lk_st_planeA(w, h, sse);
-        const int err_bytes = 4 * round16i(wh);  // row-major |diff| plane of the err pass
-        if (pa_bytes < err_bytes) pa_bytes = err_bytes;
-        pb = pa + pa_bytes;
-        total = pb + 16 * lk_st_planeB(w, h, sse);
+        dg_stride = align16(4 * (h + 1) * (w + 1));
+        iw = dg + nlev * dg_stride;
+        iw_stride = align16(8 * wh);
+        r = iw + nlev * iw_stride;
+        int rb = 12 * nlev * lk_st_planeA(w, h, sse);
+        const int pb = 16 * lk_st_planeB(w, h, sse);
+        const int eb = 4 * round16i(wh);
+        if (rb < pb) rb = pb;
+        if (rb < eb) rb = eb;
+        total = r + rb;
     }
 };
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel
-constexpr int kStMaxLds = 96 * 1024;
+constexpr int kStMaxLds = 150 * 1024;
 
 // Launchers (psn_lk_kernels.hip).
 hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s);

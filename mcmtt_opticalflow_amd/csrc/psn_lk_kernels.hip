@@ -67,11 +67,14 @@ __host__ __device__ inline int pyr_region_n(int top, int l, int T) {
     int sp = 1 << (top - l);
     return sp * T + 3 * (sp - 1);
 }
+// Level-0 region rows in LDS: the region starts at an aligned-down column
+// (offset 0..3) so interior rows move as dwords.
+__host__ __device__ inline int pyr_s0(int n0) { return (n0 + 3 + 3) & ~3; }
 __host__ __device__ inline int pyr_lds_off(int top, int l, int T) {
     int off = 0;
     for (int m = 0; m < l; m++) {
         int n = pyr_region_n(top, m, T);
-        off += align16(n * n);
+        off += align16(m == 0 ? pyr_s0(n) * n : n * n);
     }
     return off;
 }
@@ -88,12 +91,18 @@ __device__ __forceinline__ uint8_t load_src(const PyrBuildArgs &a, int y, int x)
     return (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
 }
 
-// One top-level tile (bx, by) of a multi-level build (top >= 1) by NT threads.
-// Called by pyramid_kernel and, for a deferred build fused into an LK launch,
-// by LK workgroups that have finished their point (lk_kernel_st epilogue).
+// One top-level tile (bx, by) of a multi-level build (top >= 1) by NT threads
+// laid out 16 wide (no index divisions). The tile recomputes its halo through
+// the levels in LDS: level-0 region (dword loads for interior gray tiles,
+// reflect-101 byte gathers otherwise), then per level a horizontal [1 4 6 4 1]
+// pass into int16 and a vertical pass with (sum + 128) >> 8; region positions
+// outside a level take their reflect-101 source. Each level's own tile goes
+// out as dword stores. Called by pyramid_kernel and, for a deferred build
+// fused into an LK launch, by the LK launch's workgroups (pyr_tail).
 template <int NT>
 __device__ __forceinline__ void pyr_tile(const PyrBuildArgs &a, int bx, int by, uint8_t *smem) {
-    const int tid = threadIdx.x;
+    constexpr int TX = 16, TY = NT / 16;
+    const int tx = threadIdx.x & (TX - 1), ty = threadIdx.x / TX;
     const int top = a.nlevels - 1;
     const int W0 = a.lv[0].w, H0 = a.lv[0].h;
     const int T = a.tile;
@@ -101,31 +110,47 @@ __device__ __forceinline__ void pyr_tile(const PyrBuildArgs &a, int bx, int by, 
     const int n0 = pyr_region_n(top, 0, T);
     const int span = 1 << top;
     const int s0x = span * topx - 2 * (span - 1), s0y = span * topy - 2 * (span - 1);
+    const int ax = s0x & ~3, off0 = s0x - ax, S0 = pyr_s0(n0);
+    uint8_t *B0 = smem;
     int16_t *Ht = (int16_t *)(smem + pyr_lds_off(top, top, T));
 
-    // level-0 region, reflect-101 applied for every position
+    // level-0 region
     {
-        uint8_t *B0 = smem;
-        const bool interior = s0x >= 0 && s0y >= 0 && s0x + n0 <= W0 && s0y + n0 <= H0;
-        for (int idx = tid; idx < n0 * n0; idx += NT) {
-            int yy = idx / n0, xx = idx - yy * n0;
-            int gy = s0y + yy, gx = s0x + xx;
-            if (!interior) {
-                gy = refl101(gy, H0);
-                gx = refl101(gx, W0);
+        const int m = (off0 + n0 + 3) >> 2;  // dwords per row
+        const bool dw = a.channels == 1 && s0x >= 0 && s0y >= 0 && ax + 4 * m <= W0 && s0y + n0 <= H0 &&
+                        ((uintptr_t)a.src & 3) == 0 && (a.src_stride & 3) == 0;
+        if (dw) {
+            for (int r = ty; r < n0; r += TY) {
+                const uint32_t *srow = (const uint32_t *)(a.src + (size_t)(s0y + r) * a.src_stride + ax);
+                for (int d = tx; d < m; d += TX) *(uint32_t *)(B0 + r * S0 + 4 * d) = srow[d];
             }
-            B0[idx] = load_src(a, gy, gx);
+        } else {
+            for (int r = ty; r < n0; r += TY) {
+                const int gy = refl101(s0y + r, H0);
+                for (int c = tx; c < n0; c += TX) B0[r * S0 + off0 + c] = load_src(a, gy, refl101(s0x + c, W0));
+            }
         }
-        __syncthreads();
-        // own level-0 tile
-        const int own = span * T, d = 2 * (span - 1);
+    }
+    __syncthreads();
+    // own level-0 tile
+    {
+        const int own = span * T, d0 = 2 * (span - 1);
         const int ox = topx * span, oy = topy * span;
         uint8_t *dst = a.lv[0].p;
         const int pitch = a.lv[0].pitch;
-        for (int idx = tid; idx < own * own; idx += NT) {
-            int yy = idx / own, xx = idx - yy * own;
-            int gy = oy + yy, gx = ox + xx;
-            if (gy < H0 && gx < W0) dst[(size_t)gy * pitch + gx] = B0[(yy + d) * n0 + xx + d];
+        for (int r = ty; r < own && oy + r < H0; r += TY) {
+            const uint8_t *srow = B0 + (r + d0) * S0 + off0 + d0;
+            uint8_t *drow = dst + (size_t)(oy + r) * pitch + ox;
+            for (int q = tx; q < own / 4; q += TX) {
+                const uint8_t *sp4 = srow + 4 * q;
+                if (ox + 4 * q + 4 <= W0) {
+                    *(uint32_t *)(drow + 4 * q) =
+                        sp4[0] | ((uint32_t)sp4[1] << 8) | ((uint32_t)sp4[2] << 16) | ((uint32_t)sp4[3] << 24);
+                } else {
+                    for (int b = 0; b < 4; b++)
+                        if (ox + 4 * q + b < W0) drow[4 * q + b] = sp4[b];
+                }
+            }
         }
     }
 
@@ -135,59 +160,69 @@ __device__ __forceinline__ void pyr_tile(const PyrBuildArgs &a, int bx, int by, 
         const int np = pyr_region_n(top, l - 1, T);
         const int slx = sp * topx - 2 * (sp - 1), sly = sp * topy - 2 * (sp - 1);
         const int Wl = a.lv[l].w, Hl = a.lv[l].h;
-        const uint8_t *Bp = smem + pyr_lds_off(top, l - 1, T);
+        const uint8_t *Bp = l == 1 ? B0 + off0 : smem + pyr_lds_off(top, l - 1, T);
+        const int Sp = l == 1 ? S0 : np;
         // horizontal [1 4 6 4 1] over the previous region (rows np, cols nl)
-        for (int idx = tid; idx < np * nl; idx += NT) {
-            int r = idx / nl, c = idx - r * nl;
-            const uint8_t *q = Bp + r * np + 2 * c;
-            Ht[idx] = (int16_t)(q[0] + q[4] + 4 * (q[1] + q[3]) + 6 * q[2]);
-        }
+        for (int r = ty; r < np; r += TY)
+            for (int c = tx; c < nl; c += TX) {
+                const uint8_t *q = Bp + r * Sp + 2 * c;
+                Ht[r * nl + c] = (int16_t)(q[0] + q[4] + 4 * (q[1] + q[3]) + 6 * q[2]);
+            }
         __syncthreads();
         if (l < top) {
             uint8_t *Bl = smem + pyr_lds_off(top, l, T);
-            for (int idx = tid; idx < nl * nl; idx += NT) {
-                int yy = idx / nl, xx = idx - yy * nl;
-                int gy = sly + yy, gx = slx + xx;
-                if ((unsigned)gy < (unsigned)Hl && (unsigned)gx < (unsigned)Wl) {
-                    const int16_t *c = Ht + 2 * yy * nl + xx;
-                    int v = c[0] + c[4 * nl] + 4 * (c[nl] + c[3 * nl]) + 6 * c[2 * nl];
-                    Bl[idx] = (uint8_t)((v + 128) >> 8);
+            for (int r = ty; r < nl; r += TY)
+                for (int c = tx; c < nl; c += TX) {
+                    const int gy = sly + r, gx = slx + c;
+                    if ((unsigned)gy < (unsigned)Hl && (unsigned)gx < (unsigned)Wl) {
+                        const int16_t *cc = Ht + 2 * r * nl + c;
+                        const int v = cc[0] + cc[4 * nl] + 4 * (cc[nl] + cc[3 * nl]) + 6 * cc[2 * nl];
+                        Bl[r * nl + c] = (uint8_t)((v + 128) >> 8);
+                    }
                 }
-            }
             __syncthreads();
             const bool border = slx < 0 || sly < 0 || slx + nl > Wl || sly + nl > Hl;
             if (border) {  // positions outside the level: copy their reflect-101 source
-                for (int idx = tid; idx < nl * nl; idx += NT) {
-                    int yy = idx / nl, xx = idx - yy * nl;
-                    int gy = sly + yy, gx = slx + xx;
-                    if ((unsigned)gy >= (unsigned)Hl || (unsigned)gx >= (unsigned)Wl) {
-                        int ry = refl101(gy, Hl) - sly, rx = refl101(gx, Wl) - slx;
-                        Bl[idx] = Bl[ry * nl + rx];
+                for (int r = ty; r < nl; r += TY)
+                    for (int c = tx; c < nl; c += TX) {
+                        const int gy = sly + r, gx = slx + c;
+                        if ((unsigned)gy >= (unsigned)Hl || (unsigned)gx >= (unsigned)Wl) {
+                            const int ry = refl101(gy, Hl) - sly, rx = refl101(gx, Wl) - slx;
+                            Bl[r * nl + c] = Bl[ry * nl + rx];
+                        }
                     }
-                }
                 __syncthreads();
             }
             const int own = sp * T, d = 2 * (sp - 1);
             const int ox = topx * sp, oy = topy * sp;
             uint8_t *dst = a.lv[l].p;
             const int pitch = a.lv[l].pitch;
-            for (int idx = tid; idx < own * own; idx += NT) {
-                int yy = idx / own, xx = idx - yy * own;
-                int gy = oy + yy, gx = ox + xx;
-                if (gy < Hl && gx < Wl) dst[(size_t)gy * pitch + gx] = Bl[(yy + d) * nl + xx + d];
+            for (int r = ty; r < own && oy + r < Hl; r += TY) {
+                const uint8_t *srow = Bl + (r + d) * nl + d;
+                uint8_t *drow = dst + (size_t)(oy + r) * pitch + ox;
+                for (int q = tx; q < own / 4; q += TX) {
+                    const uint8_t *sp4 = srow + 4 * q;
+                    if (ox + 4 * q + 4 <= Wl) {
+                        *(uint32_t *)(drow + 4 * q) =
+                            sp4[0] | ((uint32_t)sp4[1] << 8) | ((uint32_t)sp4[2] << 16) | ((uint32_t)sp4[3] << 24);
+                    } else {
+                        for (int b = 0; b < 4; b++)
+                            if (ox + 4 * q + b < Wl) drow[4 * q + b] = sp4[b];
+                    }
+                }
             }
         } else {
             uint8_t *dst = a.lv[l].p;
             const int pitch = a.lv[l].pitch;
-            for (int idx = tid; idx < T * T; idx += NT) {
-                int yy = idx / T, xx = idx - yy * T;
-                int gy = topy + yy, gx = topx + xx;
-                if (gy < Hl && gx < Wl) {
-                    const int16_t *c = Ht + 2 * yy * nl + xx;
-                    int v = c[0] + c[4 * nl] + 4 * (c[nl] + c[3 * nl]) + 6 * c[2 * nl];
-                    dst[(size_t)gy * pitch + gx] = (uint8_t)((v + 128) >> 8);
+            for (int r = ty; r < T; r += TY)
+                for (int c = tx; c < T; c += TX) {
+                    const int gy = topy + r, gx = topx + c;
+                    if (gy < Hl && gx < Wl) {
+                        const int16_t *cc = Ht + 2 * r * nl + c;
+                        const int v = cc[0] + cc[4 * nl] + 4 * (cc[nl] + cc[3 * nl]) + 6 * cc[2 * nl];
+                        dst[(size_t)gy * pitch + gx] = (uint8_t)((v + 128) >> 8);
+                    }
                 }
-            }
         }
         __syncthreads();
     }
@@ -994,54 +1029,42 @@ __device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ LevelDev tbl_level(const int *tbl, int pyr, int level) {
-    const int *e = tbl + (pyr * kMaxLevels + level) * 8;
-    LevelDev L;
-    L.p = (uint8_t *)(((uint64_t)(uint32_t)e[1] << 32) | (uint32_t)e[0]);
-    L.w = e[2];
-    L.h = e[3];
-    L.pitch = e[4];
-    L.pad_ = 0;
-    return L;
+
+// Element walk of a region with m elements per row: this thread's first
+// element (row, column) and the per-NT step (computed once per kernel).
+struct JWalk {
+    int ey0, ex0, sy, sx, m;
+};
+__device__ __forceinline__ JWalk jwalk(int m, int nt) {
+    JWalk wk;
+    wk.m = m;
+    wk.ey0 = threadIdx.x / m;
+    wk.ex0 = threadIdx.x - wk.ey0 * m;
+    wk.sy = nt / m;
+    wk.sx = nt - wk.sy * m;
+    return wk;
 }
 
-// Register-staged load of a PW x PH u8 region into LDS (one dword per pixel,
-// row stride PW): the loads are issued by load() and written by store(), so
-// the memory latency overlaps whatever the caller does in between. Interior
-// regions move aligned dwords (4 pixels per load); regions that cross the
-// image border gather single bytes through reflect-101. Up to KJ*NT elements
-// are in flight; any remainder is moved synchronously by store().
-constexpr int KJ = 8;
+// Register-staged load of a J region into LDS in PAIR format: dword c of a
+// row holds J[c] | J[c+1] << 16, so one LDS read feeds one packed dot
+// (v_dot2_i32_i16) half of the bilinear interpolation. load() issues the
+// global loads and store() writes LDS, so the memory latency overlaps whatever
+// the caller does in between (the next level's region is prefetched at its
+// predicted position while this level iterates). The region origin is a
+// multiple of 4 columns: interior regions move 8 bytes per element (two
+// aligned dwords) and write 4 pairs with one 16-B LDS store; regions that cross
+// the image border gather the 2 bytes of each pair through reflect-101. KJ*NT
+// elements are held in registers; the rest move synchronously in store().
+constexpr int KJ = 4;
 template <int NT>
-struct JStage {
-    int v[KJ];
+struct JPStage {
+    uint2 v[KJ];
     const uint8_t *src;
-    int pitch, lw, lh, gy0, gx0, PW, PH, ax0, ndw, n;
+    int pitch, lw, lh, gy0, gx0, PW, PH;
     bool interior;
-    __device__ __forceinline__ void fetch(int e, int &out) const {
-        if (interior) {  // element = aligned dword d of row y
-            const int y = e / ndw, d = e - y * ndw;
-            out = *(const __attribute__((address_space(1))) int *)(src + (size_t)(gy0 + y) * pitch + ax0 + 4 * d);
-        } else {
-            const int y = e / PW, x = e - y * PW;
-            out = src[(size_t)refl101(gy0 + y, lh) * pitch + refl101(gx0 + x, lw)];
-        }
-    }
-    __device__ __forceinline__ void put(uint32_t *dst, int e, int val) const {
-        if (interior) {
-            const int y = e / ndw, d = e - y * ndw;
-            const int x0 = ax0 + 4 * d - gx0;  // region column of byte 0
-            uint32_t *row = dst + y * PW;
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const int x = x0 + b;
-                if (x >= 0 && x < PW) row[x] = (uint32_t)(val >> (8 * b)) & 0xff;
-            }
-        } else {
-            dst[e] = (uint32_t)val;
-        }
-    }
-    __device__ __forceinline__ void load(const LevelDev &L, int y0, int x0, int pw, int ph) {
+    JWalk wk;
+    __device__ __forceinline__ void setup(const LevelDev &L, int y0, int x0, int pw, int ph, const JWalk &wi,
+                                          const JWalk &wb) {
         src = L.p;
         pitch = L.pitch;
         lw = L.w;
@@ -1051,60 +1074,181 @@ struct JStage {
         PW = pw;
         PH = ph;
         interior = y0 >= 0 && x0 >= 0 && y0 + ph <= lh && x0 + pw <= lw;
-        ax0 = x0 & ~3;
-        ndw = (x0 - ax0 + pw + 3) >> 2;
-        n = interior ? ph * ndw : ph * pw;
-        // dword loads may read up to 3 bytes past the region's row end: they stay
-        // inside the row's 256-B padded pitch or the next row, never past the slot
+        wk = interior ? wi : wb;
+    }
+    __device__ __forceinline__ void step(int &y, int &x) const {
+        x += wk.sx;
+        y += wk.sy;
+        if (x >= wk.m) {
+            x -= wk.m;
+            y++;
+        }
+    }
+    __device__ __forceinline__ void fetch(int y, int x, uint2 &out) const {
+        typedef const __attribute__((address_space(1))) unsigned gu32;
+        if (interior) {
+            // bytes 4x .. 4x+7 of the row (the last element reads 4 bytes past the
+            // region: inside the 256-B padded pitch, the next row, or the slot slack)
+            gu32 *q = (gu32 *)(src + (size_t)(gy0 + y) * pitch + gx0 + 4 * x);
+            out.x = q[0];
+            out.y = q[1];
+        } else {
+            const uint8_t *row = src + (size_t)refl101(gy0 + y, lh) * pitch;
+            out.x = row[refl101(gx0 + x, lw)];
+            out.y = row[refl101(gx0 + x + 1, lw)];
+        }
+    }
+    __device__ __forceinline__ void put(uint32_t *dst, int y, int x, const uint2 &val) const {
+        if (interior) {
+            uint4 q;
+            q.x = __builtin_amdgcn_perm(val.y, val.x, 0x0c010c00u);  // J[4x]   | J[4x+1] << 16
+            q.y = __builtin_amdgcn_perm(val.y, val.x, 0x0c020c01u);
+            q.z = __builtin_amdgcn_perm(val.y, val.x, 0x0c030c02u);
+            q.w = __builtin_amdgcn_perm(val.y, val.x, 0x0c040c03u);  // J[4x+3] | J[4x+4] << 16
+            *(uint4 *)(dst + y * PW + 4 * x) = q;
+        } else {
+            dst[y * PW + x] = val.x | (val.y << 16);
+        }
+    }
+    __device__ __forceinline__ void load(const LevelDev &L, int y0, int x0, int pw, int ph, const JWalk &wi,
+                                         const JWalk &wb) {
+        setup(L, y0, x0, pw, ph, wi, wb);
+        int y = wk.ey0, x = wk.ex0;
 #pragma unroll
         for (int k = 0; k < KJ; k++) {
-            const int e = threadIdx.x + k * NT;
-            if (e < n) fetch(e, v[k]);
+            if (y < PH) fetch(y, x, v[k]);
+            step(y, x);
         }
     }
     __device__ __forceinline__ void store(uint32_t *dst) const {
+        int y = wk.ey0, x = wk.ex0;
 #pragma unroll
         for (int k = 0; k < KJ; k++) {
-            const int e = threadIdx.x + k * NT;
-            if (e < n) put(dst, e, v[k]);
+            if (y < PH) put(dst, y, x, v[k]);
+            step(y, x);
         }
-        for (int e = threadIdx.x + KJ * NT; e < n; e += NT) {
-            int t;
-            fetch(e, t);
-            put(dst, e, t);
+        while (y < PH) {
+            uint2 t;
+            fetch(y, x, t);
+            put(dst, y, x, t);
+            step(y, x);
+        }
+    }
+    // synchronous load + store (restage inside the iterations)
+    __device__ __forceinline__ void copy(uint32_t *dst, const LevelDev &L, int y0, int x0, int pw, int ph,
+                                         const JWalk &wi, const JWalk &wb) {
+        setup(L, y0, x0, pw, ph, wi, wb);
+        int y = wk.ey0, x = wk.ex0;
+        while (y < PH) {
+            uint2 t;
+            fetch(y, x, t);
+            put(dst, y, x, t);
+            step(y, x);
         }
     }
 };
 
+// Level descriptor of (slot, level) from the kernel-argument ring geometry.
+__device__ __forceinline__ LevelDev ring_level(const RingGeo &r, int slot, int level) {
+    LevelDev L;
+    L.p = r.base + (long long)slot * r.slot_bytes + r.off[level];
+    L.w = r.w[level];
+    L.h = r.h[level];
+    L.pitch = r.pitch[level];
+    L.pad_ = 0;
+    return L;
+}
+
+// v_dot2_i32_i16: a.lo*b.lo + a.hi*b.hi + c on signed 16-bit halves. Signed
+// because iw11 = 2^14 - iw00 - iw01 - iw10 is -1 when the three rounded
+// weights overshoot (tiny fractional offsets); pixels (<= 255) are positive.
+__device__ __forceinline__ int sdot2(unsigned a, unsigned b, int c) {
+    typedef short i16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, b), c, false);
+}
+__device__ __forceinline__ unsigned pack_w(int lo, int hi) { return ((unsigned)lo & 0xffffu) | ((unsigned)hi << 16); }
+
+// Level geometry of the I window (prevPt/2^l - halfWin): top-left, validity and weights.
+struct IGeo {
+    int ipx, ipy, w00, w01, w10, w11;
+    bool valid;
+};
+__device__ __forceinline__ IGeo i_geo(float px0, float py0, float hwx, float hwy, int level, int w, int h, int cols,
+                                      int rows) {
+    IGeo gg;
+    const float scale = ldexpf(1.f, -level);
+    const float px = __fsub_rn(__fmul_rn(px0, scale), hwx), py = __fsub_rn(__fmul_rn(py0, scale), hwy);
+    gg.ipx = cv_floor(px);
+    gg.ipy = cv_floor(py);
+    gg.valid = !(gg.ipx < -w || gg.ipx >= cols || gg.ipy < -h || gg.ipy >= rows);
+    bilin_weights(__fsub_rn(px, (float)gg.ipx), __fsub_rn(py, (float)gg.ipy), gg.w00, gg.w01, gg.w10, gg.w11);
+    return gg;
+}
+
+// Fused next-frame ingest (PSN_LK_OVERLAP_FUSED): helper workgroups, and LK
+// workgroups whose point is done, pull top-level pyramid tiles from a work
+// counter while slower points keep iterating. Every workgroup of the launch
+// counts itself done once it stopped pulling; the last one resets the counters
+// for the next launch on the stream.
+template <int NT>
+__device__ __forceinline__ void pyr_tail(const LkLaunchArgs &A, uint8_t *smem) {
+    int *tile_slot = (int *)(smem + 2 * kMaxLevels * 8 * 4) + kStRiTile;  // inside the scratch area
+    __builtin_amdgcn_s_setprio(0);
+    for (;;) {
+        __syncthreads();  // every wave is done with LDS (LK state / previous tile)
+        if (threadIdx.x == 0) tile_slot[0] = (int)atomicAdd(&A.pyr_ctr[0], 1u);
+        __syncthreads();
+        const int tile = tile_slot[0];
+        if (tile >= A.pyr_ntiles) break;
+        const int by = tile / A.pyr_tiles_x, bx = tile - by * A.pyr_tiles_x;
+        pyr_tile<NT>(A.pyr, bx, by, smem + kStScratchBytes);  // past the scratch holding tile_slot
+    }
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const unsigned done = atomicAdd(&A.pyr_ctr[1], 1u);
+        if (done == (unsigned)A.total_wgs - 1) {
+            A.pyr_ctr[0] = 0;
+            A.pyr_ctr[1] = 0;
+        }
+    }
+}
+
+// Diagnostic stamps of the single-tile kernel (PSN_LK_STAMPS): 60 start, 50
+// prologue landed, 51 Scharr of all levels, 52 A products + reduction, 53
+// solver table; per level L*10+0 start, +1 J staged, +2 window loaded, +7
+// iterations done, +8 iteration count; 40..45 accumulated iteration phases.
 template <int NT, int EPT>
 __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int tid = threadIdx.x, lane = tid & 63;
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = blockIdx.x;
+    if (A.pyr_ntiles > 0 && g >= A.lk_wgs) {  // fused-build helper: tiles only
+        pyr_tail<NT>(A, smem);
+        return;
+    }
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
     const LkQueryDev &Q = A.q[qi];
     const int pi = Q.pt_begin + (g - Q.wg_begin);
     const int w = Q.win_w, h = Q.win_h, wh = w * h;
-    const int maxL = Q.max_level;
+    const int maxL = Q.max_level, nlev = maxL + 1;
     const int flags = Q.flags;
     const bool sse = (flags & PSN_LK_ACCUM_SCALAR) == 0;
-    const int JRW = lk_jreg_w(w), JRH = lk_jreg_h(h);
+    const int JRW = st_jreg_w(w), JRH = st_jreg_h(h);
     const int PW = w + 3, DW = w + 1;
 
-    const LkStLayout lay(w, h, sse, maxL + 1);
-    int *TBL = (int *)(smem + lay.tbl);
-    int *RI = (int *)(smem + lay.ri);  // [4][16]: iterations (x2), A-phase, err
-    uint32_t *JR = (uint32_t *)(smem + lay.jr);
-    short2 *Dg = (short2 *)(smem + lay.dg);
-    float *PA = (float *)(smem + lay.pa);
-    float *PB = (float *)(smem + lay.pb);
+    const LkStLayout lay(w, h, sse, nlev);
+    int *RI = (int *)(smem + lay.ri);
+    float *LV = (float *)(smem + lay.lv);
+    uint32_t *JP = (uint32_t *)(smem + lay.jp);
+    float *R = (float *)(smem + lay.r);
     const ChainGeo GA = chain_geo_A(w, h, sse), GB = chain_geo_B(w, h, sse);
 
     // ---- per-thread window pixels (fixed for the whole kernel). Idle lanes
     // (pixel index >= w*h) read pixel 0, carry zero gradients and write their
     // zero products into a pad slot of the chain planes: branch-free loops.
-    int ofsJ[EPT], ofsP[EPT], ofsD[EPT], posA_[EPT], posB_[EPT], ofsE[EPT];
+    int ofsJ[EPT], ofsP[EPT], ofsD[EPT], posA_[EPT], posB_[EPT], ofsE[EPT], pix[EPT];
     bool ev[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; k++) {
@@ -1112,6 +1256,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         ev[k] = idx < wh;
         const int i = ev[k] ? idx : 0;
         const int y = i / w, x = i - (i / w) * w;
+        pix[k] = i;
         ofsJ[k] = y * JRW + x;
         ofsP[k] = (y + 1) * PW + x + 1;
         ofsD[k] = y * DW + x;
@@ -1120,17 +1265,13 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         ofsE[k] = ev[k] ? idx : round16i(wh);  // err plane (row-major): idle lanes write past the end
     }
 
-    // ---- prologue: level table -> LDS, zero chain padding once ----
-    if (tid < 2 * (maxL + 1) * 8) {
-        const int pyr = tid / ((maxL + 1) * 8), rem = tid % ((maxL + 1) * 8), lvl = rem / 8, f = rem % 8;
-        const int slot = pyr == 0 ? Q.prev_slot : Q.next_slot;
-        const int *src = (const int *)&A.slots[slot * kMaxLevels + lvl];
-        if (f < 6) TBL[(pyr * kMaxLevels + lvl) * 8 + f] = src[f];
-    }
-    zero_pads<NT>(PA, GA, 3);
-    zero_pads<NT>(PB, GB, 2);
-    zero_pads<NT>(PB + 2 * GB.P, GB, 2);
-    __syncthreads();
+    // the point's waves outrank fused pyramid-tile waves sharing their SIMDs
+    if (A.pyr_ntiles > 0) __builtin_amdgcn_s_setprio(2);
+    // ---- prologue: zero the A planes' chain padding (ordered by the barrier
+    // after the DMA); level geometry comes from the kernel arguments ----
+    zero_pads<NT>(R, GA, 3 * nlev);
+    const JWalk wk_int = jwalk(JRW >> 2, NT), wk_bord = jwalk(JRW, NT);  // J staging walks
+    LK_STAMP(60);
 
     const float hwx = __fmul_rn((float)(w - 1), 0.5f), hwy = __fmul_rn((float)(h - 1), 0.5f);
     const float px0 = A.prev[2 * pi], py0 = A.prev[2 * pi + 1];
@@ -1140,30 +1281,185 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         NPy = A.next[2 * pi + 1];
     }
 
-    // ---- prologue LDS-DMA: the I patch of EVERY level + the coarsest J region ----
+    // ---- the I patch of every level by LDS-DMA; the coarsest J region into registers ----
     for (int l = 0; l <= maxL; l++) {
-        const LevelDev I = tbl_level(TBL, 0, l);
-        const float sc = ldexpf(1.f, -l);
-        const int ipx = cv_floor(__fsub_rn(__fmul_rn(px0, sc), hwx)), ipy = cv_floor(__fsub_rn(__fmul_rn(py0, sc), hwy));
-        if (ipx < -w || ipx >= I.w || ipy < -h || ipy >= I.h) continue;
-        dma_region<NT>((uint32_t *)(smem + lay.pim + l * lay.pim_stride), I, ipy - 1, ipx - 1, PW, h + 3);
+        const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
+        const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
+        if (!gg.valid) continue;
+        dma_region<NT>((uint32_t *)(smem + lay.pim + l * lay.pim_stride), I, gg.ipy - 1, gg.ipx - 1, PW, h + 3);
     }
-    int jr_x0, jr_y0;
+    JPStage<NT> pf;  // prefetched J region of level pf_level at (pf_y0, pf_x0)
+    int pf_level, pf_x0, pf_y0;
     {
         const float sc = ldexpf(1.f, -maxL);
-        float nx0 = (flags & PSN_LK_USE_INITIAL_FLOW) ? __fmul_rn(NPx, sc) : __fmul_rn(px0, sc);
-        float ny0 = (flags & PSN_LK_USE_INITIAL_FLOW) ? __fmul_rn(NPy, sc) : __fmul_rn(py0, sc);
-        jr_x0 = cv_floor(__fsub_rn(nx0, hwx)) - kJMargin;
-        jr_y0 = cv_floor(__fsub_rn(ny0, hwy)) - kJMargin;
-        dma_region<NT>(JR, tbl_level(TBL, 1, maxL), jr_y0, jr_x0, JRW, JRH);
+        const float nx0 = (flags & PSN_LK_USE_INITIAL_FLOW) ? __fmul_rn(NPx, sc) : __fmul_rn(px0, sc);
+        const float ny0 = (flags & PSN_LK_USE_INITIAL_FLOW) ? __fmul_rn(NPy, sc) : __fmul_rn(py0, sc);
+        pf_x0 = (cv_floor(__fsub_rn(nx0, hwx)) - kStJMargin) & ~3;
+        pf_y0 = cv_floor(__fsub_rn(ny0, hwy)) - kStJMargin;
+        pf_level = maxL;
+        pf.load(ring_level(A.ring, Q.next_slot, maxL), pf_y0, pf_x0, JRW, JRH, wk_int, wk_bord);
     }
     dma_wait();
     __syncthreads();
+    LK_STAMP(50);
+
+    // ---- A phase for ALL levels at once (the I window does not depend on the
+    // flow): Scharr of every patch; window values, tensor products and sums;
+    // one reduction barrier; wave 0 sums the float chains of every level in
+    // parallel lanes and writes the per-level solver table LV ----
+    for (int l = 0; l <= maxL; l++) {
+        const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
+        const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
+        if (!gg.valid) continue;
+        const uint32_t *P = (const uint32_t *)(smem + lay.pim + l * lay.pim_stride);
+        short2 *Dg = (short2 *)(smem + lay.dg + l * lay.dg_stride);
+        Walk wk;
+        wk.init(tid, NT, DW);
+        for (int idx = tid; idx < (h + 1) * DW; idx += NT, wk.step()) {
+            const int gy = gg.ipy + wk.y, gx = gg.ipx + wk.x;
+            short2 d = make_short2(0, 0);
+            if ((unsigned)gy < (unsigned)I.h && (unsigned)gx < (unsigned)I.w) {
+                const uint32_t *p = P + wk.y * PW + wk.x;
+                const int a0 = p[0], a1 = p[1], a2 = p[2];
+                const int b0 = p[PW], b2 = p[PW + 2];
+                const int c0 = p[2 * PW], c1 = p[2 * PW + 1], c2 = p[2 * PW + 2];
+                d.x = (short)(3 * (a2 + c2) + 10 * b2 - 3 * (a0 + c0) - 10 * b0);
+                d.y = (short)(3 * ((c0 - a0) + (c2 - a2)) + 10 * (c1 - a1));
+            }
+            Dg[idx] = d;
+        }
+    }
+    __syncthreads();
+    LK_STAMP(51);
+#pragma unroll
+    for (int l = 0; l < kStMaxLev; l++) {
+        if (l > maxL) break;
+        const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
+        const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
+        // Per-sum exactness: A11 (terms >= 0) is exact when s11 <= 2^24, A22 when
+        // s22 <= 2^24, A12 when sum|xy| <= (s11 + s22) / 2 <= 2^24; s11 and s22
+        // are reduced saturating, s12 wrapping
+        unsigned s11 = 0, s22 = 0;
+        int s12 = 0;
+        if (gg.valid) {
+            const uint32_t *P = (const uint32_t *)(smem + lay.pim + l * lay.pim_stride);
+            const short2 *Dg = (const short2 *)(smem + lay.dg + l * lay.dg_stride);
+            int2 *IW = (int2 *)(smem + lay.iw + l * lay.iw_stride);
+            float *PA = R + l * 3 * GA.P;
+#pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                const uint32_t *p = P + ofsP[k];
+                const int iw = PSN_DESCALE(__mul24((int)p[0], gg.w00) + __mul24((int)p[1], gg.w01) +
+                                               __mul24((int)p[PW], gg.w10) + __mul24((int)p[PW + 1], gg.w11), 9);
+                const short2 *d = Dg + ofsD[k];
+                const short2 d00 = d[0], d01 = d[1], d10 = d[DW], d11 = d[DW + 1];
+                int ix = PSN_DESCALE(__mul24((int)d00.x, gg.w00) + __mul24((int)d01.x, gg.w01) +
+                                         __mul24((int)d10.x, gg.w10) + __mul24((int)d11.x, gg.w11), 14);
+                int iy = PSN_DESCALE(__mul24((int)d00.y, gg.w00) + __mul24((int)d01.y, gg.w01) +
+                                         __mul24((int)d10.y, gg.w10) + __mul24((int)d11.y, gg.w11), 14);
+                if (ev[k]) IW[pix[k]] = make_int2(iw, (ix & 0xffff) | (iy << 16));
+                ix = ev[k] ? ix : 0;
+                iy = ev[k] ? iy : 0;
+                const int xx2 = __mul24(ix, ix), xy = __mul24(ix, iy), yy2 = __mul24(iy, iy);
+                PA[posA_[k]] = (float)xx2;
+                PA[GA.P + posA_[k]] = (float)xy;
+                PA[2 * GA.P + posA_[k]] = (float)yy2;
+                s11 += (unsigned)xx2;  // per thread <= 4 * 4080^2 < 2^30
+                s12 += xy;
+                s22 += (unsigned)yy2;
+            }
+        }
+        s11 = wave_sum_sat(s11);
+        s12 = wave_sum(s12);
+        s22 = wave_sum_sat(s22);
+        if (lane == 0) {
+            int *ra = RI + kStRiA + l * 4 * 8 + wid;
+            ra[0] = (int)s11;
+            ra[8] = s12;
+            ra[16] = (int)s22;
+        }
+    }
+    __syncthreads();
+    LK_STAMP(52);
+    if (wid == 0) {
+        float *CH = (float *)RI;  // 15 chain results per level (the iteration scratch is still unused)
+        // chain pass: slot q -> (level q/15, sum (q%15)/5, chain q%5); two slots per lane
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const int q = lane + 64 * half;
+            const int l = q / 15, r = q - 15 * (q / 15);
+            if (l <= maxL) {
+                unsigned a11 = 0, a22 = 0;
+#pragma unroll
+                for (int ww = 0; ww < NW; ww++) {
+                    a11 = sat_add(a11, (unsigned)RI[kStRiA + l * 32 + ww]);
+                    a22 = sat_add(a22, (unsigned)RI[kStRiA + l * 32 + 16 + ww]);
+                }
+                const int s = r / 5, ch = r - 5 * (r / 5);
+                const unsigned bound = s == 0 ? a11 : s == 2 ? a22 : (a11 + a22) >> 1;
+                float acc = 0.f;
+                if (bound > (unsigned)kExact) {
+                    const int base = (l * 3 + s) * GA.P + (ch < 4 ? ch * GA.S : 4 * GA.S);
+                    const int nb = (ch < 4 ? GA.S : GA.T) >> 4;
+                    acc = chain_sum16(R + base, nb);
+                }
+                CH[q] = acc;
+            }
+        }
+        // CH written by other lanes of this wave: LDS executes a wave's accesses in
+        // order; the clobber keeps the compiler from hoisting the reads
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane <= maxL) {
+            const int l = lane;
+            unsigned a11 = 0, a22 = 0;
+            int s12 = 0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ww++) {
+                const int *ra = RI + kStRiA + l * 32 + ww;
+                a11 = sat_add(a11, (unsigned)ra[0]);
+                s12 += ra[8];
+                a22 = sat_add(a22, (unsigned)ra[16]);
+            }
+            // a sum whose every term and every partial sum (in any order) is an
+            // integer <= 2^24 is exact in float: its integer value; otherwise the
+            // ordered chains
+            float s3[3];
+#pragma unroll
+            for (int s = 0; s < 3; s++) {
+                const float *c = CH + l * 15 + s * 5;
+                float tail = c[4];
+                if (sse) tail = __fadd_rn(tail, __fadd_rn(__fadd_rn(__fadd_rn(c[0], c[1]), c[2]), c[3]));
+                s3[s] = tail;
+            }
+            const float A11_ = a11 <= (unsigned)kExact ? (float)a11 : s3[0];
+            const float A12_ = ((a11 + a22) >> 1) <= (unsigned)kExact ? (float)s12 : s3[1];
+            const float A22_ = a22 <= (unsigned)kExact ? (float)a22 : s3[2];
+            float A11 = A11_, A12 = A12_, A22 = A22_;
+            const float FLT_SCALE = 1.f / (1 << 20);
+            A11 = __fmul_rn(A11, FLT_SCALE);
+            A12 = __fmul_rn(A12, FLT_SCALE);
+            A22 = __fmul_rn(A22, FLT_SCALE);
+            const float D = __fsub_rn(__fmul_rn(A11, A22), __fmul_rn(A12, A12));
+            const float dd = __fsub_rn(A11, A22);
+            const float t = __fadd_rn(__fmul_rn(dd, dd), __fmul_rn(__fmul_rn(4.f, A12), A12));
+            const float minEig = __fdiv_rn(__fsub_rn(__fadd_rn(A22, A11), sqrtf(t)), (float)(2 * wh));
+            const bool ok = !(minEig < Q.min_eig || D < FLT_EPSILON);
+            float *lv = LV + l * kStLvFloats;
+            lv[0] = A11;
+            lv[1] = A12;
+            lv[2] = A22;
+            lv[3] = ok ? __fdiv_rn(1.f, D) : 0.f;
+            lv[4] = minEig;
+            lv[5] = ok ? 1.f : 0.f;
+        }
+    }
+    __syncthreads();  // LV published; the A planes in R are dead from here
+    LK_STAMP(53);
+    zero_pads<NT>(R, GB, 4);  // b planes (2 buffers x 2 sums) now own R; ordered by the first iteration's barrier
 
     int status = 1;
     float errv = 0.f;
     const float FLT_SCALE = 1.f / (1 << 20);
-    LK_STAMP(60);
 #ifdef PSN_LK_STAMPS
     unsigned long long acc_ph[6] = {0, 0, 0, 0, 0, 0}, t_ph = 0;
 #define PH_BEGIN() t_ph = __builtin_amdgcn_s_memtime()
@@ -1185,23 +1481,22 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     do {            \
     } while (0)
 #endif
-    JStage<NT> js;
+    int jr_x0 = 0, jr_y0 = 0;
 
     for (int level = maxL; level >= 0; level--) {
         LK_STAMP(level * 10 + 0);
-        const LevelDev I = tbl_level(TBL, 0, level);
-        const LevelDev J = tbl_level(TBL, 1, level);
+        const LevelDev I = ring_level(A.ring, Q.prev_slot, level);
+        const LevelDev J = ring_level(A.ring, Q.next_slot, level);
         const int cols = I.w, rows = I.h;
         const float scale = ldexpf(1.f, -level);
-        float px = __fmul_rn(px0, scale), py = __fmul_rn(py0, scale);
         float nx, ny;
         if (level == maxL) {
             if (flags & PSN_LK_USE_INITIAL_FLOW) {
                 nx = __fmul_rn(NPx, scale);
                 ny = __fmul_rn(NPy, scale);
             } else {
-                nx = px;
-                ny = py;
+                nx = __fmul_rn(px0, scale);
+                ny = __fmul_rn(py0, scale);
             }
         } else {
             nx = __fmul_rn(NPx, 2.f);
@@ -1209,123 +1504,62 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         }
         NPx = nx;
         NPy = ny;
-        px = __fsub_rn(px, hwx);
-        py = __fsub_rn(py, hwy);
-        const int ipx = cv_floor(px), ipy = cv_floor(py);
-        if (ipx < -w || ipx >= cols || ipy < -h || ipy >= rows) {
+        const IGeo gg = i_geo(px0, py0, hwx, hwy, level, w, h, cols, rows);
+        const float *lv = LV + level * kStLvFloats;
+        const bool run = gg.valid && lv[5] != 0.f;
+        if (!gg.valid) {
             if (level == 0) {
                 status = 0;
                 errv = 0.f;
             }
-            continue;
+        } else {
+            if (flags & PSN_LK_GET_MIN_EIGENVALS) errv = lv[4];
+            if (!run && level == 0) status = 0;
         }
-        int iw00, iw01, iw10, iw11;
-        bilin_weights(__fsub_rn(px, (float)ipx), __fsub_rn(py, (float)ipy), iw00, iw01, iw10, iw11);
         nx = __fsub_rn(nx, hwx);
         ny = __fsub_rn(ny, hwy);
-        const bool new_jr = level < maxL;
-        if (new_jr) {  // J region of this level: loads in flight during the A-phase
-            jr_x0 = cv_floor(nx) - kJMargin;
-            jr_y0 = cv_floor(ny) - kJMargin;
-            js.load(J, jr_y0, jr_x0, JRW, JRH);
+        if (run) {
+            // this level's J region: the prefetched registers if they cover the start
+            const int inx0 = cv_floor(nx), iny0 = cv_floor(ny);
+            if (pf_level == level && inx0 >= pf_x0 && iny0 >= pf_y0 && inx0 + w + 1 <= pf_x0 + JRW &&
+                iny0 + h + 1 <= pf_y0 + JRH) {
+                pf.store(JP);
+                jr_x0 = pf_x0;
+                jr_y0 = pf_y0;
+            } else {
+                JPStage<NT> cp;
+                jr_x0 = (inx0 - kStJMargin) & ~3;
+                jr_y0 = iny0 - kStJMargin;
+                cp.copy(JP, J, jr_y0, jr_x0, JRW, JRH, wk_int, wk_bord);
+            }
         }
+        pf_level = -1;
+        if (level > 0) {  // prefetch the next level's region at its predicted start (2 x this start)
+            pf_x0 = (cv_floor(__fsub_rn(__fmul_rn(NPx, 2.f), hwx)) - kStJMargin) & ~3;
+            pf_y0 = cv_floor(__fsub_rn(__fmul_rn(NPy, 2.f), hwy)) - kStJMargin;
+            pf_level = level - 1;
+            pf.load(ring_level(A.ring, Q.next_slot, level - 1), pf_y0, pf_x0, JRW, JRH, wk_int, wk_bord);
+        }
+        if (!run) continue;
+        __syncthreads();  // JP published (every wave finished the previous level's reads)
         LK_STAMP(level * 10 + 1);
 
-        // ---- A-phase: Scharr of the staged I patch, bilinear window, tensor ----
-        const uint32_t *P = (const uint32_t *)(smem + lay.pim + level * lay.pim_stride);
-        {
-            Walk wk;
-            wk.init(tid, NT, DW);
-            for (int idx = tid; idx < (h + 1) * DW; idx += NT, wk.step()) {
-                const int gy = ipy + wk.y, gx = ipx + wk.x;
-                short2 d = make_short2(0, 0);
-                if ((unsigned)gy < (unsigned)rows && (unsigned)gx < (unsigned)cols) {
-                    const uint32_t *p = P + wk.y * PW + wk.x;
-                    const int a0 = p[0], a1 = p[1], a2 = p[2];
-                    const int b0 = p[PW], b2 = p[PW + 2];
-                    const int c0 = p[2 * PW], c1 = p[2 * PW + 1], c2 = p[2 * PW + 2];
-                    d.x = (short)(3 * (a2 + c2) + 10 * b2 - 3 * (a0 + c0) - 10 * b0);
-                    d.y = (short)(3 * ((c0 - a0) + (c2 - a2)) + 10 * (c1 - a1));
-                }
-                Dg[idx] = d;
-            }
-        }
-        __syncthreads();
-        LK_STAMP(level * 10 + 2);
+        const float A11 = lv[0], A12 = lv[1], A22 = lv[2], D = lv[3];
         int Iw_[EPT], Ix_[EPT], Iy_[EPT];
-        int sA11 = 0, sA12 = 0, sA22 = 0;
-        unsigned aA = 0;  // saturating sum of |every A term|
-#pragma unroll
-        for (int k = 0; k < EPT; k++) {
-            const uint32_t *p = P + ofsP[k];
-            Iw_[k] = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[PW] * iw10 + (int)p[PW + 1] * iw11, 9);
-            const short2 *d = Dg + ofsD[k];
-            const short2 d00 = d[0], d01 = d[1], d10 = d[DW], d11 = d[DW + 1];
-            const int ix = PSN_DESCALE(d00.x * iw00 + d01.x * iw01 + d10.x * iw10 + d11.x * iw11, 14);
-            const int iy = PSN_DESCALE(d00.y * iw00 + d01.y * iw01 + d10.y * iw10 + d11.y * iw11, 14);
-            Ix_[k] = ev[k] ? ix : 0;
-            Iy_[k] = ev[k] ? iy : 0;
-            const int xx2 = Ix_[k] * Ix_[k], xy = Ix_[k] * Iy_[k], yy2 = Iy_[k] * Iy_[k];
-            PA[posA_[k]] = (float)xx2;
-            PA[GA.P + posA_[k]] = (float)xy;
-            PA[2 * GA.P + posA_[k]] = (float)yy2;
-            sA11 += xx2;
-            sA12 += xy;
-            sA22 += yy2;
-            aA = sat_add(aA, sat_add(sat_add((unsigned)xx2, (unsigned)abs(xy)), (unsigned)yy2));
-        }
-        if (new_jr) js.store(JR);  // published by the barrier below
-        LK_STAMP(level * 10 + 3);
-        block_sums4<NT>(sA11, sA12, sA22, aA, RI + 32);
-        LK_STAMP(level * 10 + 4);
-        float A11, A12, A22;
-        if (aA <= (unsigned)kExact) {
-            // every term and every partial sum of the three sums is an integer
-            // <= 2^24: exact in float, so any summation order gives these values
-            A11 = (float)sA11;
-            A12 = (float)sA12;
-            A22 = (float)sA22;
-        } else {
-            float acc = 0.f;
-            if (lane < 15) {
-                const int ch = lane % 5, s = lane / 5;
-                const int base = s * GA.P + (ch < 4 ? ch * GA.S : 4 * GA.S);
-                const int nb = (ch < 4 ? GA.S : GA.T) >> 4;
-                acc = chain_sum16(PA + base, nb);
-            }
-            float s3[3];
-#pragma unroll
-            for (int s = 0; s < 3; s++) {
-                float tail = readlane_f(acc, s * 5 + 4);
-                if (sse) {
-                    const float q = __fadd_rn(__fadd_rn(__fadd_rn(readlane_f(acc, s * 5 + 0), readlane_f(acc, s * 5 + 1)),
-                                                        readlane_f(acc, s * 5 + 2)), readlane_f(acc, s * 5 + 3));
-                    tail = __fadd_rn(tail, q);
-                }
-                s3[s] = tail;
-            }
-            A11 = s3[0];
-            A12 = s3[1];
-            A22 = s3[2];
-        }
-        LK_STAMP(level * 10 + 5);
-        A11 = __fmul_rn(A11, FLT_SCALE);
-        A12 = __fmul_rn(A12, FLT_SCALE);
-        A22 = __fmul_rn(A22, FLT_SCALE);
-        float D = __fsub_rn(__fmul_rn(A11, A22), __fmul_rn(A12, A12));
+        unsigned Sxy[EPT];
         {
-            const float dd = __fsub_rn(A11, A22);
-            const float t = __fadd_rn(__fmul_rn(dd, dd), __fmul_rn(__fmul_rn(4.f, A12), A12));
-            const float minEig = __fdiv_rn(__fsub_rn(__fadd_rn(A22, A11), sqrtf(t)), (float)(2 * wh));
-            if (flags & PSN_LK_GET_MIN_EIGENVALS) errv = minEig;
-            if (minEig < Q.min_eig || D < FLT_EPSILON) {
-                if (level == 0) status = 0;
-                continue;
+            const int2 *IW = (const int2 *)(smem + lay.iw + level * lay.iw_stride);
+#pragma unroll
+            for (int k = 0; k < EPT; k++) {
+                const int2 t = IW[pix[k]];
+                Iw_[k] = t.x;
+                Ix_[k] = ev[k] ? (int)(short)(t.y & 0xffff) : 0;
+                Iy_[k] = ev[k] ? (t.y >> 16) : 0;
+                Sxy[k] = (unsigned)(abs(Ix_[k]) + abs(Iy_[k]));
             }
         }
-        D = __fdiv_rn(1.f, D);
+        LK_STAMP(level * 10 + 2);
         float pdx = 0.f, pdy = 0.f;
-        LK_STAMP(level * 10 + 6);
         int jdone = 0;
 
         for (int j = 0; j < Q.max_count; j++) {
@@ -1336,35 +1570,37 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 if (level == 0) status = 0;
                 break;
             }
+            int iw00, iw01, iw10, iw11;
             bilin_weights(__fsub_rn(nx, (float)inx), __fsub_rn(ny, (float)iny), iw00, iw01, iw10, iw11);
             if (!(inx >= jr_x0 && iny >= jr_y0 && inx + w + 1 <= jr_x0 + JRW && iny + h + 1 <= jr_y0 + JRH)) {
-                // every wave's JR reads of iteration j-1 precede that iteration's
+                // every wave's JP reads of iteration j-1 precede that iteration's
                 // barrier, which this wave has passed
-                jr_x0 = inx - kJMargin;
-                jr_y0 = iny - kJMargin;
-                js.load(J, jr_y0, jr_x0, JRW, JRH);
-                js.store(JR);
+                JPStage<NT> cp;
+                jr_x0 = (inx - kStJMargin) & ~3;
+                jr_y0 = iny - kStJMargin;
+                cp.copy(JP, J, jr_y0, jr_x0, JRW, JRH, wk_int, wk_bord);
                 __syncthreads();
                 PH_COUNT(5);
             }
-            const uint32_t *jb = JR + (iny - jr_y0) * JRW + (inx - jr_x0);
-            float *pb = PB + (j & 1) * 2 * GB.P;
+            const unsigned W0 = pack_w(iw00, iw01), W1 = pack_w(iw10, iw11);
+            const uint32_t *jb = JP + (iny - jr_y0) * JRW + (inx - jr_x0);
+            float *pb = R + (j & 1) * 2 * GB.P;
             int s1 = 0, s2 = 0;
             unsigned a = 0;
 #pragma unroll
             for (int k = 0; k < EPT; k++) {
                 const uint32_t *p = jb + ofsJ[k];
-                const int jv = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[JRW] * iw10 + (int)p[JRW + 1] * iw11, 9);
+                const int jv = sdot2(p[JRW], W1, sdot2(p[0], W0, 1 << 8)) >> 9;
                 const int diff = jv - Iw_[k];
-                const int t1 = diff * Ix_[k], t2 = diff * Iy_[k];
+                const int t1 = __mul24(diff, Ix_[k]), t2 = __mul24(diff, Iy_[k]);
                 pb[posB_[k]] = (float)t1;
                 pb[GB.P + posB_[k]] = (float)t2;
                 s1 += t1;
                 s2 += t2;
-                a = sat_add(a, sat_add((unsigned)abs(t1), (unsigned)abs(t2)));
+                a += (unsigned)__mul24(abs(diff), (int)Sxy[k]);  // |t1| + |t2| (both factors < 2^14); per thread < 2^30
             }
             PH_MARK(0);
-            block_sums3<NT>(s1, s2, a, RI + 16 * (j & 1));  // the iteration's barrier
+            block_sums3<NT>(s1, s2, a, RI + kStRiIt + 32 * (j & 1));  // the iteration's barrier
             PH_MARK(1);
             float b1, b2;
             if (a <= (unsigned)kExact) {
@@ -1422,34 +1658,36 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 status = 0;
                 continue;
             }
+            int iw00, iw01, iw10, iw11;
             bilin_weights(__fsub_rn(qx, (float)iqx), __fsub_rn(qy, (float)iqy), iw00, iw01, iw10, iw11);
-            __syncthreads();  // every wave is done with PA (A chains) and JR (last products)
+            __syncthreads();  // every wave is done with R (last products) and JP
             if (!(iqx >= jr_x0 && iqy >= jr_y0 && iqx + w + 1 <= jr_x0 + JRW && iqy + h + 1 <= jr_y0 + JRH)) {
-                jr_x0 = iqx - kJMargin;
-                jr_y0 = iqy - kJMargin;
-                js.load(J, jr_y0, jr_x0, JRW, JRH);
-                js.store(JR);
+                JPStage<NT> cp;
+                jr_x0 = (iqx - kStJMargin) & ~3;
+                jr_y0 = iqy - kStJMargin;
+                cp.copy(JP, J, jr_y0, jr_x0, JRW, JRH, wk_int, wk_bord);
                 __syncthreads();
             }
-            const uint32_t *jb = JR + (iqy - jr_y0) * JRW + (iqx - jr_x0);
+            const unsigned W0 = pack_w(iw00, iw01), W1 = pack_w(iw10, iw11);
+            const uint32_t *jb = JP + (iqy - jr_y0) * JRW + (iqx - jr_x0);
             int e1 = 0, e2 = 0;
             unsigned ea = 0;
 #pragma unroll
             for (int k = 0; k < EPT; k++) {
                 const uint32_t *p = jb + ofsJ[k];
-                const int jv = PSN_DESCALE((int)p[0] * iw00 + (int)p[1] * iw01 + (int)p[JRW] * iw10 + (int)p[JRW + 1] * iw11, 9);
+                const int jv = sdot2(p[JRW], W1, sdot2(p[0], W0, 1 << 8)) >> 9;
                 const int ad = ev[k] ? abs(jv - Iw_[k]) : 0;
-                PA[ofsE[k]] = (float)ad;  // row-major, for the sequential fallback
-                ea = sat_add(ea, (unsigned)ad);
+                R[ofsE[k]] = (float)ad;  // row-major, for the sequential fallback
+                ea += (unsigned)ad;
             }
-            for (int k = wh + tid; k < round16i(wh); k += NT) PA[k] = 0.f;
-            block_sums3<NT>(e1, e2, ea, RI + 48);
+            for (int k = wh + tid; k < round16i(wh); k += NT) R[k] = 0.f;
+            block_sums3<NT>(e1, e2, ea, RI + kStRiErr);
             float errval;
             if (ea <= (unsigned)kExact) {
                 errval = (float)ea;  // every partial sum of errval += |diff| is an exact integer
             } else {
                 float acc = 0.f;
-                if (lane == 0) acc = chain_sum16(PA, round16i(wh) >> 4);
+                if (lane == 0) acc = chain_sum16(R, round16i(wh) >> 4);
                 errval = readlane_f(acc, 0);
             }
             errv = __fdiv_rn(__fmul_rn(errval, 1.f), (float)(32 * wh));
@@ -1466,32 +1704,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         A.status[pi] = (uint8_t)status;
         if (A.err) A.err[pi] = errv;
     }
-    if (A.pyr_ntiles > 0) {
-        // fused next-frame ingest: this workgroup's point is done, so it pulls
-        // pyramid tiles while slower points keep iterating (fills the tail of
-        // the launch instead of a concurrent kernel on a second stream)
-        int *tile_slot = RI + 60;
-        for (;;) {
-            __syncthreads();  // every wave is done with LDS (LK state / previous tile)
-            if (tid == 0) tile_slot[0] = (int)atomicAdd(&A.pyr_ctr[0], 1u);
-            __syncthreads();
-            const int tile = tile_slot[0];
-            if (tile >= A.pyr_ntiles) break;
-            const int by = tile / A.pyr_tiles_x, bx = tile - by * A.pyr_tiles_x;
-            // the tile's LDS starts past the reduce scratch that holds tile_slot
-            pyr_tile<NT>(A.pyr, bx, by, smem + lay.jr);
-        }
-        if (tid == 0) {
-            // the last workgroup to finish resets the counters for the next launch;
-            // every workgroup has stopped pulling tiles before it counts itself done
-            __threadfence();
-            const unsigned done = atomicAdd(&A.pyr_ctr[1], 1u);
-            if (done == (unsigned)A.total_wgs - 1) {
-                A.pyr_ctr[0] = 0;
-                A.pyr_ctr[1] = 0;
-            }
-        }
-    }
+    if (A.pyr_ntiles > 0) pyr_tail<NT>(A, smem);
 }
 #undef PH_BEGIN
 #undef PH_MARK
@@ -1508,6 +1721,8 @@ hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_
             case 1282: hipLaunchKernelGGL((lk_kernel_st<128, 2>), grid, dim3(128), lds_bytes, s, a); break;
             case 1284: hipLaunchKernelGGL((lk_kernel_st<128, 4>), grid, dim3(128), lds_bytes, s, a); break;
             case 2562: hipLaunchKernelGGL((lk_kernel_st<256, 2>), grid, dim3(256), lds_bytes, s, a); break;
+            case 5121: hipLaunchKernelGGL((lk_kernel_st<512, 1>), grid, dim3(512), lds_bytes, s, a); break;
+            case 5122: hipLaunchKernelGGL((lk_kernel_st<512, 2>), grid, dim3(512), lds_bytes, s, a); break;
             default: hipLaunchKernelGGL((lk_kernel_st<256, 4>), grid, dim3(256), lds_bytes, s, a); break;
         }
     } else {
@@ -1528,7 +1743,8 @@ hipError_t lk_kernels_init() {
     if ((e = hipFuncSetAttribute((const void *)lk_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     const void *st[] = {(const void *)lk_kernel_st<64, 2>,  (const void *)lk_kernel_st<64, 4>,
                         (const void *)lk_kernel_st<128, 2>, (const void *)lk_kernel_st<128, 4>,
-                        (const void *)lk_kernel_st<256, 2>, (const void *)lk_kernel_st<256, 4>};
+                        (const void *)lk_kernel_st<256, 2>, (const void *)lk_kernel_st<256, 4>,
+                        (const void *)lk_kernel_st<512, 1>, (const void *)lk_kernel_st<512, 2>};
     for (const void *f : st)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)pyramid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;

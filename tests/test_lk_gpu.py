@@ -241,7 +241,7 @@ def test_lk_device_pointer_path(oracle_mod, overlap):
     assert_same(gpu, ref, "device path")
 
 
-@pytest.mark.parametrize("env", [{}, {"PSN_LK_THREADS": "128"}, {"PSN_LK_THREADS": "64"}])
+@pytest.mark.parametrize("env", [{}, {"PSN_LK_THREADS": "128"}, {"PSN_LK_THREADS": "64"}, {"PSN_LK_THREADS": "512"}])
 @pytest.mark.parametrize("win", [(21, 21), (9, 9), (64, 64)])
 def test_lk_fused_ingest_pipeline(oracle_mod, monkeypatch, env, win):
     """Fused ingest (PSN_LK_OVERLAP_FUSED): frame t+1 is pushed before frame t
@@ -291,7 +291,7 @@ def test_lk_config5_4k_5level(oracle_mod):
 
 
 @pytest.mark.parametrize("env", [{"PSN_LK_GENERIC": "1"}, {"PSN_LK_THREADS": "64"}, {"PSN_LK_THREADS": "128"},
-                                 {"PSN_LK_GENERIC": "1", "PSN_LK_THREADS": "64"}])
+                                 {"PSN_LK_THREADS": "512"}, {"PSN_LK_GENERIC": "1", "PSN_LK_THREADS": "64"}])
 @pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
 def test_lk_kernel_variants(oracle_mod, monkeypatch, env, flags):
     """The single-tile and the tiled kernel, at every workgroup size, give the

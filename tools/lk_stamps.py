@@ -20,7 +20,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from mcmtt_opticalflow_amd import _lib, lk, synth  # noqa: E402
 import hiprt  # noqa: E402
 
-PH = ["slot_load", "stage", "scharr", "iwin", "a_reduce", "a_chain_eig", "iters"]
+PRO = ["prologue_dma", "scharr_all", "a_products_reduce", "a_chains_eig"]  # stamps 60->50->51->52->53
+PH = ["level_setup_j_stage", "window_load", "iters"]  # per level: 0->1->2->7
 
 
 def main():
@@ -45,14 +46,19 @@ def main():
            "kernel_span_cycles": float(s[:, 61].max() - s[:, 60].min()),
            "start_spread_cycles": float(s[:, 60].max() - s[:, 60].min())}
     slow = int(np.argmax(tot))
+    pro = np.stack([s[:, 50] - s[:, 60], s[:, 51] - s[:, 50], s[:, 52] - s[:, 51], s[:, 53] - s[:, 52]], 1)
+    out["prologue_a_phase"] = {"mean": {k: round(float(v), 1) for k, v in zip(PRO, pro.mean(0))},
+                               "slowest_wg": {k: int(v) for k, v in zip(PRO, pro[slow])}}
+    prev_end = s[:, 53]
     for lev in range(3, -1, -1):
         b = lev * 10
-        d = np.diff(s[:, b:b + 8], axis=1)  # phases 0..6
+        d = np.stack([s[:, b + 1] - prev_end, s[:, b + 2] - s[:, b + 1], s[:, b + 7] - s[:, b + 2]], 1)
+        prev_end = s[:, b + 7]
         iters = s[:, b + 8]
         out[f"L{lev}"] = {
             "mean": {k: round(float(v), 1) for k, v in zip(PH, d.mean(0))},
             "iters_mean": float(iters.mean()), "iters_max": int(iters.max()),
-            "cycles_per_iter": round(float(d[:, 6].sum() / max(iters.sum(), 1)), 1),
+            "cycles_per_iter": round(float(d[:, 2].sum() / max(iters.sum(), 1)), 1),
             "slowest_wg": {k: int(v) for k, v in zip(PH, d[slow])} | {"iters": int(iters[slow])},
         }
     it = s[:, 40:46]
@@ -62,6 +68,15 @@ def main():
         "products": round(float(it[:, 0].sum() / tot_it), 1), "reduce_barrier": round(float(it[:, 1].sum() / tot_it), 1),
         "chain_combine": round(float(it[:, 2].sum() / tot_it), 1), "solve": round(float(it[:, 3].sum() / tot_it), 1),
         "chain_path_fraction": round(float(it[:, 4].sum() / tot_it), 3), "restage_fraction": round(float(it[:, 5].sum() / tot_it), 3)}
+    t0 = s[:, 60].min()
+    ends = (s[:, 61] - t0) / 1e3
+    out["wg_end_kcycles_percentiles"] = {str(q): round(float(np.percentile(ends, q)), 1) for q in (10, 50, 90, 99, 100)}
+    out["wg_iterations_percentiles"] = {str(q): float(np.percentile(n_it, q)) for q in (10, 50, 90, 99, 100)}
+    # per-iteration cost of the slowest workgroups (they run mostly alone in the tail)
+    order = np.argsort(tot)[-8:]
+    out["slowest8"] = [{"wg_kcycles": round(float(tot[i]) / 1e3, 1), "iters": int(n_it[i]),
+                        "iter_cycles": round(float(sum(s[i, l * 10 + 7] - s[i, l * 10 + 2] for l in range(4)) / max(n_it[i], 1)), 1),
+                        "chain_frac": round(float(s[i, 44]) / max(n_it[i], 1), 2)} for i in order]
     print(json.dumps(out, indent=1))
 
 
