@@ -1,0 +1,407 @@
+// Tracker2D flow stage (see tracker2d_flow.hpp). Reference lines cited are in
+// psn_where/PSNWhere_Tracker2D.cpp unless noted.
+#include "tracker2d_flow.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+
+namespace psn {
+
+// :452-554. Vectors with |d| >= 0.1 px vote; if fewer than half the points
+// move, the box stays put with no inliers. Otherwise the mode of dx and of dy
+// (most neighbours within 0.2 box widths, first maximum in sorted order) is
+// the box shift and the inliers are the moving vectors within that window of
+// the mode, in point order.
+Rect LocalSearchKLT(Rect preBox, const std::vector<Point2f> &preFeatures, const std::vector<Point2f> &curFeatures,
+                    std::vector<size_t> &inlierFeatureIndex) {
+    const double kMinMovement = 0.1, kNeighborRatio = 0.2;
+    const size_t numFeatures = preFeatures.size();
+    size_t numMoving = 0;
+    inlierFeatureIndex.clear();
+    std::vector<Point2D> vecMoving;
+    std::vector<size_t> vecMovingIdx;
+    std::vector<double> vecDx, vecDy;
+    for (size_t i = 0; i < numFeatures; i++) {
+        // cv::Point2f difference (float), then widened to PSN_Point2D
+        const Point2f d{curFeatures[i].x - preFeatures[i].x, curFeatures[i].y - preFeatures[i].y};
+        const Point2D mv(d);
+        if (mv.norm_L2() < kMinMovement * kFlowScale) continue;
+        vecMoving.push_back(mv);
+        vecMovingIdx.push_back(i);
+        vecDx.push_back(mv.x);
+        vecDy.push_back(mv.y);
+        numMoving++;
+    }
+    if ((double)numMoving < (double)numFeatures * 0.5) return preBox;
+    std::sort(vecDx.begin(), vecDx.end());
+    std::sort(vecDy.begin(), vecDy.end());
+    const double windowSize = preBox.w * kNeighborRatio * kFlowScale;
+    size_t maxX = 0, maxY = 0;
+    Point2D est(0.0, 0.0);
+    for (size_t d = 0; d < numMoving; d++) {
+        size_t nx = 0, ny = 0;
+        for (size_t c = 0; c < numMoving; c++) {
+            if (std::abs(vecDx[d] - vecDx[c]) < windowSize) nx++;
+            if (std::abs(vecDy[d] - vecDy[c]) < windowSize) ny++;
+        }
+        if (maxX < nx) {
+            est.x = vecDx[d];
+            maxX = nx;
+        }
+        if (maxY < ny) {
+            est.y = vecDy[d];
+            maxY = ny;
+        }
+    }
+    for (size_t v = 0; v < numMoving; v++)
+        if ((vecMoving[v] - est).norm_L2() < windowSize) inlierFeatureIndex.push_back(vecMovingIdx[v]);
+    Rect box = preBox;
+    box.x += est.x;
+    box.y += est.y;
+    return box;
+}
+
+// :600-613
+double BoxMatchingCost(const Rect &box1, const Rect &box2) {
+    const double nom = (box1.center() - box2.center()).norm_L2();
+    const double den = (box1.w + box2.w) / 2.0;
+    return (nom * nom) / (den * den);
+}
+
+// :1231-1257 (PSN_2D_DEBUG_DISPLAY_SCALE = 1.0: the float scaling is exact)
+void ResultWithTracker(const Tracker2D &tracker, Object2DInfo &out) {
+    const float s = 1.0f;
+    out.featurePointsPrev = tracker.featurePoints;
+    out.featurePointsCurr = tracker.trackedPoints;
+    out.id = tracker.id;
+    const Rect &b = tracker.boxes.back(), &h = tracker.heads.back();
+    out.box = Rect(b.x * s, b.y * s, b.w * s, b.h * s);
+    out.head = Rect(h.x * s, h.y * s, h.w * s, h.h * s);
+    out.score = 0;
+    for (size_t i = 0; i < out.featurePointsPrev.size(); i++) {
+        out.featurePointsPrev[i].x *= s;
+        out.featurePointsPrev[i].y *= s;
+        if (i >= out.featurePointsCurr.size()) continue;
+        out.featurePointsCurr[i].x *= s;
+        out.featurePointsCurr[i].y *= s;
+    }
+}
+
+int Tracker2DFlow::fail(int rc, const char *what) {
+    err_ = std::string(what) + ": " + (lk_ ? psn_lk_last_error(lk_) : "no context") + " (" + std::to_string(rc) + ")";
+    return rc;
+}
+
+int Tracker2DFlow::Initialize(unsigned camID, int width, int height, int device) {
+    Finalize();
+    camID_ = camID;
+    width_ = width;
+    height_ = height;
+    // 4 slots of full pyramids; the reference's default maxLevel 3 needs 4 levels
+    const int rc = psn_lk_create(device, width, height, kT2dInterval, 3, &lk_);
+    if (rc) {
+        lk_ = nullptr;
+        err_ = "psn_lk_create failed (" + std::to_string(rc) + ")";
+        return rc;
+    }
+    for (int i = 0; i < kT2dInterval; i++) {
+        ring_[i] = i;
+        filled_[i] = false;
+    }
+    return PSN_LK_OK;
+}
+
+void Tracker2DFlow::Finalize() {
+    if (lk_) psn_lk_destroy(lk_);
+    lk_ = nullptr;
+}
+
+int Tracker2DFlow::PushFrame(const uint8_t *frame, int stride, int channels) {
+    if (!lk_) return PSN_LK_ERR_ARG;
+    const int slot = ring_[kT2dInterval - 1];
+    const int rc = psn_lk_push_frame(lk_, slot, frame, stride, channels);
+    if (rc) return fail(rc, "psn_lk_push_frame");
+    filled_[slot] = true;
+    return PSN_LK_OK;
+}
+
+void Tracker2DFlow::RotateRing() { std::rotate(ring_, ring_ + 1, ring_ + kT2dInterval); }
+
+// One launch for all jobs: points concatenated, one query per job. err is
+// requested as the reference does (:781, :876): its bounds re-check can clear
+// status.
+int Tracker2DFlow::RunJobs(std::vector<Job> &jobs) {
+    size_t n = 0;
+    queries_.clear();
+    for (const Job &j : jobs) {
+        psn_lk_query q;
+        q.prev_slot = j.prev_slot;
+        q.next_slot = j.next_slot;
+        q.first_pt = (int)n;
+        q.num_pts = (int)j.in->size();
+        psn_lk_default_params(&q.params);  // maxLevel 3, (COUNT|EPS, 30, 0.01), minEig 1e-4
+        q.params.win_w = j.win_w;
+        q.params.win_h = j.win_h;
+        queries_.push_back(q);
+        n += j.in->size();
+    }
+    if (queries_.empty()) return PSN_LK_OK;
+    xy_in_.resize(2 * n);
+    xy_out_.resize(2 * n);
+    err_out_.resize(n);
+    st_out_.resize(n);
+    size_t o = 0;
+    for (const Job &j : jobs)
+        for (const Point2f &p : *j.in) {
+            xy_in_[2 * o] = p.x;
+            xy_in_[2 * o + 1] = p.y;
+            o++;
+        }
+    const int rc = psn_lk_track(lk_, queries_.data(), (int)queries_.size(), xy_in_.data(), xy_out_.data(),
+                                st_out_.data(), err_out_.data());
+    if (rc) return fail(rc, "psn_lk_track");
+    o = 0;
+    for (Job &j : jobs) {
+        const size_t m = j.in->size();
+        j.out->resize(m);
+        j.status->resize(m);
+        for (size_t i = 0; i < m; i++, o++) {
+            (*j.out)[i] = Point2f{xy_out_[2 * o], xy_out_[2 * o + 1]};
+            (*j.status)[i] = st_out_[o];
+        }
+    }
+    return PSN_LK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Backward chain (:690-838)
+// ---------------------------------------------------------------------------
+
+void Tracker2DFlow::BackwardBegin(const std::vector<Detection> &dets,
+                                  const std::vector<std::vector<Point2f>> &features, std::vector<DetectedObject> &out,
+                                  std::vector<Chain> &chains) {
+    out.clear();
+    chains.clear();
+    for (size_t i = 0; i < dets.size(); i++) {
+        DetectedObject o;
+        o.id = (unsigned)i;  // detectionID counts every detection past the height gate (:718)
+        o.detection = dets[i];
+        o.boxes.push_back(dets[i].box);
+        const std::vector<Point2f> &f = features[i];
+        if (f.size() < kT2dMinFeatures) continue;  // :744
+        Chain c;
+        c.curr.assign(f.begin(), f.begin() + std::min(f.size(), kT2dMaxFeatures));  // :753-757
+        c.obj = out.size();
+        c.active = true;
+        out.push_back(std::move(o));
+        chains.push_back(std::move(c));
+    }
+}
+
+// step s tracks frame t-s+1 -> t-s; it exists while the older ring slot holds a frame
+bool Tracker2DFlow::StepAvailable(int step) const {
+    return step < kT2dInterval && filled_[ring_[kT2dInterval - 1 - step]];
+}
+
+void Tracker2DFlow::BackwardJobs(int step, std::vector<Chain> &chains, const std::vector<DetectedObject> &out,
+                                 std::vector<Job> &jobs) {
+    for (Chain &c : chains) {
+        if (!c.active) continue;
+        const Rect box = out[c.obj].detection.box.scale(kFlowScale);
+        const int win = (int)(box.w * kWinSizeRatio);  // square window of the box width (:782)
+        jobs.push_back(Job{ring_[kT2dInterval - step], ring_[kT2dInterval - 1 - step], win, win, &c.curr, &c.prev,
+                           &c.status});
+    }
+}
+
+void Tracker2DFlow::BackwardStepDone(std::vector<Chain> &chains, std::vector<DetectedObject> &out) {
+    std::vector<size_t> inl;
+    for (Chain &c : chains) {
+        if (!c.active) continue;
+        DetectedObject &o = out[c.obj];
+        // status is ignored: every nextPts value feeds LocalSearchKLT (:787)
+        const Rect newRect = LocalSearchKLT(o.detection.box.scale(kFlowScale), c.curr, c.prev, inl);
+        if (inl.size() < kT2dMinFeatures) {  // :788
+            c.active = false;
+            continue;
+        }
+        o.boxes.push_back(newRect.scale(1.0 / kFlowScale));
+        if (o.vecvecTrackedFeatures.empty()) {
+            std::vector<Point2f> cur;
+            for (size_t k : inl) cur.push_back(c.curr[k]);
+            o.vecvecTrackedFeatures.push_back(cur);
+        }
+        std::vector<Point2f> next;
+        next.reserve(inl.size());
+        for (size_t k : inl) next.push_back(c.prev[k]);
+        o.vecvecTrackedFeatures.push_back(next);
+        c.curr.swap(next);
+    }
+}
+
+void Tracker2DFlow::BackwardEnd(std::vector<Chain> &chains, std::vector<DetectedObject> &out) {
+    for (Chain &c : chains)
+        if (out[c.obj].vecvecTrackedFeatures.empty()) out[c.obj].vecvecTrackedFeatures.push_back(c.curr);  // :815-818
+    // overlap flags (:824-835)
+    for (size_t a = 0; a < out.size(); a++) {
+        if (out[a].bOverlapWithOtherDetection) continue;
+        for (size_t b = a + 1; b < out.size(); b++)
+            if (out[a].detection.box.overlap(out[b].detection.box)) {
+                out[a].bOverlapWithOtherDetection = true;
+                break;
+            }
+    }
+}
+
+int Tracker2DFlow::BackwardFeatureTracking(const std::vector<Detection> &dets,
+                                           const std::vector<std::vector<Point2f>> &features,
+                                           std::vector<DetectedObject> &out) {
+    if (!lk_ || features.size() != dets.size()) return PSN_LK_ERR_ARG;
+    std::vector<Chain> chains;
+    BackwardBegin(dets, features, out, chains);
+    std::vector<Job> jobs;
+    for (int step = 1; StepAvailable(step); step++) {
+        jobs.clear();
+        BackwardJobs(step, chains, out, jobs);
+        if (jobs.empty()) break;
+        int rc = RunJobs(jobs);
+        if (rc) return rc;
+        BackwardStepDone(chains, out);
+    }
+    BackwardEnd(chains, out);
+    return PSN_LK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Forward tracking + matching score (:851-1025)
+// ---------------------------------------------------------------------------
+
+void Tracker2DFlow::ForwardJobs(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
+                                std::vector<Job> &jobs) {
+    status.assign(trackers.size(), {});
+    for (size_t t = 0; t < trackers.size(); t++) {
+        Tracker2D *tr = trackers[t];
+        tr->trackedPoints.clear();
+        const Rect cur = tr->boxes.back().scale(kFlowScale);
+        jobs.push_back(Job{ring_[kT2dInterval - 2], ring_[kT2dInterval - 1], (int)(cur.w * kWinSizeRatio),
+                           (int)(cur.h * kWinSizeRatio), &tr->featurePoints, &tr->trackedPoints, &status[t]});
+    }
+}
+
+void Tracker2DFlow::ForwardDone(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
+                                const std::vector<DetectedObject> &dets, std::vector<float> &cost) {
+    const double kBoxMaxDistance = 1.0, kMinOverlapRatio = 0.3, kMaxCenterDiffRatio = 0.5, kMajority = 0.5;
+    const size_t T = trackers.size(), D = dets.size();
+    const float inf = std::numeric_limits<float>::infinity();
+    cost.assign(D * T, inf);
+    std::vector<std::deque<int>> inBox(D);
+    std::vector<size_t> inl;
+    for (size_t t = 0; t < T; t++) {
+        Tracker2D *tr = trackers[t];
+        std::vector<Point2f> vPrev, vCurr;
+        for (size_t i = 0; i < status[t].size(); i++) {  // keep status == 1 (:883-888)
+            if (!status[t][i]) continue;
+            vPrev.push_back(tr->featurePoints[i]);
+            vCurr.push_back(tr->trackedPoints[i]);
+        }
+        if (vCurr.size() < kT2dMinFeatures) continue;  // :889 (featurePoints kept, trackedPoints = raw output)
+        Rect newBox = LocalSearchKLT(tr->boxes.back().scale(kFlowScale), vPrev, vCurr, inl);
+        newBox = newBox.scale(1.0 / kFlowScale);
+        tr->boxes.push_back(newBox);
+        tr->heads.push_back(tr->heads.empty() ? Rect() : tr->heads.back());
+        for (size_t d = 0; d < D; d++) {
+            const DetectedObject &det = dets[d];
+            const size_t pos = d * T + t;
+            if (!newBox.overlap(det.detection.box)) continue;
+            for (const Point2f &p : tr->trackedPoints)  // the raw LK output (:914-918)
+                if (det.detection.box.contain(p)) inBox[d].push_back((int)t);
+            double boxCost = 0.0;
+            const size_t len = std::min((size_t)kT2dInterval, std::min(tr->boxes.size(), det.boxes.size()));
+            size_t tb = (size_t)tr->duration;  // duration = #boxes - 1
+            for (size_t b = 0; b < len; b++, tb--) {
+                const Rect &db = det.boxes[b], &trb = tr->boxes[tb];
+                if (!db.overlap(trb) || kBoxMaxDistance < db.distance(trb) ||
+                    kMinOverlapRatio > db.overlappedArea(trb) / std::min(db.area(), trb.area()) ||
+                    kMaxCenterDiffRatio * std::max(db.w, trb.w) < (db.center() - trb.center()).norm_L2()) {
+                    boxCost = std::numeric_limits<double>::infinity();
+                    break;
+                }
+                boxCost += BoxMatchingCost(trb, db);
+            }
+            if (std::numeric_limits<double>::infinity() == boxCost) continue;
+            boxCost /= (double)len;
+            cost[pos] = (float)boxCost;
+        }
+        tr->featurePoints = vPrev;  // :977-978
+        tr->trackedPoints = vCurr;
+    }
+    // feature-point majority check (:982-1022), run lengths as the reference counts them
+    for (size_t d = 0; d < D; d++) {
+        const std::deque<int> &f = inBox[d];
+        if (f.empty()) continue;
+        int nMajor = 0, nCur = 0;
+        int major = f.front(), cur = f.front();
+        for (size_t k = 0; k < f.size(); k++) {
+            if (cur == f[k]) {
+                nCur++;
+                continue;
+            }
+            if (nCur > nMajor) {
+                major = cur;
+                nMajor = nCur;
+            }
+            cur = f[k];
+            nCur = 0;
+        }
+        (void)major;
+        if (f.front() == cur) nMajor = nCur;  // sole tracker
+        if ((double)nMajor > (double)f.size() * kMajority) continue;
+        for (size_t t = 0; t < T; t++) cost[d * T + t] = inf;
+    }
+}
+
+int Tracker2DFlow::ForwardTrackingAndGetMatchingScore(const std::vector<Tracker2D *> &trackers,
+                                                      const std::vector<DetectedObject> &dets,
+                                                      std::vector<float> &cost) {
+    if (!lk_) return PSN_LK_ERR_ARG;
+    std::vector<std::vector<uint8_t>> status;
+    std::vector<Job> jobs;
+    if (!trackers.empty() && !StepAvailable(1)) return PSN_LK_ERR_SLOT;  // no frame t-1
+    ForwardJobs(trackers, status, jobs);
+    int rc = RunJobs(jobs);
+    if (rc) return rc;
+    ForwardDone(trackers, status, dets, cost);
+    return PSN_LK_OK;
+}
+
+int Tracker2DFlow::TrackFrame(const std::vector<Detection> &dets, const std::vector<std::vector<Point2f>> &features,
+                              std::vector<DetectedObject> &out, const std::vector<Tracker2D *> &trackers,
+                              std::vector<float> &cost) {
+    if (!lk_ || features.size() != dets.size()) return PSN_LK_ERR_ARG;
+    if (!trackers.empty() && !StepAvailable(1)) return PSN_LK_ERR_SLOT;
+    std::vector<Chain> chains;
+    BackwardBegin(dets, features, out, chains);
+    std::vector<std::vector<uint8_t>> fstatus;
+    std::vector<Job> jobs;
+    // launch 1: backward step 1 of every detection + every forward call
+    if (StepAvailable(1)) BackwardJobs(1, chains, out, jobs);
+    const size_t nb = jobs.size();
+    ForwardJobs(trackers, fstatus, jobs);
+    int rc = RunJobs(jobs);
+    if (rc) return rc;
+    if (nb) BackwardStepDone(chains, out);
+    for (int step = 2; nb && StepAvailable(step); step++) {
+        jobs.clear();
+        BackwardJobs(step, chains, out, jobs);
+        if (jobs.empty()) break;
+        rc = RunJobs(jobs);
+        if (rc) return rc;
+        BackwardStepDone(chains, out);
+    }
+    BackwardEnd(chains, out);
+    ForwardDone(trackers, fstatus, out, cost);
+    return PSN_LK_OK;
+}
+
+}  // namespace psn

@@ -1,0 +1,255 @@
+"""oracle/tracker2d_oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+Plain-Python restatement of the Tracker2D flow stage of
+psn_where/PSNWhere_Tracker2D.cpp, run in the reference's own schedule (one
+calcOpticalFlowPyrLK per detection per chain step and per tracker, each on
+full frames through oracle.calc_optical_flow_pyr_lk):
+  local_search_klt        :452-554
+  box_matching_cost       :600-613
+  backward_tracking       :690-838
+  forward_tracking        :851-1025
+and PSN_Rect arithmetic (PSNWhere_Types.h:112-182). Python floats are IEEE
+doubles (the reference's double math); cv::Point2f differences are float32.
+Only tests import this module.
+
+PARITY UNPINNED (the reference ships no tests or fixtures for this path).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+import oracle as lk_oracle
+
+MIN_FEATURES = 4     # PSN_2D_FEATURE_MIN_NUM_TRACK (:12)
+MAX_FEATURES = 100   # PSN_2D_FEATURE_MAX_NUM_TRACK (:13)
+INTERVAL = 4         # PSN_2D_BACKTRACKING_INTERVAL (:16)
+SCALE = 1.0          # PSN_2D_OPTICALFLOW_SCALE (:18)
+WIN_RATIO = 1.0      # PSN_2D_FEATURE_WIN_SIZE_RATIO (:15)
+
+
+class Rect:
+    __slots__ = ("x", "y", "w", "h")
+
+    def __init__(self, x, y, w, h):
+        self.x, self.y, self.w, self.h = float(x), float(y), float(w), float(h)
+
+    def tuple(self):
+        return (self.x, self.y, self.w, self.h)
+
+    def center(self):  # ceil(w/2) (PSNWhere_Types.h:132)
+        return (self.x + math.ceil(self.w / 2.0), self.y + math.ceil(self.h / 2.0))
+
+    def scale(self, s):
+        return Rect(self.x * s, self.y * s, self.w * s, self.h * s)
+
+    def area(self):
+        return self.w * self.h
+
+    def contain(self, px, py):  # cv::Point2f overload
+        px, py = float(np.float32(px)), float(np.float32(py))
+        return px >= self.x and px < self.x + self.w and py >= self.y and py < self.y + self.h
+
+    def overlap(self, a):  # strict '<' (:161-164)
+        return (max(self.x + self.w, a.x + a.w) - min(self.x, a.x) < self.w + a.w) and \
+               (max(self.y + self.h, a.y + a.h) - min(self.y, a.y) < self.h + a.h)
+
+    def distance(self, a):  # (:165-170)
+        dx = (self.x + self.w / 2.0) - (a.x + a.w / 2.0)
+        dy = (self.y + self.h / 2.0) - (a.y + a.h / 2.0)
+        dz = self.w - a.w
+        return math.sqrt(dx * dx + dy * dy + dz * dz) / min(self.w, a.w)
+
+    def overlapped_area(self, a):  # (:171-178)
+        ow = min(self.x + self.w, a.x + a.w) - max(self.x, a.x)
+        if 0.0 >= ow:
+            return 0.0
+        oh = min(self.y + self.h, a.y + a.h) - max(self.y, a.y)
+        if 0.0 >= oh:
+            return 0.0
+        return ow * oh
+
+
+def local_search_klt(pre_box: Rect, pre: np.ndarray, cur: np.ndarray):
+    """:452-554 -> (box, inlier indices)."""
+    pre = np.asarray(pre, np.float32).reshape(-1, 2)
+    cur = np.asarray(cur, np.float32).reshape(-1, 2)
+    n = len(pre)
+    moving, idx, dxs, dys = [], [], [], []
+    for i in range(n):
+        d = cur[i] - pre[i]  # cv::Point2f - cv::Point2f (float32)
+        mx, my = float(d[0]), float(d[1])
+        if math.sqrt(mx * mx + my * my) < 0.1 * SCALE:
+            continue
+        moving.append((mx, my))
+        idx.append(i)
+        dxs.append(mx)
+        dys.append(my)
+    m = len(moving)
+    if float(m) < float(n) * 0.5:
+        return Rect(*pre_box.tuple()), []
+    dxs.sort()
+    dys.sort()
+    window = pre_box.w * 0.2 * SCALE
+    max_x = max_y = 0
+    ex = ey = 0.0
+    for d in range(m):
+        nx = sum(1 for c in range(m) if abs(dxs[d] - dxs[c]) < window)
+        ny = sum(1 for c in range(m) if abs(dys[d] - dys[c]) < window)
+        if max_x < nx:
+            ex, max_x = dxs[d], nx
+        if max_y < ny:
+            ey, max_y = dys[d], ny
+    inl = []
+    for v in range(m):
+        vx, vy = moving[v][0] - ex, moving[v][1] - ey
+        if math.sqrt(vx * vx + vy * vy) < window:
+            inl.append(idx[v])
+    box = Rect(*pre_box.tuple())
+    box.x += ex
+    box.y += ey
+    return box, inl
+
+
+def _norm(dx, dy):  # PSN_Point2D::norm_L2: sqrt(x*x + y*y)
+    return math.sqrt(dx * dx + dy * dy)
+
+
+def box_matching_cost(b1: Rect, b2: Rect) -> float:
+    c1, c2 = b1.center(), b2.center()
+    dx, dy = c1[0] - c2[0], c1[1] - c2[1]
+    nom = math.sqrt(dx * dx + dy * dy)
+    den = (b1.w + b2.w) / 2.0
+    return (nom * nom) / (den * den)
+
+
+def _lk(prev_img, next_img, pts, win):
+    pts = np.asarray(pts, np.float32).reshape(-1, 2)
+    if len(pts) == 0:
+        return np.zeros((0, 2), np.float32), np.zeros(0, np.uint8)
+    nxt, st, _ = lk_oracle.calc_optical_flow_pyr_lk(prev_img, next_img, pts, win, 3)  # err requested (:781)
+    return nxt, st
+
+
+class DetectedObject:
+    def __init__(self, id_, box: Rect):
+        self.id = id_
+        self.box = box
+        self.boxes = [box]
+        self.sets = []
+        self.overlap_other = False
+
+
+def backward_tracking(ring, dets, features):
+    """:690-838. ring: 4 gray frames oldest first (None = empty slot), ring[-1]
+    = frame t; dets: height-validated boxes; features: points at t per
+    detection (after shuffle + cap). Returns m_vecDetection2D."""
+    out = []
+    for i, box in enumerate(dets):
+        obj = DetectedObject(i, box)
+        f = np.asarray(features[i], np.float32).reshape(-1, 2)
+        if len(f) < MIN_FEATURES:
+            continue
+        curr = f[:MAX_FEATURES].copy()
+        cur_img = ring[-1]
+        for s in range(1, INTERVAL):
+            prev_img = ring[-1 - s]
+            if prev_img is None:
+                break
+            rbox = box.scale(SCALE)
+            win = int(rbox.w * WIN_RATIO)
+            prev_pts, _status = _lk(cur_img, prev_img, curr, (win, win))  # status ignored (:787)
+            new_rect, inl = local_search_klt(rbox, curr, prev_pts)
+            if len(inl) < MIN_FEATURES:
+                break
+            obj.boxes.append(new_rect.scale(1.0 / SCALE))
+            if not obj.sets:
+                obj.sets.append(curr[inl].copy())
+            curr = prev_pts[inl].copy()
+            obj.sets.append(curr.copy())
+            cur_img = prev_img
+        if not obj.sets:
+            obj.sets.append(curr.copy())
+        out.append(obj)
+    for a in range(len(out)):
+        if out[a].overlap_other:
+            continue
+        for b in range(a + 1, len(out)):
+            if out[a].box.overlap(out[b].box):
+                out[a].overlap_other = True
+                break
+    return out
+
+
+class Tracker:
+    def __init__(self, boxes, features, duration=None):
+        self.boxes = [Rect(*b) if not isinstance(b, Rect) else b for b in boxes]
+        self.duration = len(self.boxes) if duration is None else duration
+        self.features = np.asarray(features, np.float32).reshape(-1, 2)
+        self.tracked = np.zeros((0, 2), np.float32)
+        self.updated = False
+
+
+def forward_tracking(ring, trackers, dets):
+    """:851-1025. Returns the matching cost [len(dets) x len(trackers)] (float32)."""
+    T, D = len(trackers), len(dets)
+    cost = np.full((D, T), np.inf, np.float32)
+    in_box = [[] for _ in range(D)]
+    prev_img, cur_img = ring[-2], ring[-1]
+    for t, tr in enumerate(trackers):
+        rect = tr.boxes[-1].scale(SCALE)
+        tr.tracked, status = _lk(prev_img, cur_img, tr.features, (int(rect.w * WIN_RATIO), int(rect.h * WIN_RATIO)))
+        keep = [i for i in range(len(status)) if status[i]]
+        v_prev, v_curr = tr.features[keep].copy(), tr.tracked[keep].copy()
+        tr.updated = False
+        if len(v_curr) < MIN_FEATURES:
+            continue
+        new_box, _ = local_search_klt(tr.boxes[-1].scale(SCALE), v_prev, v_curr)
+        new_box = new_box.scale(1.0 / SCALE)
+        tr.boxes.append(new_box)
+        tr.updated = True
+        for d, det in enumerate(dets):
+            if not new_box.overlap(det.box):
+                continue
+            for p in tr.tracked:  # the raw LK output (:914-918)
+                if det.box.contain(p[0], p[1]):
+                    in_box[d].append(t)
+            box_cost = 0.0
+            length = min(INTERVAL, min(len(tr.boxes), len(det.boxes)))
+            tb = tr.duration
+            for b in range(length):
+                db, tbx = det.boxes[b], tr.boxes[tb]
+                if (not db.overlap(tbx) or 1.0 < db.distance(tbx)
+                        or 0.3 > db.overlapped_area(tbx) / min(db.area(), tbx.area())
+                        or 0.5 * max(db.w, tbx.w) < _norm(db.center()[0] - tbx.center()[0],
+                                                           db.center()[1] - tbx.center()[1])):
+                    box_cost = math.inf
+                    break
+                box_cost += box_matching_cost(tbx, db)
+                tb -= 1
+            if box_cost == math.inf:
+                continue
+            box_cost /= float(length)
+            cost[d, t] = np.float32(box_cost)
+        tr.features, tr.tracked = v_prev, v_curr
+    for d in range(D):
+        f = in_box[d]
+        if not f:
+            continue
+        n_major = n_cur = 0
+        cur = f[0]
+        for k in range(len(f)):
+            if cur == f[k]:
+                n_cur += 1
+                continue
+            if n_cur > n_major:
+                n_major = n_cur
+            cur = f[k]
+            n_cur = 0
+        if f[0] == cur:
+            n_major = n_cur
+        if float(n_major) > float(len(f)) * 0.5:
+            continue
+        cost[d, :] = np.inf
+    return cost
