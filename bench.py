@@ -109,7 +109,7 @@ def main():
     ap.add_argument("--overlap", choices=["off", "stream", "fused"], default="fused",
                     help="ingest of frame t+1: serial on the LK stream, on a second stream, or fused "
                          "into the tail of frame t's LK launch (default)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_summary.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01b_pmc_summary.json"),
                     help="rocprofv3 FETCH/WRITE_SIZE summary (tools/profile_round.sh) for roofline.traffic")
     args = ap.parse_args()
 
