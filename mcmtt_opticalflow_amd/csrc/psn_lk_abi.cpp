@@ -55,6 +55,7 @@ struct psn_lk_ctx {
     // PSN_LK_GENERIC=1 (always the tiled kernel)
     int force_threads = 0;
     bool force_generic = false;
+    bool onewave = true;  // PSN_LK_ONEWAVE=0: multi-wave iterations in the single-tile kernel
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     // timing: event ring, 2 events per timed call
     int tcap = 0;
@@ -137,6 +138,7 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     c->nlevels = max_level_cap + 1;
     if (const char *e = getenv("PSN_LK_THREADS")) c->force_threads = atoi(e);
     if (const char *e = getenv("PSN_LK_GENERIC")) c->force_generic = atoi(e) != 0;
+    if (const char *e = getenv("PSN_LK_ONEWAVE")) c->onewave = atoi(e) != 0;
     if (const char *e = getenv("PSN_LK_FUSED_HELPERS")) c->fused_helpers = std::max(0, atoi(e));
     auto fail = [&](int rc) {
         psn_lk_destroy(c);
@@ -404,8 +406,10 @@ int psn_lk_push_frame(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, 
 
 // Validate and plan one query into its device descriptor.
 static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::LkQueryDev &d, int &lds, bool &single,
-                      bool allow_scratch) {
+                      bool allow_scratch, int &ow_rows, int &ow_lds) {
     single = false;
+    ow_rows = 1 << 30;
+    ow_lds = 0;
     const psn_lk_params &p = q.params;
     const int limit = allow_scratch ? c->nslots : c->user_slots;
     if (q.prev_slot < 0 || q.prev_slot >= limit || q.next_slot < 0 || q.next_slot >= limit)
@@ -427,6 +431,11 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     const int budget = 160 * 1024 - 1024;
     if (w * h <= 256 * psn::kStEPTMax && st.total <= psn::kStMaxLds) {
         single = true;
+        const psn::LkStLayout so(w, h, (p.flags & PSN_LK_ACCUM_SCALAR) == 0, ml + 1, true);
+        if (psn::ow_rows(w, h) <= psn::kOwMaxRows && so.total <= psn::kStMaxLds) {
+            ow_rows = psn::ow_rows(w, h);
+            ow_lds = so.total;
+        }
     } else if (psn::lk_lds_bytes(w, h, tr) > 64 * 1024) {
         while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
         if (psn::lk_lds_bytes(w, h, tr) > budget)
@@ -445,6 +454,17 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     d.tile_rows = tr;
     d.min_eig = (float)p.min_eig_threshold;
     d.eps2 = eps * eps;
+    const int jrw = psn::st_jreg_w(w);
+    const int nc = (p.flags & PSN_LK_ACCUM_SCALAR) == 0 ? (w / 8) * 2 : 0;  // columns per SSE2 chain class
+    d.ow_g = std::max(psn::ow_groups(w), 1);
+    d.ow_rg = (h + d.ow_g - 1) / d.ow_g;
+    d.dv_w = psn::div_magic(w);
+    d.dv_dw = psn::div_magic(w + 1);
+    d.dv_pw = psn::div_magic(w + 3);
+    d.dv_jrw = psn::div_magic(jrw);
+    d.dv_jrw4 = psn::div_magic(jrw / 4);
+    d.dv_g = psn::div_magic(d.ow_g);
+    d.dv_cw = psn::div_magic(nc);
     lds = single ? st.total : psn::lk_lds_bytes(w, h, tr);
     return PSN_LK_OK;
 }
@@ -475,7 +495,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         a.status = d_status;
         a.err = d_err;
         a.stamps = c->d_stamps;
-        int wgs = 0, lds = 0, maxpx = 0, nqd = 0;
+        int wgs = 0, lds = 0, maxpx = 0, nqd = 0, rows_ow = 0, lds_ow = 0;
         bool all_single = true;
         for (int i = 0; i < n; i++) {
             const psn_lk_query &qq = q[base + i];
@@ -484,11 +504,13 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                     return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", qq.params.win_w, qq.params.win_h);
                 continue;
             }
-            int l = 0;
+            int l = 0, orows = 0, olds = 0;
             bool single = false;
-            int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch);
+            int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch, orows, olds);
             if (rc) return rc;
             all_single &= single;
+            rows_ow = std::max(rows_ow, orows);
+            lds_ow = std::max(lds_ow, olds);
             wgs += qq.num_pts;
             lds = std::max(lds, l);
             maxpx = std::max(maxpx, qq.params.win_w * qq.params.win_h);
@@ -508,6 +530,14 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             }
             const int ept = nt == 512 ? (maxpx <= 512 ? 1 : 2) : (maxpx <= 2 * nt ? 2 : 4);
             threads = nt * 10 + ept;
+            // one-wave iterations (wave 0 iterates, waves 1-3 stage the next level)
+            if (c->onewave && !forced && rows_ow <= psn::kOwMaxRows) {
+                const int oept = maxpx <= 512 ? 2 : 4;
+                int E = rows_ow <= 4 ? 4 : rows_ow <= 7 ? 7 : rows_ow <= 8 ? 8 : 16;
+                if (oept == 4 && E < 8) E = 8;
+                threads = 1000 * E + 2560 + oept;
+                lds = lds_ow;
+            }
         }
         if (c->pend && all_single) {  // fuse the deferred build into this launch's tail
             int tx, ty, plds;

@@ -42,7 +42,12 @@ struct LkQueryDev {
     int tile_rows;        // window rows per LDS tile (>= win_h: single-tile kernel)
     float min_eig;
     double eps2;
+    // division magics (q = n * dv >> 22, exact for n, d < 1024) of the per-query
+    // divisors the single-tile kernel needs, and its one-wave lane geometry
+    unsigned dv_w, dv_dw, dv_pw, dv_jrw, dv_jrw4, dv_g, dv_cw;
+    int ow_g, ow_rg, pad2_;
 };
+__host__ __device__ inline unsigned div_magic(int d) { return d > 0 ? ((1u << 22) + (unsigned)d - 1u) / (unsigned)d : 0u; }
 
 // Ring geometry as kernel arguments (every slot has the same level layout):
 // level l of slot s starts at base + s * slot_bytes + off[l].
@@ -127,15 +132,28 @@ constexpr int kStScratchBytes = 2 * kMaxLevels * 8 * 4 + kStRiInts * 4 + kStMaxL
 // 16-B LDS write), width a multiple of 4 keeping >= kStJMargin columns each side
 __host__ __device__ inline int st_jreg_w(int w) { return (w + 2 * kStJMargin + 4 + 3) & ~3; }
 __host__ __device__ inline int st_jreg_h(int h) { return h + 1 + 2 * kStJMargin; }
+// One-wave iteration mode: the J region is column-major with an odd column
+// stride (LDS banks), double-buffered, each buffer padded for the idle rows of
+// the last lanes.
+__host__ __device__ inline int st_jrh_cm(int h) { return st_jreg_h(h) | 1; }
+__host__ __device__ inline int st_jp_cm_dw(int w, int h) { return (st_jreg_w(w) * st_jrh_cm(h) + 16 + 20) & ~15; }
+// Lane geometry of the one-wave mode: window columns of one SSE2 chain class
+// on consecutive lanes, G row groups of RG rows per column (G * w <= 64).
+__host__ __device__ inline int ow_groups(int w) { return w <= 64 ? 64 / w : 0; }
+__host__ __device__ inline int ow_rows(int w, int h) {
+    const int G = ow_groups(w);
+    return G ? (h + G - 1) / G : 1 << 30;
+}
+constexpr int kOwMaxRows = 16;
 struct LkStLayout {
     int tbl, ri, lv, jp, pim, pim_stride, dg, dg_stride, iw, iw_stride, r, total;
-    __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev) {
+    __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev, bool ow = false) {
         const int wh = w * h;
         tbl = 0;
         ri = tbl + 2 * kMaxLevels * 8 * 4;
         lv = ri + kStRiInts * 4;
         jp = kStScratchBytes;                      // fused builds use LDS from here
-        pim = jp + align16(4 * st_jreg_w(w) * st_jreg_h(h));
+        pim = jp + (ow ? 8 * st_jp_cm_dw(w, h) : align16(4 * st_jreg_w(w) * st_jreg_h(h)));
         pim_stride = align16(4 * (h + 3) * (w + 3));
         dg = pim + nlev * pim_stride;
         dg_stride = align16(4 * (h + 1) * (w + 1));
@@ -156,6 +174,8 @@ constexpr int kStMaxLds = 150 * 1024;
 // Launchers (psn_lk_kernels.hip).
 hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s);
 void pyramid_grid(const PyrBuildArgs &a, int &tiles_x, int &tiles_y, int &lds_bytes);
+// threads: tiled kernel = workgroup size; single-tile kernel = NT * 10 + EPT,
+// plus 1000 * E for the one-wave iteration mode (E window rows per lane).
 hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, bool single_tile, hipStream_t s);
 hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
 

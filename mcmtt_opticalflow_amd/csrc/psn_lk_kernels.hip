@@ -288,6 +288,16 @@ __device__ __forceinline__ int wave_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
 }
+// Inclusive prefix sum over the 64 lanes (the wave_sum sequence without the final readlane).
+__device__ __forceinline__ int wave_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
 __device__ __forceinline__ unsigned sat_add(unsigned a, unsigned b) { return min(a + b, kSatCap); }
 __device__ __forceinline__ unsigned wave_sum_sat(unsigned v) {
     v = sat_add(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
@@ -333,6 +343,10 @@ __device__ __forceinline__ void block_reduce4(int &v0, int &v1, unsigned &v2, un
     }
 }
 
+// n / d for 0 <= n, d < 1024 with mg = div_magic(d) = ceil(2^22 / d): the error
+// term n * (mg * d - 2^22) < 2^20 keeps the quotient exact; n * mg < 2^32.
+__device__ __forceinline__ int qdiv(int n, unsigned mg) { return (int)(__umul24((unsigned)n, mg) >> 22); }
+
 // Per-thread walk over a PW-wide region in steps of NT elements.
 struct Walk {
     int x, y, sx, sy, pw;
@@ -342,6 +356,14 @@ struct Walk {
         y = tid / pw;
         sx = nt % pw;
         sy = nt / pw;
+    }
+    // the same with the division magic of pw (tid, nt < 1024)
+    __device__ __forceinline__ void init_m(int tid, int nt, int pw_, unsigned mg) {
+        pw = pw_;
+        y = qdiv(tid, mg);
+        x = tid - y * pw;
+        sy = qdiv(nt, mg);
+        sx = nt - sy * pw;
     }
     __device__ __forceinline__ void step() {
         x += sx;
@@ -1009,12 +1031,13 @@ typedef void __attribute__((address_space(3))) *lptr_t;
 // (reflect-101 addressing) into LDS, one dword per pixel. Wave w issues the
 // 64-pixel chunks w, w+NW, ...; completion = s_waitcnt vmcnt(0) + barrier.
 template <int NT>
-__device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH) {
+__device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH,
+                                           unsigned mg_pw) {
     const int n = PW * PH;
     const bool interior = gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     Walk wk;
-    wk.init(threadIdx.x, NT, PW);
+    wk.init_m(threadIdx.x, NT, PW, mg_pw);
     for (int c0 = wid * 64; c0 < n; c0 += NT, wk.step()) {
         if (c0 + lane < n) {
             int gy = gy0 + wk.y, gx = gx0 + wk.x;
@@ -1035,6 +1058,15 @@ __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" :
 struct JWalk {
     int ey0, ex0, sy, sx, m;
 };
+__device__ __forceinline__ JWalk jwalk_t(int t, int m, int nt, unsigned mg) {
+    JWalk wk;
+    wk.m = m;
+    wk.ey0 = qdiv(t, mg);
+    wk.ex0 = t - wk.ey0 * m;
+    wk.sy = qdiv(nt, mg);
+    wk.sx = nt - wk.sy * m;
+    return wk;
+}
 __device__ __forceinline__ JWalk jwalk(int m, int nt) {
     JWalk wk;
     wk.m = m;
@@ -1055,12 +1087,15 @@ __device__ __forceinline__ JWalk jwalk(int m, int nt) {
 // aligned dwords) and write 4 pairs with one 16-B LDS store; regions that cross
 // the image border gather the 2 bytes of each pair through reflect-101. KJ*NT
 // elements are held in registers; the rest move synchronously in store().
+// With cs > 0 the region is written COLUMN-major (pair (r, c) at c * cs + r),
+// the layout of the one-wave iteration kernel.
 constexpr int KJ = 4;
 template <int NT>
 struct JPStage {
     uint2 v[KJ];
     const uint8_t *src;
     int pitch, lw, lh, gy0, gx0, PW, PH;
+    int cs = 0;
     bool interior;
     JWalk wk;
     __device__ __forceinline__ void setup(const LevelDev &L, int y0, int x0, int pw, int ph, const JWalk &wi,
@@ -1105,9 +1140,17 @@ struct JPStage {
             q.y = __builtin_amdgcn_perm(val.y, val.x, 0x0c020c01u);
             q.z = __builtin_amdgcn_perm(val.y, val.x, 0x0c030c02u);
             q.w = __builtin_amdgcn_perm(val.y, val.x, 0x0c040c03u);  // J[4x+3] | J[4x+4] << 16
-            *(uint4 *)(dst + y * PW + 4 * x) = q;
+            if (cs > 0) {
+                uint32_t *d = dst + 4 * x * cs + y;
+                d[0] = q.x;
+                d[cs] = q.y;
+                d[2 * cs] = q.z;
+                d[3 * cs] = q.w;
+            } else {
+                *(uint4 *)(dst + y * PW + 4 * x) = q;
+            }
         } else {
-            dst[y * PW + x] = val.x | (val.y << 16);
+            dst[cs > 0 ? x * cs + y : y * PW + x] = val.x | (val.y << 16);
         }
     }
     __device__ __forceinline__ void load(const LevelDev &L, int y0, int x0, int pw, int ph, const JWalk &wi,
@@ -1167,6 +1210,31 @@ __device__ __forceinline__ int sdot2(unsigned a, unsigned b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, b), c, false);
 }
 __device__ __forceinline__ unsigned pack_w(int lo, int hi) { return ((unsigned)lo & 0xffffu) | ((unsigned)hi << 16); }
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// v_dot2_u32_u16: a.lo*b.lo + a.hi*b.hi + c on unsigned 16-bit halves.
+__device__ __forceinline__ unsigned udot2(unsigned a, unsigned b, unsigned c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b), c, false);
+}
+// Three simultaneous 64-lane sums (DPP, interleaved); a is clamped per lane to
+// 2^25 first so its total cannot wrap. Results are uniform.
+__device__ __forceinline__ void wave_sum3(int &s1, int &s2, unsigned &a) {
+    a = min(a, 1u << 25);
+#define PSN_DPP3(ctl, rm)                                                   \
+    s1 += __builtin_amdgcn_update_dpp(0, s1, ctl, rm, 0xf, false);          \
+    s2 += __builtin_amdgcn_update_dpp(0, s2, ctl, rm, 0xf, false);          \
+    a += (unsigned)__builtin_amdgcn_update_dpp(0, (int)a, ctl, rm, 0xf, false)
+    PSN_DPP3(0x111, 0xf);
+    PSN_DPP3(0x112, 0xf);
+    PSN_DPP3(0x114, 0xf);
+    PSN_DPP3(0x118, 0xf);
+    PSN_DPP3(0x142, 0xa);
+    PSN_DPP3(0x143, 0xc);
+#undef PSN_DPP3
+    s1 = __builtin_amdgcn_readlane(s1, 63);
+    s2 = __builtin_amdgcn_readlane(s2, 63);
+    a = (unsigned)__builtin_amdgcn_readlane((int)a, 63);
+}
 
 // Level geometry of the I window (prevPt/2^l - halfWin): top-left, validity and weights.
 struct IGeo {
@@ -1217,7 +1285,7 @@ __device__ __forceinline__ void pyr_tail(const LkLaunchArgs &A, uint8_t *smem) {
 // prologue landed, 51 Scharr of all levels, 52 A products + reduction, 53
 // solver table; per level L*10+0 start, +1 J staged, +2 window loaded, +7
 // iterations done, +8 iteration count; 40..45 accumulated iteration phases.
-template <int NT, int EPT>
+template <int NT, int EPT, int E>
 __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NW = NT / 64;
@@ -1238,7 +1306,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     const int JRW = st_jreg_w(w), JRH = st_jreg_h(h);
     const int PW = w + 3, DW = w + 1;
 
-    const LkStLayout lay(w, h, sse, nlev);
+    const LkStLayout lay(w, h, sse, nlev, E > 0);
     int *RI = (int *)(smem + lay.ri);
     float *LV = (float *)(smem + lay.lv);
     uint32_t *JP = (uint32_t *)(smem + lay.jp);
@@ -1255,7 +1323,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         const int idx = tid + k * NT;
         ev[k] = idx < wh;
         const int i = ev[k] ? idx : 0;
-        const int y = i / w, x = i - (i / w) * w;
+        const int y = qdiv(i, Q.dv_w), x = i - y * w;
         pix[k] = i;
         ofsJ[k] = y * JRW + x;
         ofsP[k] = (y + 1) * PW + x + 1;
@@ -1270,7 +1338,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     // ---- prologue: zero the A planes' chain padding (ordered by the barrier
     // after the DMA); level geometry comes from the kernel arguments ----
     zero_pads<NT>(R, GA, 3 * nlev);
-    const JWalk wk_int = jwalk(JRW >> 2, NT), wk_bord = jwalk(JRW, NT);  // J staging walks
+    const JWalk wk_int = jwalk_t(tid, JRW >> 2, NT, Q.dv_jrw4), wk_bord = jwalk_t(tid, JRW, NT, Q.dv_jrw);  // J staging walks
     LK_STAMP(60);
 
     const float hwx = __fmul_rn((float)(w - 1), 0.5f), hwy = __fmul_rn((float)(h - 1), 0.5f);
@@ -1286,7 +1354,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
         const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
         if (!gg.valid) continue;
-        dma_region<NT>((uint32_t *)(smem + lay.pim + l * lay.pim_stride), I, gg.ipy - 1, gg.ipx - 1, PW, h + 3);
+        dma_region<NT>((uint32_t *)(smem + lay.pim + l * lay.pim_stride), I, gg.ipy - 1, gg.ipx - 1, PW, h + 3, Q.dv_pw);
     }
     JPStage<NT> pf;  // prefetched J region of level pf_level at (pf_y0, pf_x0)
     int pf_level, pf_x0, pf_y0;
@@ -1314,7 +1382,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         const uint32_t *P = (const uint32_t *)(smem + lay.pim + l * lay.pim_stride);
         short2 *Dg = (short2 *)(smem + lay.dg + l * lay.dg_stride);
         Walk wk;
-        wk.init(tid, NT, DW);
+        wk.init_m(tid, NT, DW, Q.dv_dw);
         for (int idx = tid; idx < (h + 1) * DW; idx += NT, wk.step()) {
             const int gy = gg.ipy + wk.y, gx = gg.ipx + wk.x;
             short2 d = make_short2(0, 0);
@@ -1461,11 +1529,14 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     float errv = 0.f;
     const float FLT_SCALE = 1.f / (1 << 20);
 #ifdef PSN_LK_STAMPS
-    unsigned long long acc_ph[6] = {0, 0, 0, 0, 0, 0}, t_ph = 0;
-#define PH_BEGIN() t_ph = __builtin_amdgcn_s_memtime()
+    unsigned long long acc_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_ph = 0;
+// ordered stamps: every earlier instruction has issued and every LDS access landed
+#define PH_STAMP(t) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory")
+#define PH_BEGIN() PH_STAMP(t_ph)
 #define PH_MARK(i)                                                  \
     do {                                                            \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        unsigned long long t_;                                      \
+        PH_STAMP(t_);                                               \
         acc_ph[i] += t_ - t_ph;                                     \
         t_ph = t_;                                                  \
     } while (0)
@@ -1483,6 +1554,370 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
 #endif
     int jr_x0 = 0, jr_y0 = 0;
 
+    if constexpr (E > 0) {
+        // ---- one-wave iterations: wave 0 runs the LK iterations of every level
+        // with no workgroup barrier inside the loop; waves 1..NW-1 meanwhile
+        // stage the next level's J region (predicted start) into the other
+        // half of the double-buffered, column-major J region. ----
+        const int JRHc = st_jrh_cm(h);
+        uint32_t *const JPB0 = JP, *const JPB1 = JP + st_jp_cm_dw(w, h);
+        // lane -> (window column, row group): columns sorted by SSE2 chain class
+        // (class c < 4: x = c, c+4, ... < n8; class 4 = the scalar tail)
+        const int G = Q.ow_g, RG = Q.ow_rg;
+        const int n8 = sse ? (w / 8) * 8 : 0, cw = n8 / 4;
+        const int cr = qdiv(lane, Q.dv_g), gi = lane - cr * G;
+        const bool lane_on = cr < w;
+        const int ccl = qdiv(cr, sse ? Q.dv_cw : 0u);  // chain class of an SSE2 column
+        const int colx = !lane_on ? 0 : (cr < n8 ? ccl + 4 * (cr - ccl * cw) : cr);
+        const int oy0 = gi * RG;
+        const int lane_off = colx * JRHc + oy0;
+        // class c occupies lanes (last[c-1], last[c]]; empty classes repeat the previous bound
+        const int last4 = w * G - 1;
+        // this lane ends class cls_end (it publishes the class's scans), or -1
+        int cls_end = -1;
+        if (lane == last4) cls_end = 4;
+        if (n8 > 0)
+            for (int c = 0; c < 4; c++)
+                if (lane == (c + 1) * cw * G - 1 && lane != last4) cls_end = c;
+        int4 *CSX = (int4 *)(RI + kStRiIt + 16);  // 5 x int4 class scans
+        if (n8 == 0 && tid < 4) CSX[tid] = make_int4(0, 0, 0, 0);  // ordered by the first level barrier
+        // loop constants pinned in registers (not re-read from the kernel arguments)
+        double eps2 = Q.eps2;
+        int maxc = Q.max_count;
+        asm volatile("" : "+v"(eps2), "+s"(maxc));
+        const int th = max(tid - 64, 0);
+        const JWalk wkh_int = jwalk_t(th, JRW >> 2, NT - 64, Q.dv_jrw4), wkh_bord = jwalk_t(th, JRW, NT - 64, Q.dv_jrw);
+        const JWalk wk0_int = jwalk_t(lane, JRW >> 2, 64, Q.dv_jrw4), wk0_bord = jwalk_t(lane, JRW, 64, Q.dv_jrw);
+        pf.cs = JRHc;
+        LK_STAMP(54);
+        bool pf_regs = true;  // the prefetched region is still in registers (prologue) vs already in LDS
+        int buf = 0;
+        float *XCH = (float *)(RI + kStRiIt);  // wave 0 -> all: NPx, NPy at the end of a level
+
+        for (int level = maxL; level >= 0; level--) {
+            LK_STAMP(level * 10 + 0);
+            const LevelDev I = ring_level(A.ring, Q.prev_slot, level);
+            const LevelDev J = ring_level(A.ring, Q.next_slot, level);
+            const int cols = I.w, rows = I.h;
+            const float scale = ldexpf(1.f, -level);
+            float nx, ny;
+            if (level == maxL) {
+                if (flags & PSN_LK_USE_INITIAL_FLOW) {
+                    nx = __fmul_rn(NPx, scale);
+                    ny = __fmul_rn(NPy, scale);
+                } else {
+                    nx = __fmul_rn(px0, scale);
+                    ny = __fmul_rn(py0, scale);
+                }
+            } else {
+                nx = __fmul_rn(NPx, 2.f);
+                ny = __fmul_rn(NPy, 2.f);
+            }
+            NPx = nx;
+            NPy = ny;
+            const IGeo gg = i_geo(px0, py0, hwx, hwy, level, w, h, cols, rows);
+            const float *lv = LV + level * kStLvFloats;
+            const bool run = gg.valid && lv[5] != 0.f;
+            if (!gg.valid) {
+                if (level == 0) {
+                    status = 0;
+                    errv = 0.f;
+                }
+            } else {
+                if (flags & PSN_LK_GET_MIN_EIGENVALS) errv = lv[4];
+                if (!run && level == 0) status = 0;
+            }
+            nx = __fsub_rn(nx, hwx);
+            ny = __fsub_rn(ny, hwy);
+            uint32_t *const JC = buf ? JPB1 : JPB0;
+            if (run) {
+                const int inx0 = __builtin_amdgcn_readfirstlane(cv_floor(nx));
+                const int iny0 = __builtin_amdgcn_readfirstlane(cv_floor(ny));
+                if (pf_level == level && inx0 >= pf_x0 && iny0 >= pf_y0 && inx0 + w + 1 <= pf_x0 + JRW &&
+                    iny0 + h + 1 <= pf_y0 + JRH) {
+                    if (pf_regs) pf.store(JC);
+                    jr_x0 = pf_x0;
+                    jr_y0 = pf_y0;
+                } else {
+                    JPStage<NT> cp;
+                    cp.cs = JRHc;
+                    jr_x0 = (inx0 - kStJMargin) & ~3;
+                    jr_y0 = iny0 - kStJMargin;
+                    cp.copy(JC, J, jr_y0, jr_x0, JRW, JRH, wk_int, wk_bord);
+                }
+            }
+            pf_regs = false;
+            __syncthreads();  // JC complete; every wave is past the previous level
+            LK_STAMP(level * 10 + 1);
+            // next level's region at its predicted start (2 x this start)
+            pf_level = level > 0 ? level - 1 : -1;
+            pf_x0 = __builtin_amdgcn_readfirstlane((cv_floor(__fsub_rn(__fmul_rn(NPx, 2.f), hwx)) - kStJMargin) & ~3);
+            pf_y0 = __builtin_amdgcn_readfirstlane(cv_floor(__fsub_rn(__fmul_rn(NPy, 2.f), hwy)) - kStJMargin);
+
+            if (wid != 0) {
+                if (level > 0) {
+                    JPStage<NT> cp;
+                    cp.cs = JRHc;
+                    cp.copy(buf ? JPB0 : JPB1, ring_level(A.ring, Q.next_slot, level - 1), pf_y0, pf_x0, JRW, JRH,
+                            wkh_int, wkh_bord);
+                }
+            } else if (run) {
+                const float A11 = lv[0], A12 = lv[1], A22 = lv[2], D = lv[3];
+                // the lane's window rows, two rows per dword (int16 halves): I, Ix,
+                // Iy, |Ix| + |Iy|; rows past the window carry zero gradients
+                constexpr int E2 = (E + 1) / 2;
+                unsigned IwP[E2], IxP[E2], IyP[E2], SxyP[E2];
+                int Iw_[E];
+                {
+                    const int2 *IW = (const int2 *)(smem + lay.iw + level * lay.iw_stride);
+                    int iw[2 * E2], ix[2 * E2], iy[2 * E2];
+#pragma unroll
+                    for (int k = 0; k < 2 * E2; k++) {
+                        const int y = oy0 + k;
+                        const bool v = k < E && lane_on && k < RG && y < h;
+                        const int2 t = IW[v ? y * w + colx : 0];
+                        iw[k] = k < E ? t.x : 0;
+                        ix[k] = v ? (int)(short)(t.y & 0xffff) : 0;
+                        iy[k] = v ? (t.y >> 16) : 0;
+                        if (k < E) Iw_[k] = t.x;
+                    }
+#pragma unroll
+                    for (int q = 0; q < E2; q++) {
+                        IwP[q] = pack_w(iw[2 * q], iw[2 * q + 1]);
+                        IxP[q] = pack_w(ix[2 * q], ix[2 * q + 1]);
+                        IyP[q] = pack_w(iy[2 * q], iy[2 * q + 1]);
+                        SxyP[q] = pack_w(abs(ix[2 * q]) + abs(iy[2 * q]), abs(ix[2 * q + 1]) + abs(iy[2 * q + 1]));
+                    }
+                }
+                LK_STAMP(level * 10 + 2);
+                float pdx = 0.f, pdy = 0.f;
+                int jdone = 0;
+                unsigned dP[E2];
+                // diffs J - I of the lane's rows at offset (ox, oy) of the region
+                // (packed pairs into dP) and the lane's s1, s2, sum|t1|+|t2| (clamped)
+                auto products = [&](int ox, int oy, unsigned W0, unsigned W1, int &s1, int &s2, unsigned &a) {
+                    const uint32_t *jb = JC + __mul24(ox, JRHc) + oy + lane_off;
+                    unsigned rr[2 * E2 + 1];
+#pragma unroll
+                    for (int k = 0; k <= 2 * E2; k++) rr[k] = jb[k];
+                    s1 = 0;
+                    s2 = 0;
+                    a = 0;
+#pragma unroll
+                    for (int q = 0; q < E2; q++) {
+                        const int j0 = sdot2(rr[2 * q + 1], W1, sdot2(rr[2 * q], W0, 1 << 8)) >> 9;
+                        const int j1 = sdot2(rr[2 * q + 2], W1, sdot2(rr[2 * q + 1], W0, 1 << 8)) >> 9;
+                        const s16x2 d = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((unsigned)j1, (unsigned)j0, 0x05040100u)) -
+                                        __builtin_bit_cast(s16x2, IwP[q]);
+                        dP[q] = __builtin_bit_cast(unsigned, d);
+                        s1 = sdot2(dP[q], IxP[q], s1);
+                        s2 = sdot2(dP[q], IyP[q], s2);
+                        const s16x2 ad = __builtin_elementwise_max(d, (s16x2)0 - d);
+                        a = udot2(__builtin_bit_cast(unsigned, ad), SxyP[q], a);  // per lane < 2^30
+                    }
+                };
+                for (int j = 0; j < maxc; j++) {
+                    jdone = j + 1;
+                    PH_BEGIN();
+                    const int inx = cv_floor(nx), iny = cv_floor(ny);
+                    int iw00, iw01, iw10, iw11;
+                    bilin_weights(__fsub_rn(nx, (float)inx), __fsub_rn(ny, (float)iny), iw00, iw01, iw10, iw11);
+                    const unsigned W0 = pack_w(iw00, iw01), W1 = pack_w(iw10, iw11);
+                    // speculative: the offsets are clamped into the region, the
+                    // bounds / region tests below decide whether the sums count
+                    const int ox = min(max(inx - jr_x0, 0), JRW - w - 1), oy = min(max(iny - jr_y0, 0), JRH - h - 1);
+                    int s1, s2;
+                    unsigned a;
+                    products(ox, oy, W0, W1, s1, s2, a);
+                    int sinx = __builtin_amdgcn_readfirstlane(inx), siny = __builtin_amdgcn_readfirstlane(iny);
+                    // keep the (rarely taken) branches below the products: the
+                    // conditions formally depend on them
+                    asm volatile("; order %2 %3 %4" : "+s"(sinx), "+s"(siny) : "v"(s1), "v"(s2), "v"(a));
+                    if (sinx < -w || sinx >= cols || siny < -h || siny >= rows) {
+                        if (level == 0) status = 0;
+                        break;
+                    }
+                    if (!(sinx >= jr_x0 && siny >= jr_y0 && sinx + w + 1 <= jr_x0 + JRW && siny + h + 1 <= jr_y0 + JRH)) {
+                        // restage by this wave alone (the other waves never read JC)
+                        JPStage<NT> cp;
+                        cp.cs = JRHc;
+                        jr_x0 = __builtin_amdgcn_readfirstlane((sinx - kStJMargin) & ~3);
+                        jr_y0 = __builtin_amdgcn_readfirstlane(siny - kStJMargin);
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        cp.copy(JC, J, jr_y0, jr_x0, JRW, JRH, wk0_int, wk0_bord);
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        products(sinx - jr_x0, siny - jr_y0, W0, W1, s1, s2, a);
+                        PH_COUNT(5);
+                    }
+                    PH_MARK(0);
+                    const int l1 = s1, l2 = s2;  // the lane's own sums (class path)
+                    wave_sum3(s1, s2, a);
+                    PH_MARK(1);
+                    float b1, b2;
+                    if (a <= (unsigned)kExact) {
+                        // every term and partial sum in any order is an integer <= 2^24
+                        b1 = (float)s1;
+                        b2 = (float)s2;
+                    } else {
+                        PH_COUNT(6);
+                        // per SSE2 chain class: inclusive scans of the lanes' sums and
+                        // of sum|t1|, sum|t2|; class-end lanes publish to LDS
+                        unsigned a1 = 0, a2 = 0;
+#pragma unroll
+                        for (int q = 0; q < E2; q++) {
+                            const s16x2 d = __builtin_bit_cast(s16x2, dP[q]);
+                            const unsigned ad = __builtin_bit_cast(unsigned, __builtin_elementwise_max(d, (s16x2)0 - d));
+                            const s16x2 gx = __builtin_bit_cast(s16x2, IxP[q]), gy = __builtin_bit_cast(s16x2, IyP[q]);
+                            a1 = udot2(ad, __builtin_bit_cast(unsigned, __builtin_elementwise_max(gx, (s16x2)0 - gx)), a1);
+                            a2 = udot2(ad, __builtin_bit_cast(unsigned, __builtin_elementwise_max(gy, (s16x2)0 - gy)), a2);
+                        }
+                        a1 = min(a1, (unsigned)(2 * kExact));  // a class holding a clamped lane fails anyway
+                        a2 = min(a2, (unsigned)(2 * kExact));
+                        const int c1 = wave_scan(l1), c2 = wave_scan(l2);
+                        a1 = (unsigned)wave_scan((int)a1);
+                        a2 = (unsigned)wave_scan((int)a2);
+                        if (cls_end >= 0) CSX[cls_end] = make_int4(c1, c2, (int)a1, (int)a2);
+                        int S1[5], S2[5];
+                        bool exact = true;
+                        int4 pv = make_int4(0, 0, 0, 0);
+#pragma unroll
+                        for (int c = 0; c < 5; c++) {
+                            const int4 cv = CSX[c];  // classes 0-3 stay zero without SSE2 lanes
+                            S1[c] = cv.x - pv.x;     // wrapping: exact whenever the class passes
+                            S2[c] = cv.y - pv.y;
+                            exact = exact && (unsigned)(cv.z - pv.z) <= (unsigned)kExact &&
+                                    (unsigned)(cv.w - pv.w) <= (unsigned)kExact;
+                            pv = cv;
+                        }
+                        if (exact) {
+                            // every chain's partial sums are integers <= 2^24: each chain
+                            // sum is its integer sum; combine in the SSE2 build's order
+                            b1 = (float)S1[4];
+                            b2 = (float)S2[4];
+                            if (sse) {
+                                b1 = __fadd_rn(b1, __fadd_rn(__fadd_rn((float)S1[0], (float)S1[2]),
+                                                             __fadd_rn((float)S1[1], (float)S1[3])));
+                                b2 = __fadd_rn(b2, __fadd_rn(__fadd_rn((float)S2[0], (float)S2[2]),
+                                                             __fadd_rn((float)S2[1], (float)S2[3])));
+                            }
+                        } else {
+                            // ordered float chains: products chain-major into R, one lane per chain
+#pragma unroll
+                            for (int k = 0; k < E; k++) {
+                                const int y = oy0 + k;
+                                if (lane_on && k < RG && y < h) {
+                                    const int d = (int)(short)(k & 1 ? dP[k >> 1] >> 16 : dP[k >> 1] & 0xffff);
+                                    const int gx = (int)(short)(k & 1 ? IxP[k >> 1] >> 16 : IxP[k >> 1] & 0xffff);
+                                    const int gy = (int)(short)(k & 1 ? IyP[k >> 1] >> 16 : IyP[k >> 1] & 0xffff);
+                                    const int pos = posB(GB, y, colx);
+                                    R[pos] = (float)__mul24(d, gx);
+                                    R[GB.P + pos] = (float)__mul24(d, gy);
+                                }
+                            }
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            float acc = 0.f;
+                            if (lane < 10) {
+                                const int ch = lane % 5, s = lane / 5;
+                                const int base = s * GB.P + (ch < 4 ? ch * GB.S : 4 * GB.S);
+                                const int nb = (ch < 4 ? GB.S : GB.T) >> 4;
+                                acc = chain_sum16(R + base, nb);
+                            }
+                            b1 = readlane_f(acc, 4);
+                            b2 = readlane_f(acc, 9);
+                            if (sse) {
+                                const float bb0 = __fadd_rn(readlane_f(acc, 0), readlane_f(acc, 2));
+                                const float bb2 = __fadd_rn(readlane_f(acc, 1), readlane_f(acc, 3));
+                                const float bb1 = __fadd_rn(readlane_f(acc, 5), readlane_f(acc, 7));
+                                const float bb3 = __fadd_rn(readlane_f(acc, 6), readlane_f(acc, 8));
+                                b1 = __fadd_rn(b1, __fadd_rn(bb0, bb2));
+                                b2 = __fadd_rn(b2, __fadd_rn(bb1, bb3));
+                            }
+                            PH_COUNT(4);
+                        }
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // CSX / R reads done before the next writes
+                    }
+                    PH_MARK(2);
+                    b1 = __fmul_rn(b1, FLT_SCALE);
+                    b2 = __fmul_rn(b2, FLT_SCALE);
+                    const float dx = __fmul_rn(__fsub_rn(__fmul_rn(A12, b2), __fmul_rn(A22, b1)), D);
+                    const float dy = __fmul_rn(__fsub_rn(__fmul_rn(A12, b1), __fmul_rn(A11, b2)), D);
+                    nx = __fadd_rn(nx, dx);
+                    ny = __fadd_rn(ny, dy);
+                    NPx = __fadd_rn(nx, hwx);
+                    NPy = __fadd_rn(ny, hwy);
+                    const double dd = __dadd_rn(__dmul_rn((double)dx, (double)dx), __dmul_rn((double)dy, (double)dy));
+                    PH_MARK(3);
+                    if (dd <= eps2) break;
+                    if (j > 0 && (double)fabsf(__fadd_rn(dx, pdx)) < 0.01 && (double)fabsf(__fadd_rn(dy, pdy)) < 0.01) {
+                        NPx = __fsub_rn(NPx, __fmul_rn(dx, 0.5f));
+                        NPy = __fsub_rn(NPy, __fmul_rn(dy, 0.5f));
+                        break;
+                    }
+                    pdx = dx;
+                    pdy = dy;
+                }
+                LK_STAMP(level * 10 + 7);
+                LK_COUNT(level * 10 + 8, jdone);
+                (void)jdone;
+
+                if (level == 0 && status && A.err && (flags & PSN_LK_GET_MIN_EIGENVALS) == 0) {
+                    const float qx = __fsub_rn(NPx, hwx), qy = __fsub_rn(NPy, hwy);
+                    const int iqx = cv_floor(qx), iqy = cv_floor(qy);
+                    if (iqx < -w || iqx >= cols || iqy < -h || iqy >= rows) {
+                        status = 0;
+                    } else {
+                        int iw00, iw01, iw10, iw11;
+                        bilin_weights(__fsub_rn(qx, (float)iqx), __fsub_rn(qy, (float)iqy), iw00, iw01, iw10, iw11);
+                        if (!(iqx >= jr_x0 && iqy >= jr_y0 && iqx + w + 1 <= jr_x0 + JRW && iqy + h + 1 <= jr_y0 + JRH)) {
+                            JPStage<NT> cp;
+                            cp.cs = JRHc;
+                            jr_x0 = (iqx - kStJMargin) & ~3;
+                            jr_y0 = iqy - kStJMargin;
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            cp.copy(JC, J, jr_y0, jr_x0, JRW, JRH, wk0_int, wk0_bord);
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        }
+                        const unsigned W0 = pack_w(iw00, iw01), W1 = pack_w(iw10, iw11);
+                        const uint32_t *jb = JC + (iqx - jr_x0) * JRHc + (iqy - jr_y0) + lane_off;
+                        unsigned ea = 0;
+                        int ad[E];
+#pragma unroll
+                        for (int k = 0; k < E; k++) {
+                            const int jv = sdot2(jb[k + 1], W1, sdot2(jb[k], W0, 1 << 8)) >> 9;
+                            const int y = oy0 + k;
+                            ad[k] = (lane_on && k < RG && y < h) ? abs(jv - Iw_[k]) : 0;
+                            ea += (unsigned)ad[k];
+                        }
+                        ea = (unsigned)__builtin_amdgcn_readlane(wave_scan((int)ea), 63);
+                        float errval;
+                        if (ea <= (unsigned)kExact) {
+                            errval = (float)ea;  // every partial sum of errval += |diff| is an exact integer
+                        } else {  // row-major order, one lane
+#pragma unroll
+                            for (int k = 0; k < E; k++) {
+                                const int y = oy0 + k;
+                                if (lane_on && k < RG && y < h) R[y * w + colx] = (float)ad[k];
+                            }
+                            for (int k = wh + lane; k < round16i(wh); k += 64) R[k] = 0.f;
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            float acc = 0.f;
+                            if (lane == 0) acc = chain_sum16(R, round16i(wh) >> 4);
+                            errval = readlane_f(acc, 0);
+                        }
+                        errv = __fdiv_rn(__fmul_rn(errval, 1.f), (float)(32 * wh));
+                    }
+                }
+            }
+            if (tid == 0) {
+                XCH[0] = NPx;
+                XCH[1] = NPy;
+            }
+            __syncthreads();  // wave 0 done with JC; the next level's region staged
+            NPx = XCH[0];
+            NPy = XCH[1];
+            buf ^= 1;
+        }
+    } else {
     for (int level = maxL; level >= 0; level--) {
         LK_STAMP(level * 10 + 0);
         const LevelDev I = ring_level(A.ring, Q.prev_slot, level);
@@ -1693,10 +2128,11 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             errv = __fdiv_rn(__fmul_rn(errval, 1.f), (float)(32 * wh));
         }
     }
+    }  // legacy multi-wave iterations
 
     LK_STAMP(61);
 #ifdef PSN_LK_STAMPS
-    for (int i = 0; i < 6; i++) LK_COUNT(40 + i, acc_ph[i]);
+    for (int i = 0; i < 8; i++) LK_COUNT(40 + i, acc_ph[i]);
 #endif
     if (tid == 0) {
         A.next[2 * pi] = NPx;
@@ -1714,16 +2150,23 @@ hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_
     if (total_wgs <= 0) return hipSuccess;
     const dim3 grid(total_wgs);
     if (single_tile) {
-        // threads encodes (workgroup size, pixels per thread): NT * 10 + EPT
+        // threads encodes (workgroup size, pixels per thread, one-wave rows): E * 1000 + NT * 10 + EPT
         switch (threads) {
-            case 642: hipLaunchKernelGGL((lk_kernel_st<64, 2>), grid, dim3(64), lds_bytes, s, a); break;
-            case 644: hipLaunchKernelGGL((lk_kernel_st<64, 4>), grid, dim3(64), lds_bytes, s, a); break;
-            case 1282: hipLaunchKernelGGL((lk_kernel_st<128, 2>), grid, dim3(128), lds_bytes, s, a); break;
-            case 1284: hipLaunchKernelGGL((lk_kernel_st<128, 4>), grid, dim3(128), lds_bytes, s, a); break;
-            case 2562: hipLaunchKernelGGL((lk_kernel_st<256, 2>), grid, dim3(256), lds_bytes, s, a); break;
-            case 5121: hipLaunchKernelGGL((lk_kernel_st<512, 1>), grid, dim3(512), lds_bytes, s, a); break;
-            case 5122: hipLaunchKernelGGL((lk_kernel_st<512, 2>), grid, dim3(512), lds_bytes, s, a); break;
-            default: hipLaunchKernelGGL((lk_kernel_st<256, 4>), grid, dim3(256), lds_bytes, s, a); break;
+            case 642: hipLaunchKernelGGL((lk_kernel_st<64, 2, 0>), grid, dim3(64), lds_bytes, s, a); break;
+            case 644: hipLaunchKernelGGL((lk_kernel_st<64, 4, 0>), grid, dim3(64), lds_bytes, s, a); break;
+            case 1282: hipLaunchKernelGGL((lk_kernel_st<128, 2, 0>), grid, dim3(128), lds_bytes, s, a); break;
+            case 1284: hipLaunchKernelGGL((lk_kernel_st<128, 4, 0>), grid, dim3(128), lds_bytes, s, a); break;
+            case 2562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 0>), grid, dim3(256), lds_bytes, s, a); break;
+            case 5121: hipLaunchKernelGGL((lk_kernel_st<512, 1, 0>), grid, dim3(512), lds_bytes, s, a); break;
+            case 5122: hipLaunchKernelGGL((lk_kernel_st<512, 2, 0>), grid, dim3(512), lds_bytes, s, a); break;
+            case 6562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 4>), grid, dim3(256), lds_bytes, s, a); break;
+            case 9562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 7>), grid, dim3(256), lds_bytes, s, a); break;
+            case 10562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 8>), grid, dim3(256), lds_bytes, s, a); break;
+            case 10564: hipLaunchKernelGGL((lk_kernel_st<256, 4, 8>), grid, dim3(256), lds_bytes, s, a); break;
+            case 18562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 16>), grid, dim3(256), lds_bytes, s, a); break;
+            case 18564: hipLaunchKernelGGL((lk_kernel_st<256, 4, 16>), grid, dim3(256), lds_bytes, s, a); break;
+            case 2564: hipLaunchKernelGGL((lk_kernel_st<256, 4, 0>), grid, dim3(256), lds_bytes, s, a); break;
+            default: return hipErrorInvalidValue;
         }
     } else {
         switch (threads) {
@@ -1741,10 +2184,13 @@ hipError_t lk_kernels_init() {
     if ((e = hipFuncSetAttribute((const void *)lk_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)lk_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)lk_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
-    const void *st[] = {(const void *)lk_kernel_st<64, 2>,  (const void *)lk_kernel_st<64, 4>,
-                        (const void *)lk_kernel_st<128, 2>, (const void *)lk_kernel_st<128, 4>,
-                        (const void *)lk_kernel_st<256, 2>, (const void *)lk_kernel_st<256, 4>,
-                        (const void *)lk_kernel_st<512, 1>, (const void *)lk_kernel_st<512, 2>};
+    const void *st[] = {(const void *)lk_kernel_st<64, 2, 0>,   (const void *)lk_kernel_st<64, 4, 0>,
+                        (const void *)lk_kernel_st<128, 2, 0>,  (const void *)lk_kernel_st<128, 4, 0>,
+                        (const void *)lk_kernel_st<256, 2, 0>,  (const void *)lk_kernel_st<256, 4, 0>,
+                        (const void *)lk_kernel_st<512, 1, 0>,  (const void *)lk_kernel_st<512, 2, 0>,
+                        (const void *)lk_kernel_st<256, 2, 4>,  (const void *)lk_kernel_st<256, 2, 7>,
+                        (const void *)lk_kernel_st<256, 2, 8>,  (const void *)lk_kernel_st<256, 4, 8>,
+                        (const void *)lk_kernel_st<256, 2, 16>, (const void *)lk_kernel_st<256, 4, 16>};
     for (const void *f : st)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)pyramid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;

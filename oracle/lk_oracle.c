@@ -26,6 +26,89 @@
  * how many b-sums / A-sums stayed within the exact-integer bound 2^24. */
 static int *g_iter_log = 0; /* [npts][8] iterations at level l */
 void oracle_set_iter_log(int *buf) { g_iter_log = buf; }
+/* b-sum exactness classes (analysis only): [0] b-sums evaluated, [1] sum|t1|+sum|t2| <= 2^24,
+ * [2] max(sum|t1|, sum|t2|) <= 2^24, [3] every SSE2 chain sum|t| <= 2^24, [4] every chain's
+ * every prefix |P| <= 2^24 and every |t| <= 2^24 (sequential float sum == integer sum), [5] every pixel class
+ * (SSE2 lane or tail) sum|t1|+|t2| <= 2^24. */
+static long long *g_bsum_log = 0;
+void oracle_set_bsum_log(long long *buf) { g_bsum_log = buf; }
+static void bsum_classify(const long long *t1, const long long *t2, int w, int h, int sse) {
+    const long long E = 1LL << 24;
+    long long a1 = 0, a2 = 0, ca[10] = {0}, p[10] = {0};
+    int ok4 = 1;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const int n8 = sse ? (w / 8) * 8 : 0;
+            const int c = x < n8 ? (x & 3) : 4;
+            const long long u = t1[y * w + x], v = t2[y * w + x];
+            a1 += llabs(u);
+            a2 += llabs(v);
+            ca[c] += llabs(u);
+            ca[5 + c] += llabs(v);
+            p[c] += u;
+            p[5 + c] += v;
+            if (llabs(u) > E || llabs(v) > E || llabs(p[c]) > E || llabs(p[5 + c]) > E) ok4 = 0;
+        }
+    int ok3 = 1;
+    for (int c = 0; c < 10; c++)
+        if (ca[c] > E) ok3 = 0;
+    int ok5 = 1;
+    for (int c = 0; c < 5; c++)
+        if (ca[c] + ca[5 + c] > E) ok5 = 0;
+    g_bsum_log[5] += ok5;
+    /* lane model of the one-wave kernel: lane = (column in class order, group of RG rows) */
+    {
+        const int G = w <= 64 ? 64 / w : 1, RG = (h + G - 1) / G;
+        const int n8 = sse ? (w / 8) * 8 : 0, cw = n8 / 4;
+        long long la1[64] = {0}, la2[64] = {0};
+        int lcls[64];
+        for (int l = 0; l < 64; l++) lcls[l] = -1;
+        for (int r = 0; r < w && r * G < 64; r++) {
+            const int x = r < n8 ? r / cw + 4 * (r % cw) : r;
+            const int c = r < n8 ? r / cw : 4;
+            for (int g = 0; g < G; g++) {
+                const int lane = r * G + g;
+                if (lane >= 64) continue;
+                lcls[lane] = c;
+                for (int k = 0; k < RG; k++) {
+                    const int y = g * RG + k;
+                    if (y >= h) break;
+                    la1[lane] += llabs(t1[y * w + x]);
+                    la2[lane] += llabs(t2[y * w + x]);
+                }
+            }
+        }
+        /* (B) max lane value x lanes per class */
+        long long mx = 0;
+        int cnt[5] = {0};
+        for (int l = 0; l < 64; l++) {
+            if (lcls[l] < 0) continue;
+            cnt[lcls[l]]++;
+            if (la1[l] > mx) mx = la1[l];
+            if (la2[l] > mx) mx = la2[l];
+        }
+        int mc = 0;
+        for (int c = 0; c < 5; c++) mc = cnt[c] > mc ? cnt[c] : mc;
+        g_bsum_log[6] += mx * mc <= E;
+        /* (D) 16-lane row sums, class bound = rows it touches */
+        long long r1[4] = {0}, r2[4] = {0};
+        for (int l = 0; l < 64; l++) { r1[l / 16] += la1[l]; r2[l / 16] += la2[l]; }
+        int okd = 1;
+        for (int c = 0; c < 5; c++) {
+            int rlo = 4, rhi = -1;
+            for (int l = 0; l < 64; l++) if (lcls[l] == c) { if (l / 16 < rlo) rlo = l / 16; if (l / 16 > rhi) rhi = l / 16; }
+            long long b1 = 0, b2 = 0;
+            for (int r = rlo; r <= rhi; r++) { b1 += r1[r]; b2 += r2[r]; }
+            if (b1 > E || b2 > E) okd = 0;
+        }
+        g_bsum_log[7] += okd;
+    }
+    g_bsum_log[0]++;
+    g_bsum_log[1] += (a1 + a2) <= E;
+    g_bsum_log[2] += (a1 <= E && a2 <= E);
+    g_bsum_log[3] += ok3;
+    g_bsum_log[4] += ok4;
+}
 
 #define W_BITS 14
 #define W_BITS1 14
@@ -328,6 +411,18 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
 
         float b1 = 0, b2 = 0;
         float qb0[4] = {0, 0, 0, 0}, qb1[4] = {0, 0, 0, 0};
+        if (g_bsum_log) {
+            long long *t1 = (long long *)malloc(sizeof(long long) * 2 * win_w * win_h), *t2 = t1 + win_w * win_h;
+            for (int y = 0; y < win_h; y++)
+                for (int x = 0; x < win_w; x++) {
+                    const uint8_t *Jp = lv->J + (long)(y + iny) * stepI + inx + x;
+                    const int d = DESCALE(BILIN(Jp, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5) - Iw[y * win_w + x];
+                    t1[y * win_w + x] = (long long)d * dIw[2 * (y * win_w + x)];
+                    t2[y * win_w + x] = (long long)d * dIw[2 * (y * win_w + x) + 1];
+                }
+            bsum_classify(t1, t2, win_w, win_h, sse);
+            free(t1);
+        }
         for (int y = 0; y < win_h; y++) {
             const uint8_t *Jptr = lv->J + (long)(y + iny) * stepI + inx;
             const int16_t *Iptr = Iw + y * win_w, *dIptr = dIw + 2 * y * win_w;

@@ -76,6 +76,7 @@ int oracle_calc_optical_flow_pyr_lk(const uint8_t *prev_img, const uint8_t *next
 /* Analysis hook: when set, counts LK iterations per point and level into
  * buf[i*8 + level] (caller zeroes it). Single-threaded use only. */
 void oracle_set_iter_log(int *buf);
+void oracle_set_bsum_log(long long *buf);
 
 #ifdef __cplusplus
 }

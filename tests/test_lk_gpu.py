@@ -290,8 +290,9 @@ def test_lk_config5_4k_5level(oracle_mod):
     assert_same(gpu, ref, "4k")
 
 
-@pytest.mark.parametrize("env", [{"PSN_LK_GENERIC": "1"}, {"PSN_LK_THREADS": "64"}, {"PSN_LK_THREADS": "128"},
-                                 {"PSN_LK_THREADS": "512"}, {"PSN_LK_GENERIC": "1", "PSN_LK_THREADS": "64"}])
+@pytest.mark.parametrize("env", [{}, {"PSN_LK_ONEWAVE": "0"}, {"PSN_LK_GENERIC": "1"}, {"PSN_LK_THREADS": "64"},
+                                 {"PSN_LK_THREADS": "128"}, {"PSN_LK_THREADS": "512"},
+                                 {"PSN_LK_GENERIC": "1", "PSN_LK_THREADS": "64"}])
 @pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
 def test_lk_kernel_variants(oracle_mod, monkeypatch, env, flags):
     """The single-tile and the tiled kernel, at every workgroup size, give the
@@ -300,7 +301,10 @@ def test_lk_kernel_variants(oracle_mod, monkeypatch, env, flags):
         monkeypatch.setenv(k, v)
     sc, f0, f1 = scene_pair(10, 640, 480, 96)
     pts = sc.points_at(0)
-    for win in [(21, 21), (9, 15), (32, 32)]:
+    # one-wave mode row counts: 21x21 -> 7 rows/lane, 9x15 -> 4, 32x32 -> 16,
+    # 24x16 -> 8, 7x7 -> 4 (no SSE2 lanes), 12x70 -> 16 (4 px/thread A phase),
+    # 40x20 -> 20 rows: multi-wave iterations
+    for win in [(21, 21), (9, 15), (32, 32), (24, 16), (7, 7), (12, 70), (40, 20)]:
         ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
         gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
         assert_same(gpu, ref, f"{env} {win}")

@@ -49,6 +49,7 @@ def main():
     pro = np.stack([s[:, 50] - s[:, 60], s[:, 51] - s[:, 50], s[:, 52] - s[:, 51], s[:, 53] - s[:, 52]], 1)
     out["prologue_a_phase"] = {"mean": {k: round(float(v), 1) for k, v in zip(PRO, pro.mean(0))},
                                "slowest_wg": {k: int(v) for k, v in zip(PRO, pro[slow])}}
+    out["ow_setup_cycles"] = float((s[:, 54] - s[:, 53]).mean())  # one-wave mode: stamp 54 ends its setup
     prev_end = s[:, 53]
     for lev in range(3, -1, -1):
         b = lev * 10
@@ -61,13 +62,14 @@ def main():
             "cycles_per_iter": round(float(d[:, 2].sum() / max(iters.sum(), 1)), 1),
             "slowest_wg": {k: int(v) for k, v in zip(PH, d[slow])} | {"iters": int(iters[slow])},
         }
-    it = s[:, 40:46]
+    it = s[:, 40:48]
     n_it = sum(s[:, lev * 10 + 8] for lev in range(4))
     tot_it = n_it.sum()
     out["iteration_phases_cycles_per_iter"] = {
         "products": round(float(it[:, 0].sum() / tot_it), 1), "reduce_barrier": round(float(it[:, 1].sum() / tot_it), 1),
         "chain_combine": round(float(it[:, 2].sum() / tot_it), 1), "solve": round(float(it[:, 3].sum() / tot_it), 1),
-        "chain_path_fraction": round(float(it[:, 4].sum() / tot_it), 3), "restage_fraction": round(float(it[:, 5].sum() / tot_it), 3)}
+        "chain_path_fraction": round(float(it[:, 4].sum() / tot_it), 3), "restage_fraction": round(float(it[:, 5].sum() / tot_it), 3),
+        "class_path_fraction": round(float(it[:, 6].sum() / tot_it), 3)}
     t0 = s[:, 60].min()
     ends = (s[:, 61] - t0) / 1e3
     out["wg_end_kcycles_percentiles"] = {str(q): round(float(np.percentile(ends, q)), 1) for q in (10, 50, 90, 99, 100)}
