@@ -460,7 +460,7 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     d.ow_rg = (h + d.ow_g - 1) / d.ow_g;
     d.dv_w = psn::div_magic(w);
     d.dv_dw = psn::div_magic(w + 1);
-    d.dv_pw = psn::div_magic(w + 3);
+    d.dv_pm = psn::div_magic(psn::lk_pat_m(w));
     d.dv_jrw = psn::div_magic(jrw);
     d.dv_jrw4 = psn::div_magic(jrw / 4);
     d.dv_g = psn::div_magic(d.ow_g);

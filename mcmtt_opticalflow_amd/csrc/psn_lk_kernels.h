@@ -44,7 +44,7 @@ struct LkQueryDev {
     double eps2;
     // division magics (q = n * dv >> 22, exact for n, d < 1024) of the per-query
     // divisors the single-tile kernel needs, and its one-wave lane geometry
-    unsigned dv_w, dv_dw, dv_pw, dv_jrw, dv_jrw4, dv_g, dv_cw;
+    unsigned dv_w, dv_dw, dv_pm, dv_jrw, dv_jrw4, dv_g, dv_cw;
     int ow_g, ow_rg, pad2_;
 };
 __host__ __device__ inline unsigned div_magic(int d) { return d > 0 ? ((1u << 22) + (unsigned)d - 1u) / (unsigned)d : 0u; }
@@ -145,6 +145,11 @@ __host__ __device__ inline int ow_rows(int w, int h) {
     return G ? (h + G - 1) / G : 1 << 30;
 }
 constexpr int kOwMaxRows = 16;
+// I patch of a level in LDS: (h + 3) rows of bytes, row stride lk_pat_rs(w) =
+// 4 * lk_pat_m(w): the w + 3 patch pixels start at byte (gx0 & 3) of a row, so
+// every row moves as lk_pat_m(w) aligned dwords (LDS-DMA).
+__host__ __device__ inline int lk_pat_m(int w) { return (w + 3 + 3 + 3) >> 2; }
+__host__ __device__ inline int lk_pat_rs(int w) { return 4 * lk_pat_m(w); }
 struct LkStLayout {
     int tbl, ri, lv, jp, pim, pim_stride, dg, dg_stride, iw, iw_stride, r, total;
     __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev, bool ow = false) {
@@ -154,7 +159,7 @@ struct LkStLayout {
         lv = ri + kStRiInts * 4;
         jp = kStScratchBytes;                      // fused builds use LDS from here
         pim = jp + (ow ? 8 * st_jp_cm_dw(w, h) : align16(4 * st_jreg_w(w) * st_jreg_h(h)));
-        pim_stride = align16(4 * (h + 3) * (w + 3));
+        pim_stride = align16((h + 3) * lk_pat_rs(w));
         dg = pim + nlev * pim_stride;
         dg_stride = align16(4 * (h + 1) * (w + 1));
         iw = dg + nlev * dg_stride;

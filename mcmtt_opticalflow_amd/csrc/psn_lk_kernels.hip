@@ -27,9 +27,12 @@ namespace psn {
 
 // Diagnostic build (-DPSN_LK_STAMPS): shader-clock stamps of workgroup phases.
 #ifdef PSN_LK_STAMPS
-#define LK_STAMP(slot)                                                                                   \
-    do {                                                                                                 \
-        if (threadIdx.x == 0 && A.stamps) A.stamps[(size_t)blockIdx.x * 64 + (slot)] = __builtin_amdgcn_s_memtime(); \
+// ordered: the stamp is taken where it stands in program order (issue time)
+#define LK_STAMP(slot)                                                                            \
+    do {                                                                                          \
+        unsigned long long t_s;                                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_s) : : "memory");             \
+        if (threadIdx.x == 0 && A.stamps) A.stamps[(size_t)blockIdx.x * 64 + (slot)] = t_s;      \
     } while (0)
 #define LK_COUNT(slot, v)                                                          \
     do {                                                                           \
@@ -1050,6 +1053,37 @@ __device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int
         }
     }
 }
+// The I patch of one level (PH rows, lk_pat_m(w) dwords per row from the
+// aligned-down column gx0 & ~3) into LDS bytes: interior patches move as
+// aligned dwords by LDS-DMA (lane i of a chunk lands at dst + 4 * i, so the
+// chunk of dwords c0.. is contiguous in LDS); patches crossing the image border
+// gather their bytes through reflect-101 with plain loads and byte stores.
+template <int NT>
+__device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m,
+                                          unsigned dv_m) {
+    const int ax = gx0 & ~3;
+    const int n = PH * m;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w) {
+        // the row's last dword may read up to 6 bytes past the image width:
+        // inside the 256-B pitch, the next row, or the ring's slack
+        for (int c0 = wid * 64; c0 < n; c0 += NT) {
+            const int q = c0 + lane;
+            if (q < n) {
+                const int r = qdiv(q, dv_m), j = q - r * m;
+                const uint8_t *src = L.p + (size_t)(gy0 + r) * L.pitch + ax + 4 * j;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + 4 * c0), 4, 0, 0);
+            }
+        }
+    } else {
+        const int rb = 4 * m;
+        for (int q = threadIdx.x; q < PH * rb; q += NT) {
+            const int r = qdiv(q >> 2, dv_m), c = q - r * rb;
+            const int gy = refl101(gy0 + r, L.h), gx = refl101(ax + c, L.w);
+            dst[q] = L.p[(size_t)gy * L.pitch + gx];
+        }
+    }
+}
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 
@@ -1202,6 +1236,37 @@ __device__ __forceinline__ LevelDev ring_level(const RingGeo &r, int slot, int l
     return L;
 }
 
+// The same for a uniform runtime level: an unrolled select over static
+// kernel-argument offsets (the scalar loads issue together, no dependent
+// load per level).
+__device__ __forceinline__ LevelDev ring_level_u(const RingGeo &r, int slot, int level) {
+    LevelDev L = ring_level(r, slot, 0);
+#pragma unroll
+    for (int l = 1; l < kPyrMaxTop + 1; l++)
+        if (level == l) L = ring_level(r, slot, l);
+    return L;
+}
+// Level table in LDS (single-tile kernel): entry (pyramid s, level l) = 8 ints
+// {ptr lo, ptr hi, w, h, pitch}; s = 0 the I (prev) pyramid, 1 the J (next).
+__device__ __forceinline__ void tbl_put(int *tbl, int s, int l, const LevelDev &L) {
+    int *e = tbl + (s * kMaxLevels + l) * 8;
+    const unsigned long long pv = (unsigned long long)L.p;
+    *(int4 *)e = make_int4((int)(unsigned)pv, (int)(unsigned)(pv >> 32), L.w, L.h);
+    e[4] = L.pitch;
+}
+__device__ __forceinline__ LevelDev tbl_get(const int *tbl, int s, int l) {
+    const int *e = tbl + (s * kMaxLevels + l) * 8;
+    const int4 a = *(const int4 *)e;
+    LevelDev L;
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane(a.x), hi = (unsigned)__builtin_amdgcn_readfirstlane(a.y);
+    L.p = (uint8_t *)(((unsigned long long)hi << 32) | lo);
+    L.w = __builtin_amdgcn_readfirstlane(a.z);
+    L.h = __builtin_amdgcn_readfirstlane(a.w);
+    L.pitch = __builtin_amdgcn_readfirstlane(e[4]);
+    L.pad_ = 0;
+    return L;
+}
+
 // v_dot2_i32_i16: a.lo*b.lo + a.hi*b.hi + c on signed 16-bit halves. Signed
 // because iw11 = 2^14 - iw00 - iw01 - iw10 is -1 when the three rounded
 // weights overshoot (tiny fractional offsets); pixels (<= 255) are positive.
@@ -1210,6 +1275,13 @@ __device__ __forceinline__ int sdot2(unsigned a, unsigned b, int c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, b), c, false);
 }
 __device__ __forceinline__ unsigned pack_w(int lo, int hi) { return ((unsigned)lo & 0xffffu) | ((unsigned)hi << 16); }
+// sdot2 in the VOP3 form (separate accumulator input and result: no copy of a
+// loop-invariant accumulator into the tied VOP2 destination)
+__device__ __forceinline__ int sdot2v(unsigned a, unsigned b, int c) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // v_dot2_u32_u16: a.lo*b.lo + a.hi*b.hi + c on unsigned 16-bit halves.
@@ -1305,6 +1377,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     const bool sse = (flags & PSN_LK_ACCUM_SCALAR) == 0;
     const int JRW = st_jreg_w(w), JRH = st_jreg_h(h);
     const int PW = w + 3, DW = w + 1;
+    const int RS = lk_pat_rs(w);  // I patch row stride (bytes)
 
     const LkStLayout lay(w, h, sse, nlev, E > 0);
     int *RI = (int *)(smem + lay.ri);
@@ -1326,7 +1399,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         const int y = qdiv(i, Q.dv_w), x = i - y * w;
         pix[k] = i;
         ofsJ[k] = y * JRW + x;
-        ofsP[k] = (y + 1) * PW + x + 1;
+        ofsP[k] = (y + 1) * RS + x + 1;
         ofsD[k] = y * DW + x;
         posA_[k] = ev[k] ? posA(GA, y, x) : 4 * GA.S + GA.lenT;
         posB_[k] = ev[k] ? posB(GB, y, x) : 4 * GB.S + GB.lenT;
@@ -1348,13 +1421,29 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         NPx = A.next[2 * pi];
         NPy = A.next[2 * pi + 1];
     }
+#ifdef PSN_LK_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // point landed
+    LK_STAMP(58);
+#endif
 
     // ---- the I patch of every level by LDS-DMA; the coarsest J region into registers ----
-    for (int l = 0; l <= maxL; l++) {
+#pragma unroll
+    for (int l = 0; l < kStMaxLev; l++) {
+        if (l > maxL) break;
         const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
         const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
         if (!gg.valid) continue;
-        dma_region<NT>((uint32_t *)(smem + lay.pim + l * lay.pim_stride), I, gg.ipy - 1, gg.ipx - 1, PW, h + 3, Q.dv_pw);
+        dma_patch<NT>(smem + lay.pim + l * lay.pim_stride, I, gg.ipy - 1, gg.ipx - 1, PW, h + 3, lk_pat_m(w), Q.dv_pm);
+    }
+    // level table for the level loops (ordered by the barrier below)
+    int *TBL = (int *)(smem + lay.tbl);
+    if (tid < 2 * kStMaxLev) {
+        const int ts = tid >= kStMaxLev ? 1 : 0, tl = tid - ts * kStMaxLev;
+        LevelDev L = ring_level(A.ring, ts ? Q.next_slot : Q.prev_slot, 0);
+#pragma unroll
+        for (int l = 1; l < kStMaxLev; l++)
+            if (tl == l) L = ring_level(A.ring, ts ? Q.next_slot : Q.prev_slot, l);
+        tbl_put(TBL, ts, tl, L);
     }
     JPStage<NT> pf;  // prefetched J region of level pf_level at (pf_y0, pf_x0)
     int pf_level, pf_x0, pf_y0;
@@ -1365,8 +1454,9 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         pf_x0 = (cv_floor(__fsub_rn(nx0, hwx)) - kStJMargin) & ~3;
         pf_y0 = cv_floor(__fsub_rn(ny0, hwy)) - kStJMargin;
         pf_level = maxL;
-        pf.load(ring_level(A.ring, Q.next_slot, maxL), pf_y0, pf_x0, JRW, JRH, wk_int, wk_bord);
+        pf.load(ring_level_u(A.ring, Q.next_slot, maxL), pf_y0, pf_x0, JRW, JRH, wk_int, wk_bord);
     }
+    LK_STAMP(59);
     dma_wait();
     __syncthreads();
     LK_STAMP(50);
@@ -1375,11 +1465,13 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     // flow): Scharr of every patch; window values, tensor products and sums;
     // one reduction barrier; wave 0 sums the float chains of every level in
     // parallel lanes and writes the per-level solver table LV ----
-    for (int l = 0; l <= maxL; l++) {
+#pragma unroll
+    for (int l = 0; l < kStMaxLev; l++) {
+        if (l > maxL) break;
         const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
         const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
         if (!gg.valid) continue;
-        const uint32_t *P = (const uint32_t *)(smem + lay.pim + l * lay.pim_stride);
+        const uint8_t *P = smem + lay.pim + l * lay.pim_stride + ((gg.ipx - 1) & 3);
         short2 *Dg = (short2 *)(smem + lay.dg + l * lay.dg_stride);
         Walk wk;
         wk.init_m(tid, NT, DW, Q.dv_dw);
@@ -1387,10 +1479,10 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             const int gy = gg.ipy + wk.y, gx = gg.ipx + wk.x;
             short2 d = make_short2(0, 0);
             if ((unsigned)gy < (unsigned)I.h && (unsigned)gx < (unsigned)I.w) {
-                const uint32_t *p = P + wk.y * PW + wk.x;
+                const uint8_t *p = P + wk.y * RS + wk.x;
                 const int a0 = p[0], a1 = p[1], a2 = p[2];
-                const int b0 = p[PW], b2 = p[PW + 2];
-                const int c0 = p[2 * PW], c1 = p[2 * PW + 1], c2 = p[2 * PW + 2];
+                const int b0 = p[RS], b2 = p[RS + 2];
+                const int c0 = p[2 * RS], c1 = p[2 * RS + 1], c2 = p[2 * RS + 2];
                 d.x = (short)(3 * (a2 + c2) + 10 * b2 - 3 * (a0 + c0) - 10 * b0);
                 d.y = (short)(3 * ((c0 - a0) + (c2 - a2)) + 10 * (c1 - a1));
             }
@@ -1410,15 +1502,15 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         unsigned s11 = 0, s22 = 0;
         int s12 = 0;
         if (gg.valid) {
-            const uint32_t *P = (const uint32_t *)(smem + lay.pim + l * lay.pim_stride);
+            const uint8_t *P = smem + lay.pim + l * lay.pim_stride + ((gg.ipx - 1) & 3);
             const short2 *Dg = (const short2 *)(smem + lay.dg + l * lay.dg_stride);
             int2 *IW = (int2 *)(smem + lay.iw + l * lay.iw_stride);
             float *PA = R + l * 3 * GA.P;
 #pragma unroll
             for (int k = 0; k < EPT; k++) {
-                const uint32_t *p = P + ofsP[k];
+                const uint8_t *p = P + ofsP[k];
                 const int iw = PSN_DESCALE(__mul24((int)p[0], gg.w00) + __mul24((int)p[1], gg.w01) +
-                                               __mul24((int)p[PW], gg.w10) + __mul24((int)p[PW + 1], gg.w11), 9);
+                                               __mul24((int)p[RS], gg.w10) + __mul24((int)p[RS + 1], gg.w11), 9);
                 const short2 *d = Dg + ofsD[k];
                 const short2 d00 = d[0], d01 = d[1], d10 = d[DW], d11 = d[DW + 1];
                 int ix = PSN_DESCALE(__mul24((int)d00.x, gg.w00) + __mul24((int)d01.x, gg.w01) +
@@ -1596,8 +1688,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
 
         for (int level = maxL; level >= 0; level--) {
             LK_STAMP(level * 10 + 0);
-            const LevelDev I = ring_level(A.ring, Q.prev_slot, level);
-            const LevelDev J = ring_level(A.ring, Q.next_slot, level);
+            const LevelDev I = tbl_get(TBL, 0, level);
+            const LevelDev J = tbl_get(TBL, 1, level);
             const int cols = I.w, rows = I.h;
             const float scale = ldexpf(1.f, -level);
             float nx, ny;
@@ -1635,7 +1727,11 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 const int iny0 = __builtin_amdgcn_readfirstlane(cv_floor(ny));
                 if (pf_level == level && inx0 >= pf_x0 && iny0 >= pf_y0 && inx0 + w + 1 <= pf_x0 + JRW &&
                     iny0 + h + 1 <= pf_y0 + JRH) {
-                    if (pf_regs) pf.store(JC);
+                    if (pf_regs) {
+                        LK_STAMP(55);
+                        pf.store(JC);
+                        LK_STAMP(56);
+                    }
                     jr_x0 = pf_x0;
                     jr_y0 = pf_y0;
                 } else {
@@ -1658,7 +1754,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 if (level > 0) {
                     JPStage<NT> cp;
                     cp.cs = JRHc;
-                    cp.copy(buf ? JPB0 : JPB1, ring_level(A.ring, Q.next_slot, level - 1), pf_y0, pf_x0, JRW, JRH,
+                    cp.copy(buf ? JPB0 : JPB1, tbl_get(TBL, 1, level - 1), pf_y0, pf_x0, JRW, JRH,
                             wkh_int, wkh_bord);
                 }
             } else if (run) {
@@ -1666,7 +1762,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 // the lane's window rows, two rows per dword (int16 halves): I, Ix,
                 // Iy, |Ix| + |Iy|; rows past the window carry zero gradients
                 constexpr int E2 = (E + 1) / 2;
-                unsigned IwP[E2], IxP[E2], IyP[E2], SxyP[E2];
+                unsigned IxP[E2], IyP[E2], SxyP[E2];
+                int Cw[2 * E2];  // 256 - 512 * I: the bilinear sum plus Cw, >> 9, is J* - I*
                 int Iw_[E];
                 {
                     const int2 *IW = (const int2 *)(smem + lay.iw + level * lay.iw_stride);
@@ -1683,7 +1780,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                     }
 #pragma unroll
                     for (int q = 0; q < E2; q++) {
-                        IwP[q] = pack_w(iw[2 * q], iw[2 * q + 1]);
+                        Cw[2 * q] = 256 - 512 * iw[2 * q];
+                        Cw[2 * q + 1] = 256 - 512 * iw[2 * q + 1];
                         IxP[q] = pack_w(ix[2 * q], ix[2 * q + 1]);
                         IyP[q] = pack_w(iy[2 * q], iy[2 * q + 1]);
                         SxyP[q] = pack_w(abs(ix[2 * q]) + abs(iy[2 * q]), abs(ix[2 * q + 1]) + abs(iy[2 * q + 1]));
@@ -1705,10 +1803,10 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                     a = 0;
 #pragma unroll
                     for (int q = 0; q < E2; q++) {
-                        const int j0 = sdot2(rr[2 * q + 1], W1, sdot2(rr[2 * q], W0, 1 << 8)) >> 9;
-                        const int j1 = sdot2(rr[2 * q + 2], W1, sdot2(rr[2 * q + 1], W0, 1 << 8)) >> 9;
-                        const s16x2 d = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((unsigned)j1, (unsigned)j0, 0x05040100u)) -
-                                        __builtin_bit_cast(s16x2, IwP[q]);
+                        // (sum + 256) >> 9 - I == (sum + 256 - 512 I) >> 9: the diffs directly
+                        const int d0 = sdot2v(rr[2 * q + 1], W1, sdot2v(rr[2 * q], W0, Cw[2 * q])) >> 9;
+                        const int d1 = sdot2v(rr[2 * q + 2], W1, sdot2v(rr[2 * q + 1], W0, Cw[2 * q + 1])) >> 9;
+                        const s16x2 d = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm((unsigned)d1, (unsigned)d0, 0x05040100u));
                         dP[q] = __builtin_bit_cast(unsigned, d);
                         s1 = sdot2(dP[q], IxP[q], s1);
                         s2 = sdot2(dP[q], IyP[q], s2);
@@ -1920,8 +2018,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     } else {
     for (int level = maxL; level >= 0; level--) {
         LK_STAMP(level * 10 + 0);
-        const LevelDev I = ring_level(A.ring, Q.prev_slot, level);
-        const LevelDev J = ring_level(A.ring, Q.next_slot, level);
+        const LevelDev I = tbl_get(TBL, 0, level);
+        const LevelDev J = tbl_get(TBL, 1, level);
         const int cols = I.w, rows = I.h;
         const float scale = ldexpf(1.f, -level);
         float nx, ny;
@@ -1973,7 +2071,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             pf_x0 = (cv_floor(__fsub_rn(__fmul_rn(NPx, 2.f), hwx)) - kStJMargin) & ~3;
             pf_y0 = cv_floor(__fsub_rn(__fmul_rn(NPy, 2.f), hwy)) - kStJMargin;
             pf_level = level - 1;
-            pf.load(ring_level(A.ring, Q.next_slot, level - 1), pf_y0, pf_x0, JRW, JRH, wk_int, wk_bord);
+            pf.load(tbl_get(TBL, 1, level - 1), pf_y0, pf_x0, JRW, JRH, wk_int, wk_bord);
         }
         if (!run) continue;
         __syncthreads();  // JP published (every wave finished the previous level's reads)
