@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PSN_LK_ABI_VERSION 2
+#define PSN_LK_ABI_VERSION 3
 
 #define PSN_LK_OK 0
 #define PSN_LK_ERR_ARG (-1)
@@ -162,6 +162,40 @@ int psn_lk_timing_stats(psn_lk_ctx *ctx, int *n_push, double *push_ms, int *n_tr
  * shader-clock stamps of every LK workgroup's phases into a device buffer of
  * 64 u64 per workgroup. Returns PSN_LK_ERR_UNSUPPORTED in product builds. */
 int psn_lk_debug_set_stamps(psn_lk_ctx *ctx, void *d_stamps);
+
+/* ---- GridFAST feature extraction on a ring slot's frame ----
+ * Replaces, per detection of the backward chain (PSNWhere_Tracker2D.cpp:734-757):
+ *   m_matMaskForFeature(rectROI) = 255;
+ *   m_detector->detect(gray, newKeypoints, m_matMaskForFeature);   // "GridFAST", :142
+ *   std::random_shuffle(newKeypoints); currFeatures = first min(n, 100) points
+ * FeatureDetector::create("GridFAST") in OpenCV 2.4.6 = GridAdaptedFeatureDetector
+ * (FastFeatureDetector(threshold 10, nonmaxSuppression true), maxTotalKeypoints
+ * 1000, 4 x 4 grid); psn_gridfast_default_params() fills those values and
+ * cap = PSN_2D_FEATURE_MAX_NUM_TRACK (100).
+ * rois: nroi x {x, y, w, h} ints = rectROI (box.cropWithSize(cols, rows).cv(),
+ * :736), clipped to the image here; an empty roi yields no keypoints.
+ * Outputs per roi i: out_total[i] = newKeypoints.size() (the caller's
+ * "< PSN_2D_FEATURE_MIN_NUM_TRACK" test, :744; nullable), out_count[i] =
+ * min(total, cap), out_xy[i * cap * 2 ...] the points.
+ * Fixed choices where the reference is unspecified: keepStrongest ties at a
+ * cell's cut keep the earlier keypoint in row-major order; random_shuffle is
+ * replaced by ordering the candidates by a hash of (seed, roi index, candidate
+ * index) -- a seeded uniform permutation; same seed, same points.
+ * Limits: grid cells <= 256, max_total <= 4096, cell width <= 1030 px.
+ * Host variant synchronous; _device variant async with device out pointers. */
+typedef struct psn_gridfast_params {
+    int threshold;  /* FAST threshold (default 10), clamped to [0, 255] */
+    int nonmax;     /* nonmaxSuppression (default 1) */
+    int max_total;  /* maxTotalKeypoints (default 1000); per cell = max_total / cells */
+    int grid_rows;  /* default 4 */
+    int grid_cols;  /* default 4 */
+    int cap;        /* points kept after the shuffle (default 100) */
+} psn_gridfast_params;
+void psn_gridfast_default_params(psn_gridfast_params *p);
+int psn_gridfast_detect(psn_lk_ctx *ctx, int slot, const int *rois, int nroi, const psn_gridfast_params *p,
+                        uint32_t seed, float *out_xy, int *out_count, int *out_total);
+int psn_gridfast_detect_device(psn_lk_ctx *ctx, int slot, const int *rois, int nroi, const psn_gridfast_params *p,
+                               uint32_t seed, float *d_out_xy, int *d_out_count, int *d_out_total);
 
 /* ---- multi-GPU: per-camera tracklet slots all-gathered over RCCL/xGMI ----
  * Replaces the in-process std::vector<stTrack2DResult> hand-off into

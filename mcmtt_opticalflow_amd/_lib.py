@@ -64,6 +64,17 @@ class LkQuery(ctypes.Structure):
     ]
 
 
+class GridFastParams(ctypes.Structure):
+    _fields_ = [
+        ("threshold", ctypes.c_int),
+        ("nonmax", ctypes.c_int),
+        ("max_total", ctypes.c_int),
+        ("grid_rows", ctypes.c_int),
+        ("grid_cols", ctypes.c_int),
+        ("cap", ctypes.c_int),
+    ]
+
+
 def header_functions() -> list[str]:
     """Names of every function declared in include/psn_lk.h."""
     src = open(HEADER_PATH).read()
@@ -107,6 +118,11 @@ def load():
                                       ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double)]
     L.psn_lk_debug_set_stamps.argtypes = [vp, vp]
     L.psn_lk_set_ingest_overlap.argtypes = [vp, ip]
+    L.psn_gridfast_default_params.argtypes = [ctypes.POINTER(GridFastParams)]
+    L.psn_gridfast_default_params.restype = None
+    gfa = [vp, ip, vp, ip, ctypes.POINTER(GridFastParams), ctypes.c_uint32, vp, vp, vp]
+    L.psn_gridfast_detect.argtypes = gfa
+    L.psn_gridfast_detect_device.argtypes = gfa
     L.psn_comm_get_unique_id.argtypes = [vp]
     L.psn_comm_init.argtypes = [ip, ip, ip, vp, ctypes.POINTER(vp)]
     L.psn_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]

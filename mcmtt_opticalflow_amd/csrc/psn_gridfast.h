@@ -1,0 +1,33 @@
+// Internal (non-ABI) declarations of the GridFAST kernels (psn_gridfast.hip).
+// Public surface: psn_gridfast_* in include/psn_lk.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psn {
+
+constexpr int kGfMaxRois = 64;      // rois per launch (kernel-argument table)
+constexpr int kGfStrip = 16;        // output rows per LDS strip
+constexpr int kGfMaxRegionW = 1024; // widest cell detection region (cell width - 6)
+constexpr int kGfMaxTotal = 4096;   // maxTotalKeypoints limit (selection sort in LDS)
+
+struct GridFastArgs {
+    const uint8_t *img;  // level 0 of a ring slot (the frame's gray image)
+    int w, h, pitch;
+    int nroi;
+    int roi_base;        // index of rois[0] in the caller's array (shuffle key)
+    int threshold, nonmax, grid_rows, grid_cols, per_cell, cap;
+    uint32_t seed;
+    uint32_t *cell_kp;   // [nroi][ncell][per_cell] packed x | y << 16
+    int *cell_cnt;       // [nroi][ncell]
+    float *out_xy;       // [nroi][cap][2] (rows of rois[0..nroi))
+    int *out_count;      // [nroi] min(total, cap)
+    int *out_total;      // [nroi] keypoints before the cap (newKeypoints.size())
+    int4 rois[kGfMaxRois];
+};
+
+// Both launches (per-cell detection, per-roi selection) on stream s.
+hipError_t launch_gridfast(const GridFastArgs &a, hipStream_t s);
+
+}  // namespace psn

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "psn_lk.h"
+#include "psn_gridfast.h"
 #include "psn_lk_kernels.h"
 
 using psn::LevelDev;
@@ -57,6 +58,14 @@ struct psn_lk_ctx {
     bool force_generic = false;
     bool onewave = true;  // PSN_LK_ONEWAVE=0: multi-wave iterations in the single-tile kernel
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
+    // GridFAST scratch (per-cell keypoints of one launch) and host-call outputs
+    uint32_t *d_gf_kp = nullptr;
+    int *d_gf_cnt = nullptr;
+    size_t gf_kp_cap = 0, gf_cnt_cap = 0;
+    float *d_gf_xy = nullptr;
+    int *d_gf_oc = nullptr, *d_gf_ot = nullptr;
+    size_t gf_out_cap = 0;  // rois x cap floats pairs
+    int gf_nroi_cap = 0;
     // timing: event ring, 2 events per timed call
     int tcap = 0;
     std::vector<hipEvent_t> ev_push, ev_track;
@@ -213,7 +222,8 @@ void psn_lk_destroy(psn_lk_ctx *c) {
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
     for (void *p : {(void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
-                    (void *)c->d_err, (void *)c->d_status})
+                    (void *)c->d_err, (void *)c->d_status, (void *)c->d_gf_kp, (void *)c->d_gf_cnt, (void *)c->d_gf_xy,
+                    (void *)c->d_gf_oc, (void *)c->d_gf_ot})
         if (p) (void)hipFree(p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->ingest_stream) (void)hipStreamDestroy(c->ingest_stream);
@@ -693,6 +703,142 @@ int psn_lk_read_level(psn_lk_ctx *c, int slot, int level, uint8_t *host, int str
     rc = wait_slot_ready(c, slot);
     if (rc) return rc;
     HIPCHK(c, hipMemcpy2DAsync(host, stride, L.p, L.pitch, L.w, L.h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PSN_LK_OK;
+}
+
+// ---- GridFAST (include/psn_lk.h; kernels in psn_gridfast.hip) ----
+
+void psn_gridfast_default_params(psn_gridfast_params *p) {
+    if (!p) return;
+    p->threshold = 10;  // FastFeatureDetector(10, true)
+    p->nonmax = 1;
+    p->max_total = 1000;  // GridAdaptedFeatureDetector(detector, 1000, 4, 4)
+    p->grid_rows = 4;
+    p->grid_cols = 4;
+    p->cap = 100;  // PSN_2D_FEATURE_MAX_NUM_TRACK (PSNWhere_Tracker2D.cpp:13)
+}
+
+static int gridfast_impl(psn_lk_ctx *c, int slot, const int *rois, int nroi, const psn_gridfast_params *pp,
+                         uint32_t seed, float *d_xy, int *d_cnt, int *d_tot) {
+    psn_gridfast_params p;
+    if (pp)
+        p = *pp;
+    else
+        psn_gridfast_default_params(&p);
+    const int ncell = p.grid_rows * p.grid_cols;
+    if (p.grid_rows <= 0 || p.grid_cols <= 0 || ncell > 256 || p.max_total > psn::kGfMaxTotal || p.cap < 0)
+        return set_err(c, PSN_LK_ERR_ARG, "gridfast: grid %dx%d, max_total %d, cap %d", p.grid_rows, p.grid_cols,
+                       p.max_total, p.cap);
+    if ((c->width + p.grid_cols - 1) / p.grid_cols - 6 > psn::kGfMaxRegionW)
+        return set_err(c, PSN_LK_ERR_UNSUPPORTED, "gridfast: cell width above %d", psn::kGfMaxRegionW + 6);
+    if (slot < 0 || slot >= c->nslots || !c->filled[slot]) return set_err(c, PSN_LK_ERR_SLOT, "slot %d not filled", slot);
+    if (nroi == 0) return PSN_LK_OK;
+    // the frame must be in the slot: a deferred build of it runs first
+    if (c->pend && c->pend_slot == slot) {
+        int rc = flush_pending(c);
+        if (rc) return rc;
+    }
+    int rc = wait_slot_ready(c, slot);
+    if (rc) return rc;
+    psn::GridFastArgs a{};
+    const LevelDev &L = c->h_slots[(size_t)slot * psn::kMaxLevels];
+    a.img = L.p;
+    a.w = L.w;
+    a.h = L.h;
+    a.pitch = L.pitch;
+    a.threshold = std::min(std::max(p.threshold, 0), 255);
+    a.nonmax = p.nonmax ? 1 : 0;
+    a.grid_rows = p.grid_rows;
+    a.grid_cols = p.grid_cols;
+    // GridAdaptedFeatureDetector: nothing when maxTotalKeypoints < cells
+    a.per_cell = p.max_total >= ncell ? p.max_total / ncell : 0;
+    a.cap = p.cap;
+    a.seed = seed;
+    const size_t kp_need = (size_t)psn::kGfMaxRois * ncell * std::max(a.per_cell, 1);
+    if (c->gf_kp_cap < kp_need) {
+        if (c->d_gf_kp) (void)hipFree(c->d_gf_kp);
+        c->d_gf_kp = nullptr;
+        c->gf_kp_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_gf_kp, kp_need * sizeof(uint32_t)));
+        c->gf_kp_cap = kp_need;
+    }
+    const size_t cnt_need = (size_t)psn::kGfMaxRois * ncell;
+    if (c->gf_cnt_cap < cnt_need) {
+        if (c->d_gf_cnt) (void)hipFree(c->d_gf_cnt);
+        c->d_gf_cnt = nullptr;
+        c->gf_cnt_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_gf_cnt, cnt_need * sizeof(int)));
+        c->gf_cnt_cap = cnt_need;
+    }
+    a.cell_kp = c->d_gf_kp;
+    a.cell_cnt = c->d_gf_cnt;
+    for (int base = 0; base < nroi; base += psn::kGfMaxRois) {
+        const int n = std::min(psn::kGfMaxRois, nroi - base);
+        a.nroi = n;
+        a.roi_base = base;
+        a.out_xy = d_xy + (size_t)base * p.cap * 2;
+        a.out_count = d_cnt + base;
+        a.out_total = d_tot ? d_tot + base : nullptr;
+        for (int i = 0; i < n; i++) {
+            const int *r = rois + 4 * (size_t)(base + i);
+            // clip to the image (cropWithSize already did for the reference's rois)
+            int x0 = std::max(r[0], 0), y0 = std::max(r[1], 0);
+            int x1 = std::min((long long)r[0] + r[2], (long long)c->width) > x0 ? (int)std::min((long long)r[0] + r[2], (long long)c->width) : x0;
+            int y1 = std::min((long long)r[1] + r[3], (long long)c->height) > y0 ? (int)std::min((long long)r[1] + r[3], (long long)c->height) : y0;
+            if (r[2] <= 0 || r[3] <= 0) x1 = x0, y1 = y0;
+            a.rois[i] = make_int4(x0, y0, x1 - x0, y1 - y0);
+        }
+        HIPCHK(c, psn::launch_gridfast(a, c->stream));
+    }
+    if (c->overlap == PSN_LK_OVERLAP_STREAM) {  // a later build into this slot waits for these reads
+        HIPCHK(c, hipEventRecord(c->slot_free[slot], c->stream));
+        c->free_rec[slot] = 1;
+    }
+    return PSN_LK_OK;
+}
+
+int psn_gridfast_detect_device(psn_lk_ctx *c, int slot, const int *rois, int nroi, const psn_gridfast_params *p,
+                               uint32_t seed, float *d_out_xy, int *d_out_count, int *d_out_total) {
+    if (!c || nroi < 0 || (nroi > 0 && (!rois || !d_out_xy || !d_out_count))) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    return gridfast_impl(c, slot, rois, nroi, p, seed, d_out_xy, d_out_count, d_out_total);
+}
+
+int psn_gridfast_detect(psn_lk_ctx *c, int slot, const int *rois, int nroi, const psn_gridfast_params *pp,
+                        uint32_t seed, float *out_xy, int *out_count, int *out_total) {
+    if (!c || nroi < 0 || (nroi > 0 && (!rois || !out_xy || !out_count))) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    psn_gridfast_params p;
+    if (pp)
+        p = *pp;
+    else
+        psn_gridfast_default_params(&p);
+    if (nroi == 0 || p.cap < 0) return gridfast_impl(c, slot, rois, nroi, &p, seed, nullptr, nullptr, nullptr);
+    const size_t xy_need = (size_t)nroi * std::max(p.cap, 1) * 2;
+    if (c->gf_out_cap < xy_need) {
+        if (c->d_gf_xy) (void)hipFree(c->d_gf_xy);
+        c->d_gf_xy = nullptr;
+        c->gf_out_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_gf_xy, xy_need * sizeof(float)));
+        c->gf_out_cap = xy_need;
+    }
+    if (c->gf_nroi_cap < nroi) {
+        for (int **q : {&c->d_gf_oc, &c->d_gf_ot})
+            if (*q) (void)hipFree(*q), *q = nullptr;
+        c->gf_nroi_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_gf_oc, (size_t)nroi * sizeof(int)));
+        HIPCHK(c, hipMalloc(&c->d_gf_ot, (size_t)nroi * sizeof(int)));
+        c->gf_nroi_cap = nroi;
+    }
+    int rc = gridfast_impl(c, slot, rois, nroi, &p, seed, c->d_gf_xy, c->d_gf_oc, c->d_gf_ot);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(out_count, c->d_gf_oc, (size_t)nroi * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (out_total)
+        HIPCHK(c, hipMemcpyAsync(out_total, c->d_gf_ot, (size_t)nroi * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (p.cap > 0)
+        HIPCHK(c, hipMemcpyAsync(out_xy, c->d_gf_xy, (size_t)nroi * p.cap * 2 * sizeof(float), hipMemcpyDeviceToHost,
+                                 c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PSN_LK_OK;
 }

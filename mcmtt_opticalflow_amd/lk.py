@@ -16,7 +16,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import LkParams, LkQuery, PsnLkError
+from ._lib import GridFastParams, LkParams, LkQuery, PsnLkError
 
 
 def make_params(win_size=(21, 21), max_level=3, criteria=(3, 30, 0.01), flags=0,
@@ -35,6 +35,14 @@ def make_query(prev_slot, next_slot, first_pt, num_pts, params: LkParams) -> LkQ
     q.prev_slot, q.next_slot, q.first_pt, q.num_pts = prev_slot, next_slot, first_pt, num_pts
     q.params = params
     return q
+
+
+def gridfast_params(threshold=10, nonmax=True, max_total=1000, grid=(4, 4), cap=100) -> GridFastParams:
+    """FeatureDetector::create("GridFAST") settings + the Tracker2D point cap."""
+    p = GridFastParams()
+    p.threshold, p.nonmax, p.max_total = int(threshold), int(bool(nonmax)), int(max_total)
+    p.grid_rows, p.grid_cols, p.cap = int(grid[0]), int(grid[1]), int(cap)
+    return p
 
 
 def effective_max_level(width, height, win_w, win_h, max_level) -> int:
@@ -124,6 +132,30 @@ class LKContext:
         arr = (LkQuery * max(len(queries), 1))(*queries)
         self._check(self._L.psn_lk_track_device(self._h, arr, len(queries), d_prev, d_next, d_status, d_err),
                     "track_device")
+
+    def gridfast_detect(self, slot: int, rois, params: GridFastParams | None = None, seed: int = 0):
+        """GridFAST keypoints of slot's frame masked by each roi (x, y, w, h),
+        shuffled by `seed` and capped (PSNWhere_Tracker2D.cpp:734-757).
+        Returns (list of (n_i, 2) f32 point arrays, totals before the cap)."""
+        p = params or gridfast_params()
+        r = np.ascontiguousarray(np.asarray(rois, dtype=np.int32).reshape(-1, 4))
+        n = r.shape[0]
+        cap = max(p.cap, 0)
+        xy = np.zeros((max(n, 1), max(cap, 1), 2), np.float32)
+        cnt = np.zeros(max(n, 1), np.int32)
+        tot = np.zeros(max(n, 1), np.int32)
+        self._check(self._L.psn_gridfast_detect(self._h, slot, r.ctypes.data, n, ctypes.byref(p),
+                                                ctypes.c_uint32(seed & 0xffffffff), xy.ctypes.data,
+                                                cnt.ctypes.data, tot.ctypes.data), "gridfast_detect")
+        return [xy[i, :cnt[i]].copy() for i in range(n)], tot[:n].copy()
+
+    def gridfast_detect_device(self, slot: int, rois, params: GridFastParams | None, seed: int, d_xy: int,
+                               d_count: int, d_total: int | None):
+        p = params or gridfast_params()
+        r = np.ascontiguousarray(np.asarray(rois, dtype=np.int32).reshape(-1, 4))
+        self._check(self._L.psn_gridfast_detect_device(self._h, slot, r.ctypes.data, r.shape[0], ctypes.byref(p),
+                                                       ctypes.c_uint32(seed & 0xffffffff), d_xy, d_count, d_total),
+                    "gridfast_detect_device")
 
     def enable_timing(self, capacity: int = 1024, every: int = 1):
         """HIP-event timing of every `every`-th push (pyramid launch) / track (LK launch) call."""

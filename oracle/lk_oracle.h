@@ -78,6 +78,17 @@ int oracle_calc_optical_flow_pyr_lk(const uint8_t *prev_img, const uint8_t *next
 void oracle_set_iter_log(int *buf);
 void oracle_set_bsum_log(long long *buf);
 
+/* ---- GridFAST feature extraction (oracle/gridfast_oracle.c) ----
+ * FeatureDetector::create("GridFAST")->detect(gray, kps, mask(rect) = 255)
+ * and the shuffle + cap of PSNWhere_Tracker2D.cpp:734-757 (definitions of the
+ * reference's unspecified tie order and unseeded shuffle: gridfast_oracle.c). */
+int oracle_fast16(const uint8_t *img, int w, int h, int stride, int threshold, int nonmax, int *kx, int *ky,
+                  int *kr, int cap);
+int oracle_gridfast(const uint8_t *img, int w, int h, int stride, int rx, int ry, int rw, int rh, int threshold,
+                    int nonmax, int max_total, int grid_rows, int grid_cols, float *out_xy, int *out_resp, int cap);
+uint32_t oracle_gridfast_key(uint32_t seed, uint32_t roi, uint32_t k);
+int oracle_gridfast_select(const float *cand_xy, int n, uint32_t seed, int roi, int cap, float *out_xy);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,16 @@ def lib():
         L.oracle_lk_track_pyr.restype = ctypes.c_int
         L.oracle_calc_optical_flow_pyr_lk.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int] + common
         L.oracle_calc_optical_flow_pyr_lk.restype = ctypes.c_int
+        ip = ctypes.c_int
+        _i32p = ctypes.POINTER(ctypes.c_int)
+        L.oracle_fast16.argtypes = [_u8p, ip, ip, ip, ip, ip, _i32p, _i32p, _i32p, ip]
+        L.oracle_fast16.restype = ip
+        L.oracle_gridfast.argtypes = [_u8p, ip, ip, ip, ip, ip, ip, ip, ip, ip, ip, ip, ip, _f32p, _i32p, ip]
+        L.oracle_gridfast.restype = ip
+        L.oracle_gridfast_key.argtypes = [ctypes.c_uint32] * 3
+        L.oracle_gridfast_key.restype = ctypes.c_uint32
+        L.oracle_gridfast_select.argtypes = [_f32p, ip, ctypes.c_uint32, ip, ip, _f32p]
+        L.oracle_gridfast_select.restype = ip
         _lib = L
     return _lib
 
@@ -139,3 +149,49 @@ def calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size=(21, 21), ma
     if rc != 0:
         raise ValueError(f"oracle_calc_optical_flow_pyr_lk failed rc={rc}")
     return nxt, st, er
+
+
+# ---- GridFAST (oracle/gridfast_oracle.c) ----
+
+def fast16(img, threshold=10, nonmax=True):
+    """FAST_t<16> of OpenCV 2.4.6 on a whole image: (n, 3) int32 rows (x, y, response)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = w * h
+    kx, ky, kr = (np.empty(max(cap, 1), np.int32) for _ in range(3))
+    ip = ctypes.POINTER(ctypes.c_int)
+    n = lib().oracle_fast16(_p(img, _u8p), w, h, w, threshold, int(nonmax), _p(kx, ip), _p(ky, ip), _p(kr, ip), cap)
+    return np.stack([kx[:n], ky[:n], kr[:n]], axis=1)
+
+
+def gridfast(img, roi, threshold=10, nonmax=True, max_total=1000, grid=(4, 4)):
+    """GridAdaptedFeatureDetector(FAST)::detect(img, kps, mask = 255 on roi):
+    ((n, 2) f32 points in cell order, (n,) int32 responses)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = max(max_total, 1)
+    xy = np.empty((cap, 2), np.float32)
+    resp = np.empty(cap, np.int32)
+    n = lib().oracle_gridfast(_p(img, _u8p), w, h, w, int(roi[0]), int(roi[1]), int(roi[2]), int(roi[3]),
+                              threshold, int(nonmax), max_total, grid[0], grid[1], _p(xy, _f32p),
+                              _p(resp, ctypes.POINTER(ctypes.c_int)), cap)
+    return xy[:n].copy(), resp[:n].copy()
+
+
+def gridfast_select(cand_xy, seed, roi_index, cap=100):
+    """The seeded shuffle + cap (definition shared with the HIP kernel)."""
+    c = np.ascontiguousarray(cand_xy, dtype=np.float32).reshape(-1, 2)
+    out = np.empty((max(min(len(c), cap), 1), 2), np.float32)
+    m = lib().oracle_gridfast_select(_p(c, _f32p), len(c), seed & 0xffffffff, roi_index, cap, _p(out, _f32p))
+    return out[:m].copy()
+
+
+def gridfast_detect(img, rois, seed=0, threshold=10, nonmax=True, max_total=1000, grid=(4, 4), cap=100):
+    """Per roi: (points after shuffle + cap, total keypoints) -- what
+    psn_gridfast_detect returns."""
+    pts, tots = [], []
+    for i, r in enumerate(rois):
+        xy, _ = gridfast(img, r, threshold, nonmax, max_total, grid)
+        pts.append(gridfast_select(xy, seed, i, cap))
+        tots.append(len(xy))
+    return pts, np.asarray(tots, np.int32)
