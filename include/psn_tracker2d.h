@@ -96,6 +96,16 @@ typedef struct psn_t2d_tracker {
     int updated;                                    /* out: >= 4 points tracked, box pushed */
 } psn_t2d_tracker;
 
+/* Feature extraction of the backward chain (PSNWhere_Tracker2D.cpp:734-757) on
+ * frame t (call after psn_t2d_push_frame): GridFAST (psn_gridfast_detect with
+ * the "GridFAST" defaults) masked by each detection's rectROI =
+ * box.cropWithSize(width, height).cv() (:736), shuffled by `seed` (the
+ * reference's unseeded std::random_shuffle, :752) and capped at
+ * PSN_T2D_MAX_FEATURES. Fills dets[i].features / num_features; a detection
+ * with fewer than PSN_T2D_MIN_FEATURES points is skipped by the backward step
+ * (:744). */
+int psn_t2d_detect_features(psn_t2d *t, psn_t2d_detection *dets, int ndet, uint32_t seed);
+
 /* Track2D_BackwardFeatureTracking for all detections (batched per chain step). */
 int psn_t2d_backward(psn_t2d *t, psn_t2d_detection *dets, int ndet);
 /* Track2D_ForwardTrackingAndGetMatchingScore: cost is [valid dets][ntrk]

@@ -183,6 +183,20 @@ int psn_t2d_rotate(psn_t2d *t) {
     return 0;
 }
 
+int psn_t2d_detect_features(psn_t2d *t, psn_t2d_detection *dets, int ndet, uint32_t seed) {
+    if (!t || ndet < 0 || (ndet > 0 && !dets)) return PSN_LK_ERR_ARG;
+    std::vector<psn::Detection> d((size_t)ndet);
+    for (int i = 0; i < ndet; i++) d[(size_t)i].box = to_rect(dets[i].box);
+    std::vector<std::vector<psn::Point2f>> f;
+    const int rc = t->flow.DetectFeatures(d, seed, f);
+    if (rc) return set(t, rc);
+    for (int i = 0; i < ndet; i++) {
+        const int r = put_points(f[(size_t)i], dets[i].features, &dets[i].num_features);
+        if (r) return r;
+    }
+    return 0;
+}
+
 int psn_t2d_backward(psn_t2d *t, psn_t2d_detection *dets, int ndet) {
     if (!t || ndet < 0 || (ndet > 0 && !dets)) return PSN_LK_ERR_ARG;
     std::vector<psn::Detection> d;

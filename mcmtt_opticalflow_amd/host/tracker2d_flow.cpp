@@ -126,6 +126,36 @@ int Tracker2DFlow::PushFrame(const uint8_t *frame, int stride, int channels) {
     return PSN_LK_OK;
 }
 
+int Tracker2DFlow::DetectFeatures(const std::vector<Detection> &dets, uint32_t seed,
+                                  std::vector<std::vector<Point2f>> &features) {
+    if (!lk_) return PSN_LK_ERR_ARG;
+    const size_t n = dets.size();
+    features.assign(n, {});
+    if (n == 0) return PSN_LK_OK;
+    std::vector<int> rois(4 * n), cnt(n), tot(n);
+    for (size_t i = 0; i < n; i++) {
+        // cv::Rect((int)x, (int)y, (int)w, (int)h) of the cropped, scaled box
+        const Rect r = dets[i].box.scale(kFlowScale).cropWithSize(width_, height_);
+        rois[4 * i] = (int)r.x;
+        rois[4 * i + 1] = (int)r.y;
+        rois[4 * i + 2] = (int)r.w;
+        rois[4 * i + 3] = (int)r.h;
+    }
+    psn_gridfast_params p;
+    psn_gridfast_default_params(&p);
+    p.cap = (int)kT2dMaxFeatures;
+    gf_xy_.resize(2 * n * kT2dMaxFeatures);
+    const int rc = psn_gridfast_detect(lk_, ring_[kT2dInterval - 1], rois.data(), (int)n, &p, seed, gf_xy_.data(),
+                                       cnt.data(), tot.data());
+    if (rc) return fail(rc, "psn_gridfast_detect");
+    for (size_t i = 0; i < n; i++) {
+        const float *xy = gf_xy_.data() + 2 * kT2dMaxFeatures * i;
+        features[i].resize((size_t)cnt[i]);
+        for (int k = 0; k < cnt[i]; k++) features[i][(size_t)k] = Point2f{xy[2 * k], xy[2 * k + 1]};
+    }
+    return PSN_LK_OK;
+}
+
 void Tracker2DFlow::RotateRing() { std::rotate(ring_, ring_ + 1, ring_ + kT2dInterval); }
 
 // One launch for all jobs: points concatenated, one query per job. err is

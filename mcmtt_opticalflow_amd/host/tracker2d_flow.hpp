@@ -43,6 +43,13 @@ class Tracker2DFlow {
     // buffer circulation at the end of Run
     void RotateRing();
 
+    // Feature extraction of the backward chain (:734-757) on frame t (the
+    // newest ring slot): GridFAST masked by each detection's rectROI
+    // (box.cropWithSize(cols, rows).cv(), :736), then the seeded shuffle + cap
+    // to PSN_2D_FEATURE_MAX_NUM_TRACK. features[i] may hold < 4 points (the
+    // backward step then skips detection i, :744).
+    int DetectFeatures(const std::vector<Detection> &dets, uint32_t seed, std::vector<std::vector<Point2f>> &features);
+
     // Track2D_BackwardFeatureTracking for detections that passed the caller's
     // height gate; features[i] = detection i's points at t after shuffle + cap
     // (GridFAST stays with the caller). out = m_vecDetection2D.
@@ -94,7 +101,7 @@ class Tracker2DFlow {
     bool filled_[kT2dInterval] = {false, false, false, false};
     std::string err_;
     // batched-call staging
-    std::vector<float> xy_in_, xy_out_, err_out_;
+    std::vector<float> xy_in_, xy_out_, err_out_, gf_xy_;
     std::vector<uint8_t> st_out_;
     std::vector<psn_lk_query> queries_;
 };

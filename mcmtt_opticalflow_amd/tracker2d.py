@@ -109,6 +109,7 @@ def load():
     L.psn_t2d_last_error.restype = ctypes.c_char_p
     L.psn_t2d_push_frame.argtypes = [vp, vp, ip, ip]
     L.psn_t2d_rotate.argtypes = [vp]
+    L.psn_t2d_detect_features.argtypes = [vp, ctypes.POINTER(Detection), ip, ctypes.c_uint32]
     L.psn_t2d_backward.argtypes = [vp, ctypes.POINTER(Detection), ip]
     L.psn_t2d_forward.argtypes = [vp, ctypes.POINTER(Tracker), ip, ctypes.POINTER(Detection), ip, fp]
     L.psn_t2d_track_frame.argtypes = [vp, ctypes.POINTER(Detection), ip, ctypes.POINTER(Tracker), ip, fp]
@@ -195,6 +196,13 @@ class FlowTracker:
 
     def rotate(self):
         self._check(self._L.psn_t2d_rotate(self._h), "rotate")
+
+    def detect_features(self, dets: list[Detection], seed: int = 0):
+        """GridFAST features of each detection on frame t (fills features / num_features)."""
+        arr = (Detection * max(len(dets), 1))(*dets)
+        self._check(self._L.psn_t2d_detect_features(self._h, arr, len(dets), ctypes.c_uint32(seed & 0xffffffff)),
+                    "detect_features")
+        return list(arr)[:len(dets)]
 
     def backward(self, dets: list[Detection]):
         arr = (Detection * max(len(dets), 1))(*dets)

@@ -146,9 +146,15 @@ def _check_trackers(g, r_trk, g_cost, r_cost, what):
     np.testing.assert_array_equal(g_cost, r_cost, err_msg=what)
 
 
+def _rect_roi(b, W, H):
+    """rectROI = box.scale(1.0).cropWithSize(W, H).cv() (PSNWhere_Tracker2D.cpp:736)."""
+    x, y = max(0.0, b[0]), max(0.0, b[1])
+    return (int(x), int(y), int(min(W - x - 1, b[2])), int(min(H - y - 1, b[3])))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("merged", [False, True])
-def test_tracker2d_sequence_matches_oracle(merged):
+@pytest.mark.parametrize("merged,gridfast", [(False, False), (True, False), (True, True)])
+def test_tracker2d_sequence_matches_oracle(oracle_mod, merged, gridfast):
     W, H, T = 320, 240, 7
     sc = synth.make_scene(21, W, H, 120, nboxes=3, box_w=24, box_h=60, max_speed=3.0)
     rng = np.random.default_rng(77)
@@ -161,6 +167,12 @@ def test_tracker2d_sequence_matches_oracle(merged):
             ft.push_frame(img)
             ring[-1] = img
             dets, feats = _detections(sc, t, rng, W, H)
+            if gridfast:  # the detections' points from GridFAST on frame t (:734-757)
+                g_in = ft.detect_features([t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in dets], seed=t)
+                feats, tots = oracle_mod.gridfast_detect(img, [_rect_roi(b, W, H) for b in dets], seed=t)
+                for d, f, n in zip(g_in, feats, tots):
+                    np.testing.assert_array_equal(t2d.points(d.features, d.num_features), f, err_msg=f"frame {t}")
+                    assert len(f) == min(int(n), 100)
             r_objs = ORC.backward_tracking(ring, [ORC.Rect(*b) for b in dets], feats)
             g_trk_in = [t2d.make_tracker([b.tuple() for b in tr.boxes], tr.features, tr.duration) for tr in trackers]
             r_cost = ORC.forward_tracking(ring, trackers, r_objs) if trackers else np.zeros((len(r_objs), 0), np.float32)
