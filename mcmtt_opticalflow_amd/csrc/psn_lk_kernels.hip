@@ -1308,6 +1308,38 @@ __device__ __forceinline__ void wave_sum3(int &s1, int &s2, unsigned &a) {
     a = (unsigned)__builtin_amdgcn_readlane((int)a, 63);
 }
 
+// Four simultaneous 64-lane sums (one-wave iterations): s1, s2 and the
+// per-lane sum|t1|, sum|t2|, clamped per lane to 2^25 + 1 first (a clamped lane
+// alone fails the exactness test below; totals stay below 2^31).
+__device__ __forceinline__ void wave_sum4(int &s1, int &s2, unsigned &a1, unsigned &a2) {
+    a1 = min(a1, (1u << 25) + 1u);
+    a2 = min(a2, (1u << 25) + 1u);
+#define PSN_DPP4(ctl, rm)                                                   \
+    s1 += __builtin_amdgcn_update_dpp(0, s1, ctl, rm, 0xf, false);          \
+    s2 += __builtin_amdgcn_update_dpp(0, s2, ctl, rm, 0xf, false);          \
+    a1 += (unsigned)__builtin_amdgcn_update_dpp(0, (int)a1, ctl, rm, 0xf, false); \
+    a2 += (unsigned)__builtin_amdgcn_update_dpp(0, (int)a2, ctl, rm, 0xf, false)
+    PSN_DPP4(0x111, 0xf);
+    PSN_DPP4(0x112, 0xf);
+    PSN_DPP4(0x114, 0xf);
+    PSN_DPP4(0x118, 0xf);
+    PSN_DPP4(0x142, 0xa);
+    PSN_DPP4(0x143, 0xc);
+#undef PSN_DPP4
+    s1 = __builtin_amdgcn_readlane(s1, 63);
+    s2 = __builtin_amdgcn_readlane(s2, 63);
+    a1 = (unsigned)__builtin_amdgcn_readlane((int)a1, 63);
+    a2 = (unsigned)__builtin_amdgcn_readlane((int)a2, 63);
+}
+// Exactness of a float sum of integer terms t in ANY order or chain split:
+// every partial sum is a subset sum, inside [-N, P] (P = sum of the positive
+// terms, N = sum of |negative terms|), so max(P, N) <= 2^24 makes every
+// partial sum an exact float. With A = sum|t| and S = sum t:
+// max(P, N) = (A + |S|) / 2. A <= 2^25 also keeps the int32 S unwrapped.
+__device__ __forceinline__ bool sums_exact(unsigned A, int S) {
+    return A + (unsigned)abs(S) <= (2u << 24);
+}
+
 // Level geometry of the I window (prevPt/2^l - halfWin): top-left, validity and weights.
 struct IGeo {
     int ipx, ipy, w00, w01, w10, w11;
@@ -1762,7 +1794,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 // the lane's window rows, two rows per dword (int16 halves): I, Ix,
                 // Iy, |Ix| + |Iy|; rows past the window carry zero gradients
                 constexpr int E2 = (E + 1) / 2;
-                unsigned IxP[E2], IyP[E2], SxyP[E2];
+                unsigned IxP[E2], IyP[E2], AxP[E2], AyP[E2];
                 int Cw[2 * E2];  // 256 - 512 * I: the bilinear sum plus Cw, >> 9, is J* - I*
                 int Iw_[E];
                 {
@@ -1784,7 +1816,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                         Cw[2 * q + 1] = 256 - 512 * iw[2 * q + 1];
                         IxP[q] = pack_w(ix[2 * q], ix[2 * q + 1]);
                         IyP[q] = pack_w(iy[2 * q], iy[2 * q + 1]);
-                        SxyP[q] = pack_w(abs(ix[2 * q]) + abs(iy[2 * q]), abs(ix[2 * q + 1]) + abs(iy[2 * q + 1]));
+                        AxP[q] = pack_w(abs(ix[2 * q]), abs(ix[2 * q + 1]));
+                        AyP[q] = pack_w(abs(iy[2 * q]), abs(iy[2 * q + 1]));
                     }
                 }
                 LK_STAMP(level * 10 + 2);
@@ -1792,8 +1825,9 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 int jdone = 0;
                 unsigned dP[E2];
                 // diffs J - I of the lane's rows at offset (ox, oy) of the region
-                // (packed pairs into dP) and the lane's s1, s2, sum|t1|+|t2| (clamped)
-                auto products = [&](int ox, int oy, unsigned W0, unsigned W1, int &s1, int &s2, unsigned &a) {
+                // (packed pairs into dP) and the lane's s1, s2, sum|t1|, sum|t2|
+                auto products = [&](int ox, int oy, unsigned W0, unsigned W1, int &s1, int &s2, unsigned &a,
+                                    unsigned &a2) {
                     const uint32_t *jb = JC + __mul24(ox, JRHc) + oy + lane_off;
                     unsigned rr[2 * E2 + 1];
 #pragma unroll
@@ -1801,6 +1835,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                     s1 = 0;
                     s2 = 0;
                     a = 0;
+                    a2 = 0;
 #pragma unroll
                     for (int q = 0; q < E2; q++) {
                         // (sum + 256) >> 9 - I == (sum + 256 - 512 I) >> 9: the diffs directly
@@ -1811,7 +1846,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                         s1 = sdot2(dP[q], IxP[q], s1);
                         s2 = sdot2(dP[q], IyP[q], s2);
                         const s16x2 ad = __builtin_elementwise_max(d, (s16x2)0 - d);
-                        a = udot2(__builtin_bit_cast(unsigned, ad), SxyP[q], a);  // per lane < 2^30
+                        a = udot2(__builtin_bit_cast(unsigned, ad), AxP[q], a);  // per lane < 2^29
+                        a2 = udot2(__builtin_bit_cast(unsigned, ad), AyP[q], a2);
                     }
                 };
                 for (int j = 0; j < maxc; j++) {
@@ -1825,12 +1861,12 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                     // bounds / region tests below decide whether the sums count
                     const int ox = min(max(inx - jr_x0, 0), JRW - w - 1), oy = min(max(iny - jr_y0, 0), JRH - h - 1);
                     int s1, s2;
-                    unsigned a;
-                    products(ox, oy, W0, W1, s1, s2, a);
+                    unsigned a, a2;
+                    products(ox, oy, W0, W1, s1, s2, a, a2);
                     int sinx = __builtin_amdgcn_readfirstlane(inx), siny = __builtin_amdgcn_readfirstlane(iny);
                     // keep the (rarely taken) branches below the products: the
                     // conditions formally depend on them
-                    asm volatile("; order %2 %3 %4" : "+s"(sinx), "+s"(siny) : "v"(s1), "v"(s2), "v"(a));
+                    asm volatile("; order %2 %3 %4 %5" : "+s"(sinx), "+s"(siny) : "v"(s1), "v"(s2), "v"(a), "v"(a2));
                     if (sinx < -w || sinx >= cols || siny < -h || siny >= rows) {
                         if (level == 0) status = 0;
                         break;
@@ -1844,33 +1880,25 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         cp.copy(JC, J, jr_y0, jr_x0, JRW, JRH, wk0_int, wk0_bord);
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                        products(sinx - jr_x0, siny - jr_y0, W0, W1, s1, s2, a);
+                        products(sinx - jr_x0, siny - jr_y0, W0, W1, s1, s2, a, a2);
                         PH_COUNT(5);
                     }
                     PH_MARK(0);
                     const int l1 = s1, l2 = s2;  // the lane's own sums (class path)
-                    wave_sum3(s1, s2, a);
+                    const unsigned la1 = a, la2 = a2;
+                    wave_sum4(s1, s2, a, a2);
                     PH_MARK(1);
                     float b1, b2;
-                    if (a <= (unsigned)kExact) {
-                        // every term and partial sum in any order is an integer <= 2^24
+                    if (sums_exact(a, s1) && sums_exact(a2, s2)) {
+                        // every partial sum in any order is an integer of magnitude <= 2^24
                         b1 = (float)s1;
                         b2 = (float)s2;
                     } else {
                         PH_COUNT(6);
                         // per SSE2 chain class: inclusive scans of the lanes' sums and
                         // of sum|t1|, sum|t2|; class-end lanes publish to LDS
-                        unsigned a1 = 0, a2 = 0;
-#pragma unroll
-                        for (int q = 0; q < E2; q++) {
-                            const s16x2 d = __builtin_bit_cast(s16x2, dP[q]);
-                            const unsigned ad = __builtin_bit_cast(unsigned, __builtin_elementwise_max(d, (s16x2)0 - d));
-                            const s16x2 gx = __builtin_bit_cast(s16x2, IxP[q]), gy = __builtin_bit_cast(s16x2, IyP[q]);
-                            a1 = udot2(ad, __builtin_bit_cast(unsigned, __builtin_elementwise_max(gx, (s16x2)0 - gx)), a1);
-                            a2 = udot2(ad, __builtin_bit_cast(unsigned, __builtin_elementwise_max(gy, (s16x2)0 - gy)), a2);
-                        }
-                        a1 = min(a1, (unsigned)(2 * kExact));  // a class holding a clamped lane fails anyway
-                        a2 = min(a2, (unsigned)(2 * kExact));
+                        unsigned a1 = min(la1, (1u << 25) + 1u);  // a clamped lane fails its class
+                        a2 = min(la2, (1u << 25) + 1u);
                         const int c1 = wave_scan(l1), c2 = wave_scan(l2);
                         a1 = (unsigned)wave_scan((int)a1);
                         a2 = (unsigned)wave_scan((int)a2);
@@ -1883,8 +1911,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                             const int4 cv = CSX[c];  // classes 0-3 stay zero without SSE2 lanes
                             S1[c] = cv.x - pv.x;     // wrapping: exact whenever the class passes
                             S2[c] = cv.y - pv.y;
-                            exact = exact && (unsigned)(cv.z - pv.z) <= (unsigned)kExact &&
-                                    (unsigned)(cv.w - pv.w) <= (unsigned)kExact;
+                            exact = exact && sums_exact((unsigned)(cv.z - pv.z), S1[c]) &&
+                                    sums_exact((unsigned)(cv.w - pv.w), S2[c]);
                             pv = cv;
                         }
                         if (exact) {

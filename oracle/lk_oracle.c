@@ -103,6 +103,15 @@ static void bsum_classify(const long long *t1, const long long *t2, int w, int h
         }
         g_bsum_log[7] += okd;
     }
+    {   /* [8] max(sum of positive terms, sum of |negative terms|) <= 2^24 for b1 and b2:
+         * every subset sum (any order, any chain split) is then an exact integer */
+        long long P1 = 0, N1 = 0, P2 = 0, N2 = 0;
+        for (int i = 0; i < w * h; i++) {
+            if (t1[i] > 0) P1 += t1[i]; else N1 -= t1[i];
+            if (t2[i] > 0) P2 += t2[i]; else N2 -= t2[i];
+        }
+        g_bsum_log[8] += P1 <= E && N1 <= E && P2 <= E && N2 <= E;
+    }
     g_bsum_log[0]++;
     g_bsum_log[1] += (a1 + a2) <= E;
     g_bsum_log[2] += (a1 <= E && a2 <= E);
