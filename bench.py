@@ -14,6 +14,9 @@ One step = one camera-frame of the per-camera hot path on every rank:
 Workload (BASELINE.json configs[1]): 1 camera per GPU, 1920x1080 gray, 512
 points, 4-level pyramid, 21x21 window, default criteria. Inputs are synthetic
 (mcmtt_opticalflow_amd/synth.py) and resident in HBM before timing.
+--cameras C puts C cameras on every GPU (north_star's "4 x 1080p cameras at
+1 GPU" target): their LK queries share ONE launch per frame-set and their
+pyramid builds run on the ingest stream beside it.
 
 Single GPU:  python bench.py --steps 200 --warmup 10
 Multi GPU:   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -106,13 +109,16 @@ def main():
     ap.add_argument("--period", type=int, default=10)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--overlap", choices=["off", "stream", "fused"], default="fused",
+    ap.add_argument("--cameras", type=int, default=1, help="cameras per GPU (default 1 = configs[1])")
+    ap.add_argument("--overlap", choices=["auto", "off", "stream", "fused"], default="auto",
                     help="ingest of frame t+1: serial on the LK stream, on a second stream, or fused "
-                         "into the tail of frame t's LK launch (default)")
+                         "into the tail of frame t's LK launch (auto: fused for 1 camera per GPU, "
+                         "stream for more)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01b_pmc_summary.json"),
                     help="rocprofv3 FETCH/WRITE_SIZE summary (tools/profile_round.sh) for roofline.traffic")
     args = ap.parse_args()
 
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -126,45 +132,56 @@ def main():
     device = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
-    cam = rank
+    C = max(1, args.cameras)
+    cams = [rank * C + k for k in range(C)]
     W, H, N, L, win = args.width, args.height, args.points, args.levels, args.win
-    R = 4  # ring slots, PSN_2D_BACKTRACKING_INTERVAL (PSNWhere_Tracker2D.cpp:16)
+    R = 4  # ring slots per camera, PSN_2D_BACKTRACKING_INTERVAL (PSNWhere_Tracker2D.cpp:16)
 
-    scene = synth.make_scene(cam, W, H, N)
-    frames = render_frames_torch(scene, args.period, device)
+    scenes = [synth.make_scene(c, W, H, N) for c in cams]
+    scene = scenes[0]
+    frames = [render_frames_torch(sc, args.period, device) for sc in scenes]
     # one explicit stream for the library kernels and the torch ops around them
     stream = torch.cuda.Stream(device)
     torch.cuda.set_stream(stream)
-    ctx = lk.LKContext(W, H, ring_slots=R, max_level_cap=L - 1, device=local_rank)
+    # one context holds every local camera's ring: camera k uses slots [k*R, k*R + R)
+    ctx = lk.LKContext(W, H, ring_slots=R * C, max_level_cap=L - 1, device=local_rank)
     ctx.set_stream(stream.cuda_stream)
     # frame t+1's pyramid overlaps frame t's LK (fused: built by the LK launch's
-    # tail workgroups); the frames are resident and complete before timing starts
-    mode = {"off": 0, "stream": 1, "fused": 2}[args.overlap]
+    # tail workgroups; stream: on the ingest stream); the frames are resident and
+    # complete before timing starts
+    overlap = args.overlap if args.overlap != "auto" else ("fused" if C == 1 else "stream")
+    mode = {"off": 0, "stream": 1, "fused": 2}[overlap]
     ctx.set_ingest_overlap(mode)
 
-    sb = pdist.slot_bytes(N)
+    sb = pdist.slot_bytes(N, C)
     slots = [torch.zeros(sb, dtype=torch.uint8, device=device) for _ in range(2)]
-    views = [pdist.slot_views(s, N) for s in slots]
+    views = [pdist.slot_views(s, N, C) for s in slots]
     for hdr, nxt, _, _ in views:
-        hdr.copy_(torch.tensor([cam, 0, N, 0], dtype=torch.int32))
-    views[0][1].copy_(torch.from_numpy(scene.points_at(0)))
+        hdr.copy_(torch.tensor([[c, 0, N, 0] for c in cams], dtype=torch.int32).view(hdr.shape))
+    views[0][1].copy_(torch.from_numpy(np.concatenate([sc.points_at(0) for sc in scenes])))
     gathered = torch.empty((world, sb), dtype=torch.uint8, device=device)
     params = lk.make_params((win, win), L - 1)
-    ctx.push_frame_device(0, frames[0].data_ptr(), W, 1)
-    if mode == 2:
-        ctx.push_frame_device(1, frames[ping_pong(1, args.period)].data_ptr(), W, 1)
+
+    def push(t):  # frame t of every local camera into its ring
+        for k in range(C):
+            ctx.push_frame_device(k * R + t % R, frames[k][ping_pong(t, args.period)].data_ptr(), W, 1)
+
+    push(0)
+    if mode:
+        push(1)
         ctx.sync()
-    queries = [lk.make_query((t - 1) % R, t % R, 0, N, params) for t in range(R)]
+    queries = [[lk.make_query(k * R + (t - 1) % R, k * R + t % R, k * N, N, params) for k in range(C)]
+               for t in range(R)]
 
     def step(t):
         cur, prv = views[t % 2], views[(t - 1) % 2]
-        if mode == 2:  # ingest frame t+1 (deferred into this step's LK launch)
-            ctx.push_frame_device((t + 1) % R, frames[ping_pong(t + 1, args.period)].data_ptr(), W, 1)
+        if mode:  # ingest frame t+1 (overlapping this step's LK launch)
+            push(t + 1)
         else:  # ingest frame t
-            ctx.push_frame_device(t % R, frames[ping_pong(t, args.period)].data_ptr(), W, 1)
-        q = queries[t % R]
-        ctx.track_device([q], prv[1].data_ptr(), cur[1].data_ptr(), cur[3].data_ptr(), cur[2].data_ptr())
-        cur[0][1].fill_(t)
+            push(t)
+        ctx.track_device(queries[t % R], prv[1].data_ptr(), cur[1].data_ptr(), cur[3].data_ptr(),
+                         cur[2].data_ptr())
+        (cur[0][:, 1] if C > 1 else cur[0][1]).fill_(t)
         if world > 1:
             pdist.allgather_slots(slots[t % 2], world, out=gathered)
 
@@ -193,15 +210,15 @@ def main():
     pyr_bytes, lk_bytes = algorithmic_bytes(W, H, L, N)
     pyr_us = 1e3 * ts["push_ms"] / max(ts["n_push"], 1) if ts["n_push"] else None
     lk_us = 1e3 * ts["track_ms"] / max(ts["n_track"], 1)
-    fps_all = world * args.steps / elapsed
-    per_gpu_fps = args.steps / elapsed
+    fps_all = world * C * args.steps / elapsed
+    per_gpu_fps = C * args.steps / elapsed
     frame_bytes = pyr_bytes + lk_bytes
 
     if rank == 0:
-        if mode == 2:  # one launch per frame: LK of frame t + pyramid of frame t+1
-            dom = ("lk_kernel_st+fused_pyramid", lk_bytes + pyr_bytes, lk_us)
+        if mode == 2:  # one launch per frame: LK of frame t + pyramid of frame t+1 (+ C-1 separate builds)
+            dom = ("lk_kernel_st+fused_pyramid", C * lk_bytes + pyr_bytes, lk_us)
         elif pyr_us is None or lk_us >= pyr_us:
-            dom = ("lk_kernel", lk_bytes, lk_us)
+            dom = ("lk_kernel", C * lk_bytes, lk_us)
         else:
             dom = ("pyramid_kernel", pyr_bytes, pyr_us)
         achieved = dom[1] / (dom[2] * 1e-6) / 1e9
@@ -226,11 +243,14 @@ def main():
             "dtype": "u8+f32",
             "data": "synthetic",
             "config": {
-                "workload": "BASELINE.json configs[1]: 1 camera per GPU, 1920x1080 gray, 512 points, "
-                            "4-level pyramid, 21x21 window, per-frame pyramid build + LK + tracklet propagation"
-                            + (", RCCL all-gather of per-camera slots" if world > 1 else ""),
-                "cameras": world, "width": W, "height": H, "points_per_camera": N, "levels": L,
-                "win": [win, win], "parallelism": f"camera-per-GPU x{world}",
+                "workload": (("BASELINE.json configs[1]: 1 camera per GPU" if C == 1 else
+                              f"{C} cameras per GPU (north_star 4-camera target shape)")
+                             + f", {W}x{H} gray, {N} points, {L}-level pyramid, {win}x{win} window, "
+                               "per-frame pyramid build + LK + tracklet propagation"
+                             + (", RCCL all-gather of per-camera slots" if world > 1 else "")),
+                "cameras": world * C, "cameras_per_gpu": C, "width": W, "height": H, "points_per_camera": N,
+                "levels": L, "win": [win, win],
+                "parallelism": f"camera-per-GPU x{world}" if C == 1 else f"{C} cameras-per-GPU x{world}",
             },
             "roofline": {
                 "kernel": dom[0], "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
@@ -240,7 +260,7 @@ def main():
             },
             "kernels_us": {"pyramid_kernel": None if pyr_us is None else round(pyr_us, 3),
                            "lk_kernel": round(lk_us, 3)},
-            "ingest_overlap": args.overlap,
+            "ingest_overlap": overlap,
             "frame_level": {
                 "algorithmic_bytes_per_camera_frame": frame_bytes,
                 "achieved_GBps_per_gpu": round(frame_bytes * per_gpu_fps / 1e9, 2),

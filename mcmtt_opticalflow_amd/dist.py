@@ -7,11 +7,12 @@ the per-camera std::vector<stTrack2DResult> to CPSNWhere_Associator3D::Run
 (rank == camera index) and the only exchange is one all-gather per frame of a
 fixed-size slot per camera, so the gathered rows are ordered by camera index.
 
-Slot layout (bytes, all offsets 4-byte aligned):
-  [0, 16)            int32 header: cam, frame, npts, reserved
-  [16, 16+8N)        float32 next_xy (LK output, written in place by the kernel)
-  [16+8N, 16+12N)    float32 err
-  [16+12N, 16+13N)   uint8 status
+Slot layout of a rank holding C cameras of N points each (M = C*N points;
+bytes, all offsets 4-byte aligned; C = 1 is the one-camera-per-GPU case):
+  [0, 16C)             int32 header per camera: cam, frame, npts, reserved
+  [16C, 16C+8M)        float32 next_xy, camera-major (LK output, written in place)
+  [16C+8M, 16C+12M)    float32 err
+  [16C+12M, 16C+13M)   uint8 status
 padded to a multiple of 64 bytes.
 
 Works with any torch.distributed backend: nccl (= RCCL over xGMI on ROCm) for
@@ -22,19 +23,23 @@ from __future__ import annotations
 HEADER_BYTES = 16
 
 
-def slot_bytes(npts: int) -> int:
-    n = HEADER_BYTES + 13 * npts
+def slot_bytes(npts: int, ncam: int = 1) -> int:
+    """Bytes of one rank's slot: `ncam` cameras of `npts` points each."""
+    n = HEADER_BYTES * ncam + 13 * npts * ncam
     return (n + 63) // 64 * 64
 
 
-def slot_views(slot, npts: int):
-    """(header int32[4], next_xy float32[npts,2], err float32[npts], status uint8[npts]) views of a
-    uint8 torch tensor of slot_bytes(npts) bytes."""
+def slot_views(slot, npts: int, ncam: int = 1):
+    """(header int32[4] (ncam == 1) or [ncam, 4], next_xy float32[M,2], err float32[M],
+    status uint8[M]) views of a uint8 torch tensor of slot_bytes(npts, ncam) bytes, M = ncam*npts."""
     import torch
 
-    assert slot.dtype == torch.uint8 and slot.numel() >= slot_bytes(npts)
-    o = HEADER_BYTES
+    assert slot.dtype == torch.uint8 and slot.numel() >= slot_bytes(npts, ncam)
+    o = HEADER_BYTES * ncam
     header = slot[0:o].view(torch.int32)
+    if ncam > 1:
+        header = header.view(ncam, 4)
+    npts = npts * ncam
     nxt = slot[o:o + 8 * npts].view(torch.float32).view(npts, 2)
     err = slot[o + 8 * npts:o + 12 * npts].view(torch.float32)
     status = slot[o + 12 * npts:o + 13 * npts]
