@@ -13,6 +13,8 @@ import re
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSN_LK_LIB") or os.path.join(_HERE, "lib", "libpsn_lk.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psn_lk.h")
+# every header whose entry points libpsn_lk.so exports
+HEADER_PATHS = [HEADER_PATH, os.path.join(os.path.dirname(_HERE), "include", "psn_sgsmooth.h")]
 
 PSN_LK_OK = 0
 ERRORS = {
@@ -76,8 +78,8 @@ class GridFastParams(ctypes.Structure):
 
 
 def header_functions() -> list[str]:
-    """Names of every function declared in include/psn_lk.h."""
-    src = open(HEADER_PATH).read()
+    """Names of every function declared in include/psn_lk.h and psn_sgsmooth.h."""
+    src = "".join(open(p).read() for p in HEADER_PATHS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(psn_\w+)\s*\(", src)))
 
@@ -123,6 +125,14 @@ def load():
     gfa = [vp, ip, vp, ip, ctypes.POINTER(GridFastParams), ctypes.c_uint32, vp, vp, vp]
     L.psn_gridfast_detect.argtypes = gfa
     L.psn_gridfast_detect_device.argtypes = gfa
+    L.psn_sg_create.argtypes = [ip, ip, ip, ip, ip, ctypes.POINTER(vp)]
+    L.psn_sg_destroy.argtypes = [vp]
+    L.psn_sg_destroy.restype = None
+    L.psn_sg_reset.argtypes = [vp]
+    L.psn_sg_set_stream.argtypes = [vp, vp]
+    L.psn_sg_insert_device.argtypes = [vp, vp, ip, vp, vp, vp]
+    L.psn_sg_insert.argtypes = [vp, vp, ip, vp, vp, vp]
+    L.psn_sg_lengths.argtypes = [vp, vp]
     L.psn_comm_get_unique_id.argtypes = [vp]
     L.psn_comm_init.argtypes = [ip, ip, ip, vp, ctypes.POINTER(vp)]
     L.psn_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]

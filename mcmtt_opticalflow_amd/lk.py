@@ -196,3 +196,48 @@ def calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size=(21, 21), ma
     with LKContext(w, h, ring_slots=1, max_level_cap=min(cap, 5), device=device) as ctx:
         return ctx.calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size, max_level, criteria,
                                             flags, min_eig_threshold, next_pts, want_err)
+
+
+class SGSmoother:
+    """Batched CPSNWhere_SGSmooth (psn_sgsmooth.h): `nseries` trajectories of
+    `dims` coordinates, one Insert per series per call, on the device."""
+
+    def __init__(self, nseries: int, dims: int = 2, span: int = 9, degree: int = 1, device: int = 0):
+        self._L = _lib.load()
+        self.nseries, self.dims, self.span = nseries, dims, span
+        h = ctypes.c_void_p()
+        rc = self._L.psn_sg_create(device, nseries, dims, span, degree, ctypes.byref(h))
+        if rc != 0:
+            raise PsnLkError(rc, "psn_sg_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psn_sg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def insert(self, values: np.ndarray, active: np.ndarray | None = None):
+        """values (nseries, >= dims) f32. Returns (refresh (n,) int32, out (n, span, dims) f64):
+        row k of series i = smoothed position refresh[i] + k (rows < length - refresh valid)."""
+        v = np.ascontiguousarray(values, dtype=np.float32).reshape(self.nseries, -1)
+        act = None if active is None else np.ascontiguousarray(active, dtype=np.uint8)
+        ref = np.zeros(self.nseries, np.int32)
+        out = np.zeros((self.nseries, self.span, self.dims), np.float64)
+        rc = self._L.psn_sg_insert(self._h, v.ctypes.data, v.shape[1], act.ctypes.data if act is not None else None,
+                                   ref.ctypes.data, out.ctypes.data)
+        if rc != 0:
+            raise PsnLkError(rc, "psn_sg_insert")
+        return ref, out
+
+    def lengths(self) -> np.ndarray:
+        n = np.zeros(self.nseries, np.int32)
+        rc = self._L.psn_sg_lengths(self._h, n.ctypes.data)
+        if rc != 0:
+            raise PsnLkError(rc, "psn_sg_lengths")
+        return n
