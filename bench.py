@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cameras", type=int, default=1, help="cameras per GPU (default 1 = configs[1])")
+    ap.add_argument("--sg", action="store_true",
+                    help="SG(9, 1) post-filter of every tracked point's trajectory after the LK (configs[4])")
     ap.add_argument("--overlap", choices=["auto", "off", "stream", "fused"], default="auto",
                     help="ingest of frame t+1: serial on the LK stream, on a second stream, or fused "
                          "into the tail of frame t's LK launch (auto: fused for 1 camera per GPU, "
@@ -173,6 +175,13 @@ def main():
     queries = [[lk.make_query(k * R + (t - 1) % R, k * R + t % R, k * N, N, params) for k in range(C)]
                for t in range(R)]
 
+    sg = None
+    if args.sg:  # trajectory post-filter: one SGSmooth Insert per point and frame, same stream
+        sg = lk.SGSmoother(C * N, 2, 9, 1, device=local_rank)
+        sg.set_stream(stream.cuda_stream)
+        sg_ref = torch.empty(C * N, dtype=torch.int32, device=device)
+        sg_out = torch.empty((C * N, 9, 2), dtype=torch.float64, device=device)
+
     def step(t):
         cur, prv = views[t % 2], views[(t - 1) % 2]
         if mode:  # ingest frame t+1 (overlapping this step's LK launch)
@@ -181,6 +190,8 @@ def main():
             push(t)
         ctx.track_device(queries[t % R], prv[1].data_ptr(), cur[1].data_ptr(), cur[3].data_ptr(),
                          cur[2].data_ptr())
+        if sg is not None:  # status as the active mask: lost points are not inserted
+            sg.insert_device(cur[1].data_ptr(), 2, cur[3].data_ptr(), sg_ref.data_ptr(), sg_out.data_ptr())
         (cur[0][:, 1] if C > 1 else cur[0][1]).fill_(t)
         if world > 1:
             pdist.allgather_slots(slots[t % 2], world, out=gathered)
@@ -261,6 +272,7 @@ def main():
             "kernels_us": {"pyramid_kernel": None if pyr_us is None else round(pyr_us, 3),
                            "lk_kernel": round(lk_us, 3)},
             "ingest_overlap": overlap,
+            "sg_post_filter": bool(args.sg),
             "frame_level": {
                 "algorithmic_bytes_per_camera_frame": frame_bytes,
                 "achieved_GBps_per_gpu": round(frame_bytes * per_gpu_fps / 1e9, 2),
@@ -273,6 +285,8 @@ def main():
             out["cpu_baseline"] = cpu_baseline(scene, args.period, N, (win, win), L - 1, args.cpu_budget, 2000)
             out["speedup_vs_cpu"] = round(fps_all / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
+    if sg is not None:
+        sg.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

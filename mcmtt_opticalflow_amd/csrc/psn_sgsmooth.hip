@@ -83,6 +83,8 @@ void calculate_q(int w, int degree, std::vector<double> &qb, std::vector<double>
     }
 }
 
+constexpr int kSgFastSpan = 16;  // windows up to this size run from registers
+
 __global__ __launch_bounds__(256) void sg_insert_kernel(SgArgs A) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A.nseries) return;
@@ -92,21 +94,46 @@ __global__ __launch_bounds__(256) void sg_insert_kernel(SgArgs A) {
     }
     const int S = A.span, D = A.dims, N = A.nseries;
     int L = A.len[i];
-    double *h = A.hist + i;
+    double *__restrict__ h = A.hist + i;
+    double *__restrict__ o = A.out + (size_t)i * S * D;
     auto at = [&](int pos, int d) -> double { return h[((size_t)(pos % S) * D + d) * N]; };
     for (int d = 0; d < D; d++) h[((size_t)(L % S) * D + d) * N] = (double)A.in[(size_t)i * A.in_stride + d];
     L++;
     A.len[i] = L;
-    double *o = A.out + (size_t)i * S * D;
     int w = min(S, L);
     w -= (w + 1) % 2;
     if (w <= A.degree) {  // bypass: the raw value
         A.refresh[i] = L - 1;
-        for (int d = 0; d < D; d++) o[d] = at(L - 1, d);
+        for (int d = 0; d < D; d++) o[d] = (double)A.in[(size_t)i * A.in_stride + d];
         return;
     }
     const int hf = (w - 1) / 2;
     const double *qb = A.q + A.qoff[w], *qm = qb + hf * w, *qe = qm + w;
+    if (A.qrows[i] == w && w <= kSgFastSpan) {
+        // steady state: position L-1-hf by the filter and the last hf rows, from
+        // the last w samples held in registers (x[j] = sample L-1-j; static
+        // indices, every load in flight at once)
+        A.refresh[i] = L - 1 - hf;
+        for (int d = 0; d < D; d++) {
+            double x[kSgFastSpan];
+#pragma unroll
+            for (int j = 0; j < kSgFastSpan; j++) x[j] = j < w ? at(L - 1 - j, d) : 0.0;
+            double acc = 0.0;
+#pragma unroll
+            for (int c = 0; c < kSgFastSpan; c++)  // Filter: newest sample first
+                if (c < w) acc += qm[c] * x[c];
+            o[d] = acc;
+            for (int p = 0; p < hf; p++) {  // end rows: samples L-w .. L-1 in order
+                const double *qr = qe + p * w + w - 1;
+                double e = 0.0;
+#pragma unroll
+                for (int j = kSgFastSpan - 1; j >= 0; j--)
+                    if (j < w) e += qr[-j] * x[j];
+                o[(1 + p) * D + d] = e;
+            }
+        }
+        return;
+    }
     int k = 0;  // output row
     int mid0, mid1;  // smoothed positions of the moving filter [mid0, mid1)
     if (A.qrows[i] != w) {  // entire update (L <= span: every value is in the ring)

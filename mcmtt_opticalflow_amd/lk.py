@@ -235,6 +235,16 @@ class SGSmoother:
             raise PsnLkError(rc, "psn_sg_insert")
         return ref, out
 
+    def set_stream(self, stream_ptr: int | None):
+        rc = self._L.psn_sg_set_stream(self._h, stream_ptr)
+        if rc != 0:
+            raise PsnLkError(rc, "psn_sg_set_stream")
+
+    def insert_device(self, d_in: int, in_stride: int, d_active: int | None, d_refresh: int, d_out: int):
+        rc = self._L.psn_sg_insert_device(self._h, d_in, in_stride, d_active, d_refresh, d_out)
+        if rc != 0:
+            raise PsnLkError(rc, "psn_sg_insert_device")
+
     def lengths(self) -> np.ndarray:
         n = np.zeros(self.nseries, np.int32)
         rc = self._L.psn_sg_lengths(self._h, n.ctypes.data)
