@@ -117,6 +117,53 @@ int psn_t2d_forward(psn_t2d *t, psn_t2d_tracker *trk, int ntrk, const psn_t2d_de
 int psn_t2d_track_frame(psn_t2d *t, psn_t2d_detection *dets, int ndet, psn_t2d_tracker *trk, int ntrk,
                         float *cost);
 
+/* ---- stTrack2DResult: the Tracker2D -> Associator3D hand-off ----
+ * stObject2DInfo (PSNWhere_Types.h:190-198) and stTrack2DResult (:200-209)
+ * as plain C records with caller-owned arrays (cap_* = capacity, used by the
+ * readers; matMatchingCost is not part of either format). */
+typedef struct psn_object2d {
+    unsigned id;
+    psn_rect box, head;
+    double score;
+    int num_prev;                                   /* featurePointsPrev */
+    float prev[PSN_T2D_MAX_FEATURES][2];
+    int num_curr;                                   /* featurePointsCurr */
+    float curr[PSN_T2D_MAX_FEATURES][2];
+} psn_object2d;
+
+typedef struct psn_track2d_result {
+    unsigned cam_id, frame_idx;
+    int num_objects, cap_objects;
+    psn_object2d *objects;
+    int num_detection_rects, cap_detection_rects;
+    psn_rect *detection_rects;
+    int num_tracker_rects, cap_tracker_rects;
+    psn_rect *tracker_rects;
+} psn_track2d_result;
+
+/* CPSNWhere_Tracker2D::FilePrintResult (PSNWhere_Tracker2D.cpp:1268-1334):
+ * writes <dir>/track2D_result_cam%d_frame%04d.txt in the reference's text
+ * format ("%f" fields; dir must end with a separator, as RESULT_SAVE_PATH
+ * "tracklets/" does). Returns 0 or PSN_LK_ERR_ARG (cannot open). */
+int psn_t2d_write_result_txt(const char *dir, const psn_track2d_result *r);
+/* psn::Read2DTrackResultWithTxt (PSNWhere_Utils.cpp:1148-1237): parses that
+ * file (values pass through float, as the reference's fscanf "%f" does).
+ * Returns 0, PSN_LK_ERR_ARG (cannot open / malformed) or PSN_T2D_ERR_CAPACITY. */
+int psn_t2d_read_result_txt(const char *dir, unsigned cam_id, unsigned frame_idx, psn_track2d_result *r);
+
+/* Fixed-size binary slot of one camera's result for the per-frame RCCL
+ * all-gather into Associator3D (psn_comm_allgather, psn_lk.h): exact (no
+ * text rounding), little-endian, self-describing:
+ *   u32 magic 'PT2R', u32 version 1, u32 cam_id, u32 frame_idx,
+ *   u32 nobj, u32 ndet, u32 ntrk, u32 bytes_used,
+ *   nobj x {u32 id, u32 num_prev, u32 num_curr, u32 pad, f64 box[4], f64 head[4],
+ *           f64 score, f32 prev[num_prev][2], f32 curr[num_curr][2]} (8-B aligned),
+ *   ndet x f64[4], ntrk x f64[4].
+ * psn_t2d_result_slot_bytes(max objects, max rects) sizes a slot. */
+size_t psn_t2d_result_slot_bytes(int max_objects, int max_rects);
+int psn_t2d_pack_result(const psn_track2d_result *r, void *slot, size_t slot_bytes);
+int psn_t2d_unpack_result(const void *slot, size_t slot_bytes, psn_track2d_result *r);
+
 #ifdef __cplusplus
 }
 #endif

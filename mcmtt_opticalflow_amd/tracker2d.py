@@ -73,6 +73,21 @@ class Tracker(ctypes.Structure):
     ]
 
 
+class Object2D(ctypes.Structure):  # psn_object2d (stObject2DInfo)
+    _fields_ = [("id", ctypes.c_uint), ("box", Rect), ("head", Rect), ("score", ctypes.c_double),
+                ("num_prev", ctypes.c_int), ("prev", (ctypes.c_float * 2) * MAX_FEATURES),
+                ("num_curr", ctypes.c_int), ("curr", (ctypes.c_float * 2) * MAX_FEATURES)]
+
+
+class Track2DResult(ctypes.Structure):  # psn_track2d_result (stTrack2DResult)
+    _fields_ = [("cam_id", ctypes.c_uint), ("frame_idx", ctypes.c_uint),
+                ("num_objects", ctypes.c_int), ("cap_objects", ctypes.c_int), ("objects", ctypes.POINTER(Object2D)),
+                ("num_detection_rects", ctypes.c_int), ("cap_detection_rects", ctypes.c_int),
+                ("detection_rects", ctypes.POINTER(Rect)),
+                ("num_tracker_rects", ctypes.c_int), ("cap_tracker_rects", ctypes.c_int),
+                ("tracker_rects", ctypes.POINTER(Rect))]
+
+
 def header_functions() -> list[str]:
     src = open(HEADER_PATH).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
@@ -109,6 +124,12 @@ def load():
     L.psn_t2d_last_error.restype = ctypes.c_char_p
     L.psn_t2d_push_frame.argtypes = [vp, vp, ip, ip]
     L.psn_t2d_rotate.argtypes = [vp]
+    L.psn_t2d_write_result_txt.argtypes = [ctypes.c_char_p, ctypes.POINTER(Track2DResult)]
+    L.psn_t2d_read_result_txt.argtypes = [ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(Track2DResult)]
+    L.psn_t2d_result_slot_bytes.argtypes = [ip, ip]
+    L.psn_t2d_result_slot_bytes.restype = ctypes.c_size_t
+    L.psn_t2d_pack_result.argtypes = [ctypes.POINTER(Track2DResult), vp, ctypes.c_size_t]
+    L.psn_t2d_unpack_result.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(Track2DResult)]
     L.psn_t2d_detect_features.argtypes = [vp, ctypes.POINTER(Detection), ip, ctypes.c_uint32]
     L.psn_t2d_backward.argtypes = [vp, ctypes.POINTER(Detection), ip]
     L.psn_t2d_forward.argtypes = [vp, ctypes.POINTER(Tracker), ip, ctypes.POINTER(Detection), ip, fp]
@@ -226,3 +247,85 @@ class FlowTracker:
         dets_out = list(da)[:len(dets)]
         nvalid = sum(1 for d in dets_out if d.valid)
         return dets_out, list(ta)[:len(trackers)], cost[:nvalid * len(trackers)].reshape(nvalid, len(trackers))
+
+
+# ---- stTrack2DResult formats (tracker2d_io.cpp) ----
+
+class ResultBuffers:
+    """A Track2DResult with caller-owned arrays (capacities for the readers)."""
+
+    def __init__(self, cap_objects=64, cap_rects=64):
+        self.objs = (Object2D * max(cap_objects, 1))()
+        self.dets = (Rect * max(cap_rects, 1))()
+        self.trks = (Rect * max(cap_rects, 1))()
+        self.r = Track2DResult()
+        self.r.objects = ctypes.cast(self.objs, ctypes.POINTER(Object2D))
+        self.r.detection_rects = ctypes.cast(self.dets, ctypes.POINTER(Rect))
+        self.r.tracker_rects = ctypes.cast(self.trks, ctypes.POINTER(Rect))
+        self.r.cap_objects, self.r.cap_detection_rects, self.r.cap_tracker_rects = cap_objects, cap_rects, cap_rects
+
+    @classmethod
+    def from_dict(cls, d):
+        b = cls(max(len(d["objects"]), 1), max(len(d["detection_rects"]), len(d["tracker_rects"]), 1))
+        b.r.cam_id, b.r.frame_idx = d["cam_id"], d["frame_idx"]
+        for i, o in enumerate(d["objects"]):
+            ob = b.objs[i]
+            ob.id = o["id"]
+            ob.box, ob.head, ob.score = rect(*o["box"]), rect(*o["head"]), float(o["score"])
+            for key, nk in (("prev", "num_prev"), ("curr", "num_curr")):
+                pts = np.asarray(o[key], np.float32).reshape(-1, 2)
+                setattr(ob, nk, len(pts))
+                arr = getattr(ob, key)
+                for k, (x, y) in enumerate(pts):
+                    arr[k][0], arr[k][1] = x, y
+        b.r.num_objects = len(d["objects"])
+        for i, t in enumerate(d["detection_rects"]):
+            b.dets[i] = rect(*t)
+        for i, t in enumerate(d["tracker_rects"]):
+            b.trks[i] = rect(*t)
+        b.r.num_detection_rects, b.r.num_tracker_rects = len(d["detection_rects"]), len(d["tracker_rects"])
+        return b
+
+    def to_dict(self):
+        r = self.r
+        objs = []
+        for i in range(r.num_objects):
+            o = self.objs[i]
+            objs.append({"id": o.id, "box": o.box.tuple(), "head": o.head.tuple(), "score": o.score,
+                         "prev": points(o.prev, o.num_prev), "curr": points(o.curr, o.num_curr)})
+        return {"cam_id": r.cam_id, "frame_idx": r.frame_idx, "objects": objs,
+                "detection_rects": [self.dets[i].tuple() for i in range(r.num_detection_rects)],
+                "tracker_rects": [self.trks[i].tuple() for i in range(r.num_tracker_rects)]}
+
+
+def write_result_txt(dirpath: str, result: dict):
+    rc = load().psn_t2d_write_result_txt(dirpath.encode(), ctypes.byref(ResultBuffers.from_dict(result).r))
+    if rc:
+        raise T2dError(rc, "psn_t2d_write_result_txt")
+
+
+def read_result_txt(dirpath: str, cam_id: int, frame_idx: int, cap_objects=64, cap_rects=64) -> dict:
+    b = ResultBuffers(cap_objects, cap_rects)
+    rc = load().psn_t2d_read_result_txt(dirpath.encode(), cam_id, frame_idx, ctypes.byref(b.r))
+    if rc:
+        raise T2dError(rc, "psn_t2d_read_result_txt")
+    return b.to_dict()
+
+
+def result_slot_bytes(max_objects: int, max_rects: int) -> int:
+    return load().psn_t2d_result_slot_bytes(max_objects, max_rects)
+
+
+def pack_result(result: dict, slot: np.ndarray):
+    rc = load().psn_t2d_pack_result(ctypes.byref(ResultBuffers.from_dict(result).r), slot.ctypes.data, slot.nbytes)
+    if rc:
+        raise T2dError(rc, "psn_t2d_pack_result")
+
+
+def unpack_result(slot: np.ndarray, cap_objects=64, cap_rects=64) -> dict:
+    b = ResultBuffers(cap_objects, cap_rects)
+    s = np.ascontiguousarray(slot, np.uint8)
+    rc = load().psn_t2d_unpack_result(s.ctypes.data, s.nbytes, ctypes.byref(b.r))
+    if rc:
+        raise T2dError(rc, "psn_t2d_unpack_result")
+    return b.to_dict()

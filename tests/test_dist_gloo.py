@@ -75,3 +75,66 @@ def test_slot_layout_alignment():
         slot = torch.zeros(b, dtype=torch.uint8)
         hdr, nxt, err, st = pdist.slot_views(slot, n)
         assert nxt.shape == (n, 2) and err.shape == (n,) and st.shape == (n,)
+
+
+def test_slot_layout_multi_camera():
+    from mcmtt_opticalflow_amd import dist as pdist
+
+    n, c = 100, 4
+    b = pdist.slot_bytes(n, c)
+    assert b % 64 == 0 and b >= 16 * c + 13 * n * c
+    slot = torch.zeros(b, dtype=torch.uint8)
+    hdr, nxt, err, st = pdist.slot_views(slot, n, c)
+    assert hdr.shape == (c, 4) and nxt.shape == (c * n, 2) and err.shape == (c * n,) and st.shape == (c * n,)
+    assert pdist.slot_bytes(n, 1) == pdist.slot_bytes(n)
+
+
+def _result_worker(rank, world, port, q):
+    """Each rank packs its camera's stTrack2DResult (psn_t2d_pack_result) and
+    the slots are all-gathered: row r unpacks to camera r's result, exactly."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mcmtt_opticalflow_amd import tracker2d as t2d
+
+        rng = np.random.default_rng(100 + rank)
+        objs = [{"id": 10 * rank + k, "box": (1.5 * k, 2.0, 64.0, 160.0), "head": (0.0, 0.0, 0.0, 0.0),
+                 "score": 0.25 * k, "prev": rng.uniform(0, 999, (k * 7, 2)).astype(np.float32),
+                 "curr": rng.uniform(0, 999, (k * 5, 2)).astype(np.float32)} for k in range(rank + 2)]
+        res = {"cam_id": rank, "frame_idx": 42, "objects": objs, "detection_rects": [(1.0, 2.0, 3.0, 4.0)] * rank,
+               "tracker_rects": [(5.0, 6.0, 7.0, 8.0)]}
+        nb = t2d.result_slot_bytes(8, 8)
+        buf = np.zeros(nb, np.uint8)
+        t2d.pack_result(res, buf)
+        gathered = torch.empty((world, nb), dtype=torch.uint8)
+        dist.all_gather_into_tensor(gathered.view(-1), torch.from_numpy(buf))
+        rows = [t2d.unpack_result(gathered[r].numpy()) for r in range(world)]
+        q.put((rank, res, rows))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_result_slots_allgather_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_result_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sent = {rank: res for rank, res, _ in out}
+    for _, _, rows in out:
+        for cam, g in enumerate(rows):
+            r = sent[cam]
+            assert g["cam_id"] == cam and g["frame_idx"] == 42
+            assert len(g["objects"]) == len(r["objects"])
+            for a, b in zip(g["objects"], r["objects"]):
+                assert (a["id"], a["box"], a["score"]) == (b["id"], b["box"], b["score"])
+                np.testing.assert_array_equal(a["prev"], b["prev"])
+                np.testing.assert_array_equal(a["curr"], b["curr"])
+            assert g["detection_rects"] == r["detection_rects"] and g["tracker_rects"] == r["tracker_rects"]
