@@ -136,6 +136,14 @@ int psn_lk_track(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const float *pr
 int psn_lk_track_device(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const float *d_prev_xy,
                         float *d_next_xy, uint8_t *d_status, float *d_err);
 
+/* The same with per-query point counts that live on the device (e.g. written
+ * by a previous kernel on the context stream): query i processes points
+ * [first_pt, first_pt + d_counts[i]) with d_counts[i] <= num_pts (num_pts =
+ * the capacity the launch is sized for); outputs past the count are not
+ * written. Used by the device-side backward chain (psn_t2d_*). */
+int psn_lk_track_device_counted(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const int *d_counts,
+                                const float *d_prev_xy, float *d_next_xy, uint8_t *d_status, float *d_err);
+
 /* One-shot cv::calcOpticalFlowPyrLK(prevImg, nextImg, prevPts, nextPts, status,
  * err, winSize, maxLevel, criteria, flags, minEigThreshold) on two host gray
  * images of the context's size, using two scratch slots of the context. */

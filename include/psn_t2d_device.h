@@ -1,0 +1,58 @@
+/*
+ * include/psn_t2d_device.h -- device-side step of the Tracker2D backward
+ * chain (part of libpsn_lk.so; driven by libpsn_tracker2d.so).
+ *
+ * CPSNWhere_Tracker2D::Track2D_BackwardFeatureTracking (PSNWhere_Tracker2D.cpp:
+ * 763-811) runs, per detection, up to 3 chained LK calls; after each one
+ * LocalSearchKLT (:452-554) shifts the box by the mode of the flow vectors and
+ * keeps the inliers, which feed the next LK call. Here that step runs on the
+ * device for every detection at once, right after the (counted) LK launch of
+ * the chain step, so the 3 steps of a frame need no host round trip:
+ * psn_lk_track_device_counted reads the per-detection counts this kernel
+ * writes. Arithmetic is the reference's (cv::Point2f differences in float,
+ * PSN_Point2D / PSN_Rect in IEEE double, correctly rounded sqrt).
+ */
+#ifndef PSN_T2D_DEVICE_H
+#define PSN_T2D_DEVICE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSN_T2D_CHAIN_CAP 100  /* PSN_2D_FEATURE_MAX_NUM_TRACK */
+#define PSN_T2D_CHAIN_STEPS 4  /* PSN_2D_BACKTRACKING_INTERVAL: boxes / point sets per detection */
+
+/* Device buffers of the chains of one frame (all device pointers):
+ *   boxes    [ndet][4]       detection box (x, y, w, h) LocalSearchKLT searches around
+ *   cur      [ndet][cap][2]  input points of this step (the LK prevPts)
+ *   nxt      [ndet][cap][2]  the LK nextPts of this step (every point, status ignored: :787)
+ *   cnt      [ndet]          in: points of this step (0 = chain stopped);
+ *                            out: inliers kept, 0 when fewer than 4 (:788)
+ *   next_in  [ndet][cap][2]  out: the inliers' nextPts = the next step's input
+ *   out_boxes[ndet][steps][4] out: box pushed at step s in row s (row 0 = the host's detection box)
+ *   sets     [ndet][steps][cap][2], set_cnt [ndet][steps]
+ *                            out: vecvecTrackedFeatures; step 1 writes row 0 (inliers at t)
+ *                            and row 1, step s row s
+ *   nsteps   [ndet]          out: last step that kept >= 4 inliers */
+typedef struct psn_t2d_chain_dev {
+    int ndet, cap;
+    const double *boxes;
+    const float *cur, *nxt;
+    int *cnt;
+    float *next_in;
+    double *out_boxes;
+    float *sets;
+    int *set_cnt;
+    int *nsteps;
+} psn_t2d_chain_dev;
+
+/* LocalSearchKLT + inlier compaction of chain step `step` (1..3) for every
+ * detection, asynchronous on `hip_stream`. Returns 0 or a PSN_LK_ERR_* code. */
+int psn_t2d_chain_step_device(const psn_t2d_chain_dev *c, int step, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSN_T2D_DEVICE_H */

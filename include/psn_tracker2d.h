@@ -65,6 +65,11 @@ typedef struct psn_t2d psn_t2d;
 int psn_t2d_create(int device, unsigned cam_id, int width, int height, psn_t2d **out);
 void psn_t2d_destroy(psn_t2d *t);
 const char *psn_t2d_last_error(psn_t2d *t);
+/* Where the backward chain's LocalSearchKLT steps run: 1 (default) on the
+ * device -- every chain step's LK launch and LocalSearchKLT kernel enqueued
+ * back to back, one host sync per frame -- or 0 on the host between launches
+ * (env PSN_T2D_HOST_CHAIN=1 selects 0 at create). Results are identical. */
+int psn_t2d_set_device_chain(psn_t2d *t, int on);
 /* ingest frame t into the ring's newest slot (cvtColor + resize, :256-263) */
 int psn_t2d_push_frame(psn_t2d *t, const uint8_t *frame, int stride, int channels);
 /* end of Run: the oldest slot becomes the next frame's slot (:310-316) */

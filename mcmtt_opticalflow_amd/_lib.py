@@ -14,7 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSN_LK_LIB") or os.path.join(_HERE, "lib", "libpsn_lk.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psn_lk.h")
 # every header whose entry points libpsn_lk.so exports
-HEADER_PATHS = [HEADER_PATH, os.path.join(os.path.dirname(_HERE), "include", "psn_sgsmooth.h")]
+HEADER_PATHS = [HEADER_PATH] + [os.path.join(os.path.dirname(_HERE), "include", h)
+                                for h in ("psn_sgsmooth.h", "psn_t2d_device.h")]
 
 PSN_LK_OK = 0
 ERRORS = {
@@ -112,6 +113,7 @@ def load():
     L.psn_lk_push_frame_device.argtypes = [vp, ip, vp, ip, ip]
     L.psn_lk_track.argtypes = [vp, ctypes.POINTER(LkQuery), ip, fp, fp, u8p, fp]
     L.psn_lk_track_device.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp]
+    L.psn_lk_track_device_counted.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp, vp]
     L.psn_calc_optical_flow_pyr_lk.argtypes = [vp, u8p, u8p, ip, fp, fp, u8p, fp, ip, ctypes.POINTER(LkParams)]
     L.psn_lk_read_level.argtypes = [vp, ip, ip, u8p, ip]
     L.psn_lk_level_size.argtypes = [vp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]

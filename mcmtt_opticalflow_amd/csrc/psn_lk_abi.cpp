@@ -480,7 +480,11 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
 }
 
 static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
-                             uint8_t *d_status, float *d_err, bool allow_scratch) {
+                             uint8_t *d_status, float *d_err, bool allow_scratch, const int *d_counts = nullptr) {
+    if (d_counts && c->pend) {  // early-exit workgroups cannot take part in a fused build
+        int rc = flush_pending(c);
+        if (rc) return rc;
+    }
     // slots built on the ingest stream must be complete before the LK reads them;
     // a deferred build of a slot this call reads runs first, as its own launch
     for (int i = 0; i < nq; i++)
@@ -505,6 +509,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         a.status = d_status;
         a.err = d_err;
         a.stamps = c->d_stamps;
+        a.counts = d_counts;
         int wgs = 0, lds = 0, maxpx = 0, nqd = 0, rows_ow = 0, lds_ow = 0;
         bool all_single = true;
         for (int i = 0; i < n; i++) {
@@ -518,6 +523,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             bool single = false;
             int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch, orows, olds);
             if (rc) return rc;
+            a.q[nqd].qidx = base + i;
             all_single &= single;
             rows_ow = std::max(rows_ow, orows);
             lds_ow = std::max(lds_ow, olds);
@@ -598,6 +604,13 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                     c->free_rec[sl] = 1;
                 }
     return PSN_LK_OK;
+}
+
+int psn_lk_track_device_counted(psn_lk_ctx *c, const psn_lk_query *q, int nq, const int *d_counts,
+                                const float *d_prev, float *d_next, uint8_t *d_status, float *d_err) {
+    if (!c || !d_counts || (nq > 0 && (!q || !d_prev || !d_next || !d_status)) || nq < 0) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    return track_device_impl(c, q, nq, d_prev, d_next, d_status, d_err, false, d_counts);
 }
 
 int psn_lk_track_device(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,

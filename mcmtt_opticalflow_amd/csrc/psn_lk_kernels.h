@@ -45,7 +45,8 @@ struct LkQueryDev {
     // division magics (q = n * dv >> 22, exact for n, d < 1024) of the per-query
     // divisors the single-tile kernel needs, and its one-wave lane geometry
     unsigned dv_w, dv_dw, dv_pm, dv_jrw, dv_jrw4, dv_g, dv_cw;
-    int ow_g, ow_rg, pad2_;
+    int ow_g, ow_rg;
+    int qidx;             // the caller's query index (LkLaunchArgs::counts)
 };
 __host__ __device__ inline unsigned div_magic(int d) { return d > 0 ? ((1u << 22) + (unsigned)d - 1u) / (unsigned)d : 0u; }
 
@@ -68,6 +69,10 @@ struct LkLaunchArgs {
     unsigned long long *stamps;  // diagnostic build only (PSN_LK_STAMPS): [wg][64] s_memtime
     int nq;
     int pad_;
+    // optional per-query point counts on the device (<= num_pts, the grid
+    // capacity): workgroups past a query's count exit at once (device-side
+    // chains whose counts come from a previous kernel)
+    const int *counts;
     LkQueryDev q[kMaxQueries];
     // Deferred pyramid build fused into this launch (single-tile kernel only):
     // workgroups that finish their point pull top-level tiles of `pyr` from

@@ -520,6 +520,7 @@ __global__ __launch_bounds__(NT) void lk_kernel(LkLaunchArgs A) {
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
     const LkQueryDev &Q = A.q[qi];
+    if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) return;  // past the query's device count
     const int pi = Q.pt_begin + (g - Q.wg_begin);
     const int w = Q.win_w, h = Q.win_h;
     const int TR = Q.tile_rows;
@@ -1402,6 +1403,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
     const LkQueryDev &Q = A.q[qi];
+    if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) return;  // past the query's device count
     const int pi = Q.pt_begin + (g - Q.wg_begin);
     const int w = Q.win_w, h = Q.win_h, wh = w * h;
     const int maxL = Q.max_level, nlev = maxL + 1;

@@ -172,6 +172,12 @@ void psn_t2d_destroy(psn_t2d *t) { delete t; }
 
 const char *psn_t2d_last_error(psn_t2d *t) { return t ? t->err.c_str() : "null context"; }
 
+int psn_t2d_set_device_chain(psn_t2d *t, int on) {
+    if (!t) return PSN_LK_ERR_ARG;
+    t->flow.SetDeviceChain(on != 0);
+    return 0;
+}
+
 int psn_t2d_push_frame(psn_t2d *t, const uint8_t *frame, int stride, int channels) {
     if (!t) return PSN_LK_ERR_ARG;
     return set(t, t->flow.PushFrame(frame, stride, channels));

@@ -2,9 +2,14 @@
 // psn_where/PSNWhere_Tracker2D.cpp unless noted.
 #include "tracker2d_flow.hpp"
 
+#include <hip/hip_runtime_api.h>
+
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
+
+#include "psn_t2d_device.h"
 
 namespace psn {
 
@@ -95,6 +100,7 @@ int Tracker2DFlow::fail(int rc, const char *what) {
 
 int Tracker2DFlow::Initialize(unsigned camID, int width, int height, int device) {
     Finalize();
+    if (const char *e = std::getenv("PSN_T2D_HOST_CHAIN")) device_chain_ = std::atoi(e) == 0;
     camID_ = camID;
     width_ = width;
     height_ = height;
@@ -112,9 +118,231 @@ int Tracker2DFlow::Initialize(unsigned camID, int width, int height, int device)
     return PSN_LK_OK;
 }
 
+// Device and pinned-host buffers of the device-side chain (grown on demand).
+struct Tracker2DFlow::DeviceBuffers {
+    size_t nchains = 0, nfwd_pts = 0, nfwd_jobs = 0;
+    float *d_in = nullptr, *d_out = nullptr, *d_buf[2] = {nullptr, nullptr}, *d_err = nullptr;
+    uint8_t *d_status = nullptr;
+    double *d_boxes = nullptr, *d_obox = nullptr;
+    float *d_sets = nullptr;
+    int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr;
+    // pinned staging: inputs, then results
+    float *h_in = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
+    uint8_t *h_fwd_st = nullptr;
+    double *h_boxes = nullptr, *h_obox = nullptr;
+    int *h_cnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr;
+    void release() {
+        for (void *p : {(void *)d_in, (void *)d_out, (void *)d_buf[0], (void *)d_buf[1], (void *)d_err, (void *)d_status,
+                        (void *)d_boxes, (void *)d_obox, (void *)d_sets, (void *)d_cnt, (void *)d_setcnt,
+                        (void *)d_nsteps})
+            if (p) (void)hipFree(p);
+        for (void *p : {(void *)h_in, (void *)h_fwd_out, (void *)h_sets, (void *)h_fwd_st, (void *)h_boxes,
+                        (void *)h_obox, (void *)h_cnt, (void *)h_setcnt, (void *)h_nsteps})
+            if (p) (void)hipHostFree(p);
+        *this = DeviceBuffers();
+    }
+};
+
 void Tracker2DFlow::Finalize() {
+    if (dev_) {
+        if (lk_) psn_lk_sync(lk_);
+        dev_->release();
+        delete dev_;
+        dev_ = nullptr;
+    }
     if (lk_) psn_lk_destroy(lk_);
     lk_ = nullptr;
+}
+
+int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_jobs) {
+    if (!dev_) dev_ = new DeviceBuffers();
+    DeviceBuffers &b = *dev_;
+    if (b.nchains >= nchains && b.nfwd_pts >= nfwd_pts && b.nfwd_jobs >= nfwd_jobs && b.d_in) return PSN_LK_OK;
+    if (lk_) psn_lk_sync(lk_);
+    b.release();
+    const size_t K = std::max<size_t>(nchains, 16), F = std::max<size_t>(nfwd_pts, 1024), J = std::max<size_t>(nfwd_jobs, 16);
+    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, npt = K * cap + F;
+    bool ok = true;
+    auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
+    auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
+    dm((void **)&b.d_in, npt * 8);
+    dm((void **)&b.d_out, npt * 8);
+    dm((void **)&b.d_buf[0], K * cap * 8);
+    dm((void **)&b.d_buf[1], K * cap * 8);
+    dm((void **)&b.d_err, npt * 4);
+    dm((void **)&b.d_status, npt);
+    dm((void **)&b.d_boxes, K * 4 * 8);
+    dm((void **)&b.d_obox, K * S * 4 * 8);
+    dm((void **)&b.d_sets, K * S * cap * 8);
+    dm((void **)&b.d_cnt, (K + J) * 4);
+    dm((void **)&b.d_setcnt, K * S * 4);
+    dm((void **)&b.d_nsteps, K * 4);
+    hm((void **)&b.h_in, npt * 8);
+    hm((void **)&b.h_fwd_out, F * 8);
+    hm((void **)&b.h_sets, K * S * cap * 8);
+    hm((void **)&b.h_fwd_st, F);
+    hm((void **)&b.h_boxes, K * 4 * 8);
+    hm((void **)&b.h_obox, K * S * 4 * 8);
+    hm((void **)&b.h_cnt, (K + J) * 4);
+    hm((void **)&b.h_setcnt, K * S * 4);
+    hm((void **)&b.h_nsteps, K * 4);
+    if (!ok) {
+        b.release();
+        err_ = "device-chain buffers: allocation failed";
+        return PSN_LK_ERR_NOMEM;
+    }
+    b.nchains = K;
+    b.nfwd_pts = F;
+    b.nfwd_jobs = J;
+    return PSN_LK_OK;
+}
+
+// The backward chains of a frame on the device (:763-811): per step one
+// counted LK launch over every chain (capacity PSN_T2D_CHAIN_CAP points each;
+// a stopped chain's count is 0 so its workgroups exit at once) and one
+// LocalSearchKLT + inlier-compaction kernel writing the next step's points and
+// counts. The forward calls ride in step 1's launch. Everything is enqueued on
+// the LK context stream; the host waits once, for the packed results.
+int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<DetectedObject> &out, std::vector<Job> *fwd) {
+    const size_t K = chains.size(), cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
+    size_t F = 0;
+    const size_t J = fwd ? fwd->size() : 0;
+    for (size_t j = 0; j < J; j++) F += (*fwd)[j].in->size();
+    if (K == 0 && F == 0 && J == 0) return PSN_LK_OK;
+    int rc = EnsureDevice(K, F, J);
+    if (rc) return rc;
+    DeviceBuffers &b = *dev_;
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_);
+    // inputs: chain k's points at k*cap, then the forward jobs' points
+    for (size_t k = 0; k < K; k++) {
+        const Chain &c = chains[k];
+        const Rect box = out[c.obj].detection.box.scale(kFlowScale);
+        b.h_boxes[4 * k] = box.x;
+        b.h_boxes[4 * k + 1] = box.y;
+        b.h_boxes[4 * k + 2] = box.w;
+        b.h_boxes[4 * k + 3] = box.h;
+        for (size_t i = 0; i < c.curr.size(); i++) {
+            b.h_in[2 * (k * cap + i)] = c.curr[i].x;
+            b.h_in[2 * (k * cap + i) + 1] = c.curr[i].y;
+        }
+        b.h_cnt[k] = (int)c.curr.size();
+    }
+    size_t o = K * cap;
+    for (size_t j = 0; j < J; j++) {
+        const std::vector<Point2f> &pts = *(*fwd)[j].in;
+        for (size_t i = 0; i < pts.size(); i++, o++) {
+            b.h_in[2 * o] = pts[i].x;
+            b.h_in[2 * o + 1] = pts[i].y;
+        }
+        b.h_cnt[K + j] = (int)pts.size();
+    }
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && !rc) {
+            err_ = std::string(what) + ": " + hipGetErrorString(e);
+            rc = PSN_LK_ERR_HIP;
+        }
+    };
+    chk(hipMemcpyAsync(b.d_in, b.h_in, (K * cap + F) * 8, hipMemcpyHostToDevice, st), "chain inputs");
+    chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, std::max<size_t>(K, 1) * 32, hipMemcpyHostToDevice, st), "chain boxes");
+    chk(hipMemcpyAsync(b.d_cnt, b.h_cnt, (K + J) * 4, hipMemcpyHostToDevice, st), "chain counts");
+    chk(hipMemsetAsync(b.d_nsteps, 0, std::max<size_t>(K, 1) * 4, st), "chain steps");
+    chk(hipMemsetAsync(b.d_setcnt, 0, std::max<size_t>(K, 1) * S * 4, st), "chain set counts");
+    if (rc) return rc;
+    psn_t2d_chain_dev cd{};
+    cd.ndet = (int)K;
+    cd.cap = (int)cap;
+    cd.boxes = b.d_boxes;
+    cd.cnt = b.d_cnt;
+    cd.out_boxes = b.d_obox;
+    cd.sets = b.d_sets;
+    cd.set_cnt = b.d_setcnt;
+    cd.nsteps = b.d_nsteps;
+    const bool step1 = StepAvailable(1);
+    for (int step = 1; step < (int)S && (step == 1 || (K && StepAvailable(step))); step++) {
+        queries_.clear();
+        if (step > 1 || step1)
+            for (size_t k = 0; k < K; k++) {
+                psn_lk_query q;
+                q.prev_slot = ring_[kT2dInterval - step];
+                q.next_slot = ring_[kT2dInterval - 1 - step];
+                q.first_pt = (int)(k * cap);
+                q.num_pts = (int)cap;
+                psn_lk_default_params(&q.params);
+                q.params.win_w = q.params.win_h = (int)(b.h_boxes[4 * k + 2] * kWinSizeRatio);
+                queries_.push_back(q);
+            }
+        const size_t nb = queries_.size();
+        if (step == 1) {
+            for (size_t j = 0, off = K * cap; j < J; j++) {
+                const Job &jb = (*fwd)[j];
+                psn_lk_query q;
+                q.prev_slot = jb.prev_slot;
+                q.next_slot = jb.next_slot;
+                q.first_pt = (int)off;
+                q.num_pts = (int)jb.in->size();
+                psn_lk_default_params(&q.params);
+                q.params.win_w = jb.win_w;
+                q.params.win_h = jb.win_h;
+                queries_.push_back(q);
+                off += jb.in->size();
+            }
+            if (nb == 0 && K) {  // no frame t-1 for the chains: their counts must not be read as the
+                // forward queries' (the counted launch indexes counts by query)
+                chk(hipMemcpyAsync(b.d_cnt, b.h_cnt + K, J * 4, hipMemcpyHostToDevice, st), "forward counts");
+            }
+        }
+        if (queries_.empty()) break;
+        const float *in = step == 1 ? b.d_in : b.d_buf[step & 1];
+        rc = rc ? rc
+                : psn_lk_track_device_counted(lk_, queries_.data(), (int)queries_.size(), b.d_cnt, in, b.d_out,
+                                              b.d_status, b.d_err);
+        if (rc) return fail(rc, "psn_lk_track_device_counted");
+        if (step == 1 && F) {  // the forward results leave before step 2 reuses the buffers
+            chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, st), "forward points");
+            chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, st), "forward status");
+        }
+        if (nb == 0) break;
+        cd.cur = in;
+        cd.nxt = b.d_out;
+        cd.next_in = b.d_buf[(step + 1) & 1];
+        rc = psn_t2d_chain_step_device(&cd, step, st);
+        if (rc) return fail(rc, "psn_t2d_chain_step_device");
+    }
+    if (K) {
+        chk(hipMemcpyAsync(b.h_nsteps, b.d_nsteps, K * 4, hipMemcpyDeviceToHost, st), "chain steps");
+        chk(hipMemcpyAsync(b.h_obox, b.d_obox, K * S * 32, hipMemcpyDeviceToHost, st), "chain boxes");
+        chk(hipMemcpyAsync(b.h_setcnt, b.d_setcnt, K * S * 4, hipMemcpyDeviceToHost, st), "chain set counts");
+        chk(hipMemcpyAsync(b.h_sets, b.d_sets, K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain sets");
+    }
+    chk(hipStreamSynchronize(st), "chain sync");
+    if (rc) return rc;
+    for (size_t k = 0; k < K; k++) {
+        DetectedObject &ob = out[chains[k].obj];
+        const int ns = b.h_nsteps[k];
+        for (int s2 = 1; s2 <= ns; s2++) {
+            const double *r = b.h_obox + (k * S + s2) * 4;
+            ob.boxes.push_back(Rect(r[0], r[1], r[2], r[3]).scale(1.0 / kFlowScale));
+        }
+        for (int r = 0; ns > 0 && r <= ns; r++) {
+            const int n = b.h_setcnt[k * S + r];
+            const float *p = b.h_sets + (k * S + r) * cap * 2;
+            std::vector<Point2f> v((size_t)n);
+            for (int i = 0; i < n; i++) v[(size_t)i] = Point2f{p[2 * i], p[2 * i + 1]};
+            ob.vecvecTrackedFeatures.push_back(std::move(v));
+        }
+        chains[k].active = false;
+    }
+    for (size_t j = 0, off = 0; j < J; j++) {
+        Job &jb = (*fwd)[j];
+        const size_t m = jb.in->size();
+        jb.out->resize(m);
+        jb.status->resize(m);
+        for (size_t i = 0; i < m; i++, off++) {
+            (*jb.out)[i] = Point2f{b.h_fwd_out[2 * off], b.h_fwd_out[2 * off + 1]};
+            (*jb.status)[i] = b.h_fwd_st[off];
+        }
+    }
+    return PSN_LK_OK;
 }
 
 int Tracker2DFlow::PushFrame(const uint8_t *frame, int stride, int channels) {
@@ -290,6 +518,12 @@ int Tracker2DFlow::BackwardFeatureTracking(const std::vector<Detection> &dets,
     if (!lk_ || features.size() != dets.size()) return PSN_LK_ERR_ARG;
     std::vector<Chain> chains;
     BackwardBegin(dets, features, out, chains);
+    if (device_chain_) {
+        const int rc = ChainsOnDevice(chains, out, nullptr);
+        if (rc) return rc;
+        BackwardEnd(chains, out);
+        return PSN_LK_OK;
+    }
     std::vector<Job> jobs;
     for (int step = 1; StepAvailable(step); step++) {
         jobs.clear();
@@ -414,6 +648,14 @@ int Tracker2DFlow::TrackFrame(const std::vector<Detection> &dets, const std::vec
     BackwardBegin(dets, features, out, chains);
     std::vector<std::vector<uint8_t>> fstatus;
     std::vector<Job> jobs;
+    if (device_chain_) {
+        ForwardJobs(trackers, fstatus, jobs);
+        const int rc = ChainsOnDevice(chains, out, &jobs);
+        if (rc) return rc;
+        BackwardEnd(chains, out);
+        ForwardDone(trackers, fstatus, out, cost);
+        return PSN_LK_OK;
+    }
     // launch 1: backward step 1 of every detection + every forward call
     if (StepAvailable(1)) BackwardJobs(1, chains, out, jobs);
     const size_t nb = jobs.size();

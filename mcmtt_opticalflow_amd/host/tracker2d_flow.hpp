@@ -64,6 +64,9 @@ class Tracker2DFlow {
                    std::vector<DetectedObject> &out, const std::vector<Tracker2D *> &trackers, std::vector<float> &cost);
 
     psn_lk_ctx *lk() const { return lk_; }
+    // backward chain steps on the device (default) or on the host (PSN_T2D_HOST_CHAIN=1)
+    void SetDeviceChain(bool on) { device_chain_ = on; }
+    bool DeviceChain() const { return device_chain_; }
     const std::string &last_error() const { return err_; }
 
   private:
@@ -89,6 +92,10 @@ class Tracker2DFlow {
     void BackwardStepDone(std::vector<Chain> &chains, std::vector<DetectedObject> &out);
     void BackwardEnd(std::vector<Chain> &chains, std::vector<DetectedObject> &out);
     bool StepAvailable(int step) const;
+    // every chain step (LK launch + LocalSearchKLT kernel) enqueued back to back,
+    // one host sync at the end; forward jobs share step 1's launch
+    int ChainsOnDevice(std::vector<Chain> &chains, std::vector<DetectedObject> &out, std::vector<Job> *fwd);
+    int EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_jobs);
     void ForwardJobs(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
                      std::vector<Job> &jobs);
     void ForwardDone(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
@@ -104,6 +111,9 @@ class Tracker2DFlow {
     std::vector<float> xy_in_, xy_out_, err_out_, gf_xy_;
     std::vector<uint8_t> st_out_;
     std::vector<psn_lk_query> queries_;
+    bool device_chain_ = true;
+    struct DeviceBuffers;
+    DeviceBuffers *dev_ = nullptr;
 };
 
 }  // namespace psn

@@ -130,6 +130,7 @@ def load():
     L.psn_t2d_result_slot_bytes.restype = ctypes.c_size_t
     L.psn_t2d_pack_result.argtypes = [ctypes.POINTER(Track2DResult), vp, ctypes.c_size_t]
     L.psn_t2d_unpack_result.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(Track2DResult)]
+    L.psn_t2d_set_device_chain.argtypes = [vp, ip]
     L.psn_t2d_detect_features.argtypes = [vp, ctypes.POINTER(Detection), ip, ctypes.c_uint32]
     L.psn_t2d_backward.argtypes = [vp, ctypes.POINTER(Detection), ip]
     L.psn_t2d_forward.argtypes = [vp, ctypes.POINTER(Tracker), ip, ctypes.POINTER(Detection), ip, fp]
@@ -209,6 +210,10 @@ class FlowTracker:
 
     def __exit__(self, *a):
         self.close()
+
+    def set_device_chain(self, on: bool):
+        """LocalSearchKLT chain steps on the device (default) or on the host."""
+        self._check(self._L.psn_t2d_set_device_chain(self._h, int(bool(on))), "set_device_chain")
 
     def push_frame(self, img: np.ndarray):
         img = np.ascontiguousarray(img, np.uint8)

@@ -153,15 +153,22 @@ def _rect_roi(b, W, H):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("merged,gridfast", [(False, False), (True, False), (True, True)])
-def test_tracker2d_sequence_matches_oracle(oracle_mod, merged, gridfast):
-    W, H, T = 320, 240, 7
-    sc = synth.make_scene(21, W, H, 120, nboxes=3, box_w=24, box_h=60, max_speed=3.0)
+@pytest.mark.parametrize("merged,gridfast,device_chain,big", [(False, False, False, False), (True, False, False, False),
+                                                              (False, False, True, False), (True, False, True, False),
+                                                              (True, True, True, False), (True, True, True, True),
+                                                              (True, False, False, True)])
+def test_tracker2d_sequence_matches_oracle(oracle_mod, merged, gridfast, device_chain, big):
+    # big: 1080p-class boxes (64 x 160): 64 x 64 backward and 64 x 160 forward
+    # windows run the tiled LK kernel (the counted launches included)
+    W, H, T = (960, 540, 6) if big else (320, 240, 7)
+    bw, bh = (64, 160) if big else (24, 60)
+    sc = synth.make_scene(21, W, H, 120, nboxes=3, box_w=bw, box_h=bh, max_speed=3.0)
     rng = np.random.default_rng(77)
     ring = [None] * 4
     trackers = []  # oracle trackers (the harness's matching keeps both sides in sync)
     n_cost_finite = n_chain_steps = 0
     with t2d.FlowTracker(W, H) as ft:
+        ft.set_device_chain(device_chain)
         for t in range(T):
             img = sc.frame(t)
             ft.push_frame(img)
