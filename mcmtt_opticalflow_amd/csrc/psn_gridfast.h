@@ -8,8 +8,8 @@
 namespace psn {
 
 constexpr int kGfMaxRois = 64;      // rois per launch (kernel-argument table)
-constexpr int kGfStrip = 16;        // output rows per LDS strip
 constexpr int kGfMaxRegionW = 1024; // widest cell detection region (cell width - 6)
+constexpr int kGfMaxLds = 96 * 1024; // dynamic LDS of the per-cell kernel
 constexpr int kGfMaxTotal = 4096;   // maxTotalKeypoints limit (selection sort in LDS)
 
 struct GridFastArgs {
@@ -18,6 +18,7 @@ struct GridFastArgs {
     int nroi;
     int roi_base;        // index of rois[0] in the caller's array (shuffle key)
     int threshold, nonmax, grid_rows, grid_cols, per_cell, cap;
+    int rw_max, strip, list_cap;  // LDS plan: widest region of the launch, strip rows, keypoint list entries
     uint32_t seed;
     uint32_t *cell_kp;   // [nroi][ncell][per_cell] packed x | y << 16
     int *cell_cnt;       // [nroi][ncell]
@@ -27,6 +28,8 @@ struct GridFastArgs {
     int4 rois[kGfMaxRois];
 };
 
+// Dynamic LDS bytes of the per-cell kernel for a plan (rw_max, strip, list_cap).
+int gridfast_lds_bytes(int rw_max, int strip, int list_cap);
 // Both launches (per-cell detection, per-roi selection) on stream s.
 hipError_t launch_gridfast(const GridFastArgs &a, hipStream_t s);
 

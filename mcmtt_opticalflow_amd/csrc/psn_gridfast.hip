@@ -28,10 +28,6 @@ namespace psn {
 namespace {
 
 constexpr int kGfThreads = 256;
-constexpr int kPixRows = kGfStrip + 2 + 6;         // score rows + FAST radius
-constexpr int kPixCols = kGfMaxRegionW + 2 + 6;
-constexpr int kScoreRows = kGfStrip + 2;
-constexpr int kScoreCols = kGfMaxRegionW + 2;
 
 // fast.cpp makeOffsets(16): circle (dx, dy)
 __constant__ signed char kCircDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
@@ -52,13 +48,13 @@ __device__ __forceinline__ bool arc9(unsigned m) {
 // FAST-9/16 at tile position (tx, ty) (centre pixel): 0 = no corner, else
 // response + 1. cornerScore<16> in closed form: max(t, max over 9-arcs of
 // min(v - x), max over 9-arcs of min(x - v)) - 1 (fast_score.cpp).
-__device__ int fast_resp1(const uint8_t *pix, int ty, int tx, int t, int nonmax) {
-    const int v = pix[ty * kPixCols + tx];
+__device__ int fast_resp1(const uint8_t *pix, int pc, int ty, int tx, int t, int nonmax) {
+    const int v = pix[ty * pc + tx];
     int e[16];
     unsigned br = 0, dk = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        e[k] = (int)pix[(ty + kCircDy[k]) * kPixCols + tx + kCircDx[k]] - v;
+        e[k] = (int)pix[(ty + kCircDy[k]) * pc + tx + kCircDx[k]] - v;
         br |= (unsigned)(e[k] > t) << k;
         dk |= (unsigned)(e[k] < -t) << k;
     }
@@ -105,15 +101,38 @@ __device__ int block_scan_excl(int v, int *scratch, int *tot) {
 
 }  // namespace
 
+// q / d for 0 <= q < 2^24 by a float reciprocal and one correction step
+__device__ __forceinline__ int fdiv(int q, int d, float inv) {
+    int y = (int)((float)q * inv);
+    const int r = q - y * d;
+    if (r >= d) y++;
+    else if (r < 0) y--;
+    return y;
+}
+
 // One workgroup per (cell, roi): the cell's keypoints inside the roi after
-// keepStrongest, in row-major order.
+// keepStrongest, in row-major order. Dynamic LDS (host-sized for the widest
+// region of the launch, A.rw_max, and the strip height A.strip):
+//   pix   (strip + 8) x pc  bytes   frame rows of the strip + FAST radius + 1
+//   sco   (strip + 2) x sc  bytes   responses + 1 (0 = no corner) with a 1-px ring
+//   ks    strip x rw_max    bytes   keypoint responses + 1 of the strip
+//   list  A.list_cap u32            keypoints of the region in row-major order
+//                                   (x | y << 12 | response << 24; single pass)
+// Single pass when the region's keypoints surely fit the list (non-max: no
+// two keypoints are 8-neighbours, so at most ceil(W/2) * ceil(H/2)): FAST,
+// non-max and the score histogram while collecting, then keepStrongest over
+// the list. Otherwise two passes over the frame (histogram, then selection).
 __global__ __launch_bounds__(kGfThreads) void gridfast_cell_kernel(GridFastArgs A) {
-    __shared__ uint8_t pix[kPixRows * kPixCols];
-    __shared__ uint8_t sco[kScoreRows * kScoreCols];
-    __shared__ uint8_t ks[kGfStrip * kGfMaxRegionW];
+    extern __shared__ __attribute__((aligned(16))) uint8_t gsm[];
     __shared__ int hist[256];
     __shared__ int scratch[8];
-    __shared__ int sel[2];  // threshold response + 1 (-1: keep all), ties to keep
+    __shared__ int sel[2];  // threshold response (-1: keep all), ties to keep
+
+    const int SH = A.strip, PC = (A.rw_max + 8 + 3) & ~3, SC = A.rw_max + 2;
+    uint8_t *pix = gsm;
+    uint8_t *sco = pix + (SH + 8) * PC;
+    uint8_t *ks = sco + (((SH + 2) * SC + 15) & ~15);
+    uint32_t *list = (uint32_t *)(ks + ((SH * A.rw_max + 15) & ~15));
 
     const int cell = blockIdx.x, r = blockIdx.y;
     const int ci = cell / A.grid_cols, cj = cell - ci * A.grid_cols;
@@ -132,13 +151,46 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_cell_kernel(GridFastArgs 
         if (tid == 0) *cnt = 0;
         return;
     }
-    const int RW = ax1 - ax0;
-    const int SW = RW + 2;
+    const int RW = ax1 - ax0, RH = ay1 - ay0;
+    const int SW = RW + 2, PW = RW + 8;
+    const float invSW = 1.f / (float)SW, invRW = 1.f / (float)RW;
+    const bool single = A.nonmax && ((RW + 1) / 2) * ((RH + 1) / 2) <= A.list_cap;
 
     for (int i = tid; i < 256; i += kGfThreads) hist[i] = 0;
-    int tie_run = 0, kept_run = 0;
+    int tie_run = 0, kept_run = 0, nlist = 0;
 
-    for (int pass = 0; pass < 2; pass++) {
+    // ordered keep-selection over n row-major items (thread runs): item i has
+    // response resp(i) (< 0: none); kept items go to `out` in order
+    auto select_run = [&](int n, int T, int need, auto resp, auto coord) {
+        const int run = (n + kGfThreads - 1) / kGfThreads;
+        const int p0 = min(n, tid * run), p1 = min(n, p0 + run);
+        int ties = 0;
+        if (T >= 0)
+            for (int p = p0; p < p1; p++) ties += resp(p) == T;
+        int tie_tot;
+        const int tie_base = tie_run + block_scan_excl(ties, scratch, &tie_tot);
+        int keep = 0;
+        for (int p = p0, tb = tie_base; p < p1; p++) {
+            const int s = resp(p);
+            if (s < 0) continue;
+            if (s > T) keep++;
+            else if (s == T) keep += tb++ < need;
+        }
+        int kept_tot;
+        int pos = kept_run + block_scan_excl(keep, scratch, &kept_tot);
+        for (int p = p0, tb = tie_base; p < p1; p++) {
+            const int s = resp(p);
+            if (s < 0) continue;
+            bool k = s > T;
+            if (s == T) k = tb++ < need;
+            if (k) out[pos++] = coord(p);
+        }
+        tie_run += tie_tot;
+        kept_run += kept_tot;
+    };
+
+    const int npass = single ? 1 : 2;
+    for (int pass = 0; pass < npass; pass++) {
         if (pass == 1) {
             if (tid == 0) {
                 int total = 0;
@@ -161,75 +213,103 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_cell_kernel(GridFastArgs 
             __syncthreads();
         }
         const int T = pass ? sel[0] : 0, need = pass ? sel[1] : 0;
-        for (int y0 = ay0; y0 < ay1; y0 += kGfStrip) {
-            const int sh = min(kGfStrip, ay1 - y0);
+        for (int y0 = ay0; y0 < ay1; y0 += SH) {
+            const int sh = min(SH, ay1 - y0);
             // pixels rows [y0 - 4, y0 + sh + 4), cols [ax0 - 4, ax1 + 4), clamped
             // into the image (clamped values are never read by a computed score)
-            const int pr = sh + 8, pc = RW + 8;
             __syncthreads();  // previous strip's readers are done
-            for (int q = tid; q < pr * pc; q += kGfThreads) {
-                const int yy = q / pc, xx = q - yy * pc;
-                const int gy = clampi(y0 - 4 + yy, 0, A.h - 1), gx = clampi(ax0 - 4 + xx, 0, A.w - 1);
-                pix[yy * kPixCols + xx] = A.img[(size_t)gy * A.pitch + gx];
+            {  // every thread issues up to 16 loads before its first LDS store
+                const int n = (sh + 8) * PW;
+                const float invPW = 1.f / (float)PW;
+                for (int b0 = 0; b0 < n; b0 += 16 * kGfThreads) {
+                    uint8_t v[16];
+                    int dst[16];
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int q = b0 + k * kGfThreads + tid;
+                        dst[k] = -1;
+                        if (q < n) {
+                            const int yy = fdiv(q, PW, invPW), xx = q - yy * PW;
+                            v[k] = A.img[(size_t)clampi(y0 - 4 + yy, 0, A.h - 1) * A.pitch + clampi(ax0 - 4 + xx, 0, A.w - 1)];
+                            dst[k] = yy * PC + xx;
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < 16; k++)
+                        if (dst[k] >= 0) pix[dst[k]] = v[k];
+                }
             }
             __syncthreads();
-            // scores at rows [y0 - 1, y0 + sh + 1), cols [ax0 - 1, ax1 + 1)
+            // responses at rows [y0 - 1, y0 + sh + 1), cols [ax0 - 1, ax1 + 1)
             for (int q = tid; q < (sh + 2) * SW; q += kGfThreads) {
-                const int yy = q / SW, xx = q - yy * SW;
+                const int yy = fdiv(q, SW, invSW), xx = q - yy * SW;
                 const int gy = y0 - 1 + yy, gx = ax0 - 1 + xx;
-                int s = 0;
-                if (gy >= dy0 && gy < dy1 && gx >= dx0 && gx < dx1) s = fast_resp1(pix, yy + 3, xx + 3, A.threshold, A.nonmax);
-                sco[yy * kScoreCols + xx] = (uint8_t)s;
+                int v = 0;
+                if (gy >= dy0 && gy < dy1 && gx >= dx0 && gx < dx1) v = fast_resp1(pix, PC, yy + 3, xx + 3, A.threshold, A.nonmax);
+                sco[yy * SC + xx] = (uint8_t)v;
             }
             __syncthreads();
-            // keypoints of the strip (strict 8-neighbour maximum of the score)
+            // keypoints of the strip (strict 8-neighbour maximum of the response)
             for (int q = tid; q < sh * RW; q += kGfThreads) {
-                const int yy = q / RW, xx = q - yy * RW;
-                const uint8_t *c = sco + (yy + 1) * kScoreCols + xx + 1;
-                const int s = c[0];
-                bool kp = s != 0;
+                const int yy = fdiv(q, RW, invRW), xx = q - yy * RW;
+                const uint8_t *c = sco + (yy + 1) * SC + xx + 1;
+                const int v = c[0];
+                bool kp = v != 0;
                 if (kp && A.nonmax) {
                     // FAST_t compares responses, a non-corner counting as 0
-                    int nb = max(max(max(c[-1], c[1]), max(c[-kScoreCols - 1], c[-kScoreCols])),
-                                 max(max(c[-kScoreCols + 1], c[kScoreCols - 1]), max(c[kScoreCols], c[kScoreCols + 1])));
-                    kp = s - 1 > max(nb - 1, 0);
+                    const int nb = max(max(max(c[-1], c[1]), max(c[-SC - 1], c[-SC])),
+                                       max(max(c[-SC + 1], c[SC - 1]), max(c[SC], c[SC + 1])));
+                    kp = v - 1 > max(nb - 1, 0);
                 }
-                ks[q] = kp ? (uint8_t)s : 0;
-                if (kp && pass == 0) atomicAdd(&hist[s - 1], 1);
+                ks[q] = kp ? (uint8_t)v : 0;
+                if (kp && pass == 0) atomicAdd(&hist[v - 1], 1);
             }
             __syncthreads();
-            if (pass == 0) continue;
-            // ordered selection: thread runs of contiguous row-major positions
-            const int n = sh * RW, run = (n + kGfThreads - 1) / kGfThreads;
-            const int p0 = min(n, tid * run), p1 = min(n, p0 + run);
-            int ties = 0;
-            if (T >= 0)
-                for (int p = p0; p < p1; p++) ties += ks[p] == T + 1;
-            int tie_tot;
-            int tie_base = tie_run + block_scan_excl(ties, scratch, &tie_tot);
-            int keep = 0;
-            for (int p = p0, tb = tie_base; p < p1; p++) {
-                const int s = (int)ks[p] - 1;
-                if (s < 0) continue;
-                if (s > T) keep++;
-                else if (s == T) keep += tb++ < need;
-            }
-            int kept_tot;
-            int pos = kept_run + block_scan_excl(keep, scratch, &kept_tot);
-            for (int p = p0, tb = tie_base; p < p1; p++) {
-                const int s = (int)ks[p] - 1;
-                if (s < 0) continue;
-                bool k = s > T;
-                if (s == T) k = tb++ < need;
-                if (k) {
-                    const int yy = p / RW, xx = p - yy * RW;
-                    out[pos++] = (uint32_t)(ax0 + xx) | ((uint32_t)(y0 + yy) << 16);
+            if (single) {  // append the strip's keypoints to the list, in order
+                const int n = sh * RW, run = (n + kGfThreads - 1) / kGfThreads;
+                const int p0 = min(n, tid * run), p1 = min(n, p0 + run);
+                int m = 0;
+                for (int p = p0; p < p1; p++) m += ks[p] != 0;
+                int tot;
+                int pos = nlist + block_scan_excl(m, scratch, &tot);
+                for (int p = p0; p < p1; p++) {
+                    const int v = ks[p];
+                    if (!v) continue;
+                    const int yy = fdiv(p, RW, invRW), xx = p - yy * RW;
+                    list[pos++] = (uint32_t)(ax0 + xx) | ((uint32_t)(y0 + yy) << 12) | ((uint32_t)(v - 1) << 24);
                 }
+                nlist += tot;
+                continue;
             }
-            tie_run += tie_tot;
-            kept_run += kept_tot;
+            if (pass == 0) continue;
+            select_run(sh * RW, T, need, [&](int p) { return (int)ks[p] - 1; },
+                       [&](int p) {
+                           const int yy = fdiv(p, RW, invRW), xx = p - yy * RW;
+                           return (uint32_t)(ax0 + xx) | ((uint32_t)(y0 + yy) << 16);
+                       });
         }
         __syncthreads();
+    }
+    if (single) {  // keepStrongest over the collected list
+        if (tid == 0) {
+            int T = -1, need = 0;
+            if (nlist > A.per_cell) {
+                int cum = 0;
+                for (int s = 255; s >= 0; s--) {
+                    if (cum + hist[s] >= A.per_cell) {
+                        T = s;
+                        need = A.per_cell - cum;
+                        break;
+                    }
+                    cum += hist[s];
+                }
+            }
+            sel[0] = T;
+            sel[1] = need;
+        }
+        __syncthreads();
+        select_run(nlist, sel[0], sel[1], [&](int p) { return (int)(list[p] >> 24); },
+                   [&](int p) { return (list[p] & 0xfffu) | (((list[p] >> 12) & 0xfffu) << 16); });
     }
     if (tid == 0) *cnt = kept_run;
 }
@@ -300,9 +380,22 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_select_kernel(GridFastArg
     }
 }
 
+int gridfast_lds_bytes(int rw_max, int strip, int list_cap) {
+    const int pc = (rw_max + 8 + 3) & ~3, sc = rw_max + 2;
+    return (strip + 8) * pc + (((strip + 2) * sc + 15) & ~15) + ((strip * rw_max + 15) & ~15) + 4 * list_cap;
+}
+
 hipError_t launch_gridfast(const GridFastArgs &a, hipStream_t s) {
     if (a.nroi <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gridfast_cell_kernel, dim3(a.grid_rows * a.grid_cols, a.nroi), dim3(kGfThreads), 0, s, a);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void *)gridfast_cell_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           kGfMaxLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int lds = gridfast_lds_bytes(a.rw_max, a.strip, a.list_cap);
+    hipLaunchKernelGGL(gridfast_cell_kernel, dim3(a.grid_rows * a.grid_cols, a.nroi), dim3(kGfThreads), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(gridfast_select_kernel, dim3(a.nroi), dim3(kGfThreads), 0, s, a);

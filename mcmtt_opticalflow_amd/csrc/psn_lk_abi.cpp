@@ -793,6 +793,16 @@ static int gridfast_impl(psn_lk_ctx *c, int slot, const int *rois, int nroi, con
         a.out_xy = d_xy + (size_t)base * p.cap * 2;
         a.out_count = d_cnt + base;
         a.out_total = d_tot ? d_tot + base : nullptr;
+        // LDS plan: the widest region a (roi, cell) workgroup can see, the strip
+        // height, the single-pass keypoint list (coordinates packed in 12 bits)
+        int rw_max = 1;
+        const int cell_w = (c->width + p.grid_cols - 1) / p.grid_cols - 6;
+        for (int i = 0; i < n; i++) rw_max = std::max(rw_max, std::min(rois[4 * (size_t)(base + i) + 2], cell_w));
+        a.rw_max = rw_max;
+        a.list_cap = (c->width <= 4096 && c->height <= 4096) ? 4096 : 0;
+        a.strip = 32;
+        while (a.strip > 8 && psn::gridfast_lds_bytes(rw_max, a.strip, a.list_cap) > psn::kGfMaxLds) a.strip >>= 1;
+        while (a.list_cap > 0 && psn::gridfast_lds_bytes(rw_max, a.strip, a.list_cap) > psn::kGfMaxLds) a.list_cap >>= 1;
         for (int i = 0; i < n; i++) {
             const int *r = rois + 4 * (size_t)(base + i);
             // clip to the image (cropWithSize already did for the reference's rois)
