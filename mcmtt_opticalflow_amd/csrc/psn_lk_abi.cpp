@@ -57,6 +57,9 @@ struct psn_lk_ctx {
     int force_threads = 0;
     bool force_generic = false;
     bool onewave = true;  // PSN_LK_ONEWAVE=0: multi-wave iterations in the single-tile kernel
+    // PSN_LK_TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
+    // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
+    int tiled_lds = 76 * 1024;
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     // GridFAST scratch (per-cell keypoints of one launch) and host-call outputs
     uint32_t *d_gf_kp = nullptr;
@@ -148,6 +151,7 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (const char *e = getenv("PSN_LK_THREADS")) c->force_threads = atoi(e);
     if (const char *e = getenv("PSN_LK_GENERIC")) c->force_generic = atoi(e) != 0;
     if (const char *e = getenv("PSN_LK_ONEWAVE")) c->onewave = atoi(e) != 0;
+    if (const char *e = getenv("PSN_LK_TILED_LDS")) c->tiled_lds = std::max(16 * 1024, std::min(atoi(e), 160 * 1024 - 1024));
     if (const char *e = getenv("PSN_LK_FUSED_HELPERS")) c->fused_helpers = std::max(0, atoi(e));
     auto fail = [&](int rc) {
         psn_lk_destroy(c);
@@ -446,7 +450,9 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
             ow_rows = psn::ow_rows(w, h);
             ow_lds = so.total;
         }
-    } else if (psn::lk_lds_bytes(w, h, tr) > 64 * 1024) {
+    } else if (psn::lk_lds_bytes(w, h, tr) > std::min(64 * 1024, c->tiled_lds)) {
+        // tile rows: within the occupancy budget when the window allows, else the LDS limit
+        while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > c->tiled_lds) tr--;
         while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
         if (psn::lk_lds_bytes(w, h, tr) > budget)
             return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d does not fit LDS", w, h);
@@ -580,6 +586,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                 psn::LkQueryDev &d = a.q[i];
                 if (d.tile_rows >= d.win_h) {
                     int tr = d.win_h;
+                    while (tr > 1 && psn::lk_lds_bytes(d.win_w, d.win_h, tr) > c->tiled_lds) tr--;
                     while (tr > 1 && psn::lk_lds_bytes(d.win_w, d.win_h, tr) > 160 * 1024 - 1024) tr--;
                     d.tile_rows = tr;
                 }

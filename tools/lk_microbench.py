@@ -24,13 +24,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--points", type=int, default=512)
     ap.add_argument("--win", type=int, default=21)
+    ap.add_argument("--win-h", type=int, default=0)
     ap.add_argument("--levels", type=int, default=1)
     ap.add_argument("--iters", default="0,1,2,4,8,16,30")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--textures", default="strong,weak")
     args = ap.parse_args()
     W, H = 1920, 1080
     out = []
-    for texture in ("strong", "weak"):
+    textures = args.textures.split(",")
+    for texture in textures:
         sc = synth.make_scene(0, W, H, args.points)
         f0, f1 = sc.frame(0), sc.frame(1)
         if texture == "weak":  # 1/8 contrast: gradients 8x smaller, b-sums mostly exact
@@ -41,7 +44,7 @@ def main():
             ctx.push_frame(0, f0)
             ctx.push_frame(1, f1)
             for k in [int(x) for x in args.iters.split(",")]:
-                p = lk.make_params((args.win, args.win), args.levels - 1, criteria=(1, k, 0.0))
+                p = lk.make_params((args.win, args.win_h or args.win), args.levels - 1, criteria=(1, k, 0.0))
                 q = lk.make_query(0, 1, 0, len(pts), p)
                 ctx.track([q], pts)  # warm
                 ctx.enable_timing(args.reps)
@@ -51,7 +54,7 @@ def main():
                 us = 1e3 * ts["track_ms"] / ts["n_track"]
                 out.append({"texture": texture, "iters": k, "us": round(us, 2)})
                 print(json.dumps(out[-1]), flush=True)
-    for texture in ("strong", "weak"):
+    for texture in textures:
         xs = np.array([o["iters"] for o in out if o["texture"] == texture], float)
         ys = np.array([o["us"] for o in out if o["texture"] == texture], float)
         slope, icpt = np.polyfit(xs, ys, 1)
