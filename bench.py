@@ -254,8 +254,9 @@ def main():
             "dtype": "u8+f32",
             "data": "synthetic",
             "config": {
-                "workload": (("BASELINE.json configs[1]: 1 camera per GPU" if C == 1 else
-                              f"{C} cameras per GPU (north_star 4-camera target shape)")
+                "workload": (("BASELINE.json configs[1]: 1 camera per GPU"
+                              if (C, W, H, N, L, win) == (1, 1920, 1080, 512, 4, 21) else
+                              f"{C} camera(s) per GPU" + (" (north_star 4-camera target shape)" if C == 4 else ""))
                              + f", {W}x{H} gray, {N} points, {L}-level pyramid, {win}x{win} window, "
                                "per-frame pyramid build + LK + tracklet propagation"
                              + (", RCCL all-gather of per-camera slots" if world > 1 else "")),
