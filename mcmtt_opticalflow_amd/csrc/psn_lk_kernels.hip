@@ -282,6 +282,16 @@ hipError_t launch_pyramid(const PyrBuildArgs &a, hipStream_t s) {
 constexpr unsigned kSatCap = 1u << 30;
 constexpr int kExact = 1 << 24;
 
+// Exactness of a float sum of integer terms t in ANY order or chain split:
+// every partial sum is a subset sum, inside [-N, P] (P = sum of the positive
+// terms, N = sum of |negative terms|), so max(P, N) <= 2^24 makes every
+// partial sum an exact float. With A = sum|t| and S = sum t:
+// max(P, N) = (A + |S|) / 2. A <= 2^25 also keeps an int32 S unwrapped
+// (A is reduced saturating, so a wrapped S comes with a failing A).
+__device__ __forceinline__ bool sums_exact(unsigned A, int S) {
+    return A + (unsigned)abs(S) <= (2u << 24);
+}
+
 __device__ __forceinline__ int wave_sum(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
@@ -742,7 +752,7 @@ __global__ __launch_bounds__(NT) void lk_kernel(LkLaunchArgs A) {
             }
             block_reduce4<NT, false>(s1, s2, a1, a2, REDI);
             float b1, b2;
-            if (a1 <= (unsigned)kExact && a2 <= (unsigned)kExact) {
+            if (sums_exact(a1, s1) && sums_exact(a2, s2)) {  // subset-sum bound (see sums_exact)
                 b1 = (float)s1;
                 b2 = (float)s2;
             } else {
@@ -1332,15 +1342,6 @@ __device__ __forceinline__ void wave_sum4(int &s1, int &s2, unsigned &a1, unsign
     a1 = (unsigned)__builtin_amdgcn_readlane((int)a1, 63);
     a2 = (unsigned)__builtin_amdgcn_readlane((int)a2, 63);
 }
-// Exactness of a float sum of integer terms t in ANY order or chain split:
-// every partial sum is a subset sum, inside [-N, P] (P = sum of the positive
-// terms, N = sum of |negative terms|), so max(P, N) <= 2^24 makes every
-// partial sum an exact float. With A = sum|t| and S = sum t:
-// max(P, N) = (A + |S|) / 2. A <= 2^25 also keeps the int32 S unwrapped.
-__device__ __forceinline__ bool sums_exact(unsigned A, int S) {
-    return A + (unsigned)abs(S) <= (2u << 24);
-}
-
 // Level geometry of the I window (prevPt/2^l - halfWin): top-left, validity and weights.
 struct IGeo {
     int ipx, ipy, w00, w01, w10, w11;
@@ -1469,6 +1470,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
         if (!gg.valid) continue;
         dma_patch<NT>(smem + lay.pim + l * lay.pim_stride, I, gg.ipy - 1, gg.ipx - 1, PW, h + 3, lk_pat_m(w), Q.dv_pm);
     }
+    LK_STAMP(62);
     // level table for the level loops (ordered by the barrier below)
     int *TBL = (int *)(smem + lay.tbl);
     if (tid < 2 * kStMaxLev) {
@@ -1479,6 +1481,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             if (tl == l) L = ring_level(A.ring, ts ? Q.next_slot : Q.prev_slot, l);
         tbl_put(TBL, ts, tl, L);
     }
+    LK_STAMP(63);
     JPStage<NT> pf;  // prefetched J region of level pf_level at (pf_y0, pf_x0)
     int pf_level, pf_x0, pf_y0;
     {

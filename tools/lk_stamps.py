@@ -52,6 +52,8 @@ def main():
     out["ow_setup_cycles"] = float((s[:, 54] - s[:, 53]).mean())  # one-wave mode: stamp 54 ends its setup
     out["l3_setup_split"] = {"54_55": float((s[:, 55] - s[:, 54]).mean()), "pf_store": float((s[:, 56] - s[:, 55]).mean()),
                              "to_barrier_done": float((s[:, 31] - s[:, 56]).mean())}
+    out["dma_issue_split"] = {"i_patches": float((s[:, 62] - s[:, 58]).mean()), "level_table": float((s[:, 63] - s[:, 62]).mean()),
+                              "j_prefetch": float((s[:, 59] - s[:, 63]).mean())}
     out["prologue_split"] = {"point_load": float((s[:, 58] - s[:, 60]).mean()), "dma_issue": float((s[:, 59] - s[:, 58]).mean()),
                              "dma_wait_barrier": float((s[:, 50] - s[:, 59]).mean())}
     prev_end = s[:, 53]
