@@ -60,6 +60,7 @@ struct psn_lk_ctx {
     // PSN_LK_TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
     // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
     int tiled_lds = 76 * 1024;
+    int num_cus = 256;  // compute units of the device (launch shaping)
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     // GridFAST scratch (per-cell keypoints of one launch) and host-call outputs
     uint32_t *d_gf_kp = nullptr;
@@ -151,6 +152,11 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (const char *e = getenv("PSN_LK_THREADS")) c->force_threads = atoi(e);
     if (const char *e = getenv("PSN_LK_GENERIC")) c->force_generic = atoi(e) != 0;
     if (const char *e = getenv("PSN_LK_ONEWAVE")) c->onewave = atoi(e) != 0;
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->num_cus = cus;
+    }
     if (const char *e = getenv("PSN_LK_TILED_LDS")) c->tiled_lds = std::max(16 * 1024, std::min(atoi(e), 160 * 1024 - 1024));
     if (const char *e = getenv("PSN_LK_FUSED_HELPERS")) c->fused_helpers = std::max(0, atoi(e));
     auto fail = [&](int rc) {
@@ -559,6 +565,9 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                 if (oept == 4 && E < 8) E = 8;
                 threads = 1000 * E + 2560 + oept;
                 lds = lds_ow;
+                // more points than two workgroups per CU hold, and LDS for three:
+                // the 168-VGPR variant (three per CU; one-camera launches fit at two)
+                if (oept == 2 && E <= 8 && lds_ow <= 53 * 1024 && wgs > 2 * c->num_cus) threads += 200000;
             }
         }
         if (c->pend && all_single) {  // fuse the deferred build into this launch's tail

@@ -155,27 +155,47 @@ constexpr int kOwMaxRows = 16;
 // every row moves as lk_pat_m(w) aligned dwords (LDS-DMA).
 __host__ __device__ inline int lk_pat_m(int w) { return (w + 3 + 3 + 3) >> 2; }
 __host__ __device__ inline int lk_pat_rs(int w) { return 4 * lk_pat_m(w); }
+//   one-wave layout (ow): the window values IW of every level, then a union
+//     of what only the prologue uses (I patches, Scharr planes, the A-phase
+//     float chain planes RA) and what only the iterations use (the two J
+//     regions JP, the b chain planes / err row R) -- 49.6 KB at 21x21 with 4
+//     levels: three workgroups per CU.
 struct LkStLayout {
-    int tbl, ri, lv, jp, pim, pim_stride, dg, dg_stride, iw, iw_stride, r, total;
+    int tbl, ri, lv, jp, pim, pim_stride, dg, dg_stride, iw, iw_stride, r, ra, total;
     __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev, bool ow = false) {
         const int wh = w * h;
         tbl = 0;
         ri = tbl + 2 * kMaxLevels * 8 * 4;
         lv = ri + kStRiInts * 4;
-        jp = kStScratchBytes;                      // fused builds use LDS from here
-        pim = jp + (ow ? 8 * st_jp_cm_dw(w, h) : align16(4 * st_jreg_w(w) * st_jreg_h(h)));
         pim_stride = align16((h + 3) * lk_pat_rs(w));
-        dg = pim + nlev * pim_stride;
         dg_stride = align16(4 * (h + 1) * (w + 1));
-        iw = dg + nlev * dg_stride;
         iw_stride = align16(8 * wh);
-        r = iw + nlev * iw_stride;
-        int rb = 12 * nlev * lk_st_planeA(w, h, sse);
+        const int rb_a = 12 * nlev * lk_st_planeA(w, h, sse);
         const int pb = 16 * lk_st_planeB(w, h, sse);
         const int eb = 4 * round16i(wh);
-        if (rb < pb) rb = pb;
-        if (rb < eb) rb = eb;
-        total = r + rb;
+        if (ow) {
+            iw = kStScratchBytes;  // fused builds use LDS from kStScratchBytes, after the LK work
+            const int u = iw + nlev * iw_stride;
+            pim = u;  // prologue view
+            dg = pim + nlev * pim_stride;
+            ra = dg + nlev * dg_stride;
+            const int end_pro = ra + rb_a;
+            jp = u;  // iteration view
+            r = jp + 8 * st_jp_cm_dw(w, h);
+            const int end_it = r + (pb > eb ? pb : eb);
+            total = end_pro > end_it ? end_pro : end_it;
+        } else {
+            jp = kStScratchBytes;  // fused builds use LDS from here
+            pim = jp + align16(4 * st_jreg_w(w) * st_jreg_h(h));
+            dg = pim + nlev * pim_stride;
+            iw = dg + nlev * dg_stride;
+            r = iw + nlev * iw_stride;
+            ra = r;
+            int rb = rb_a;
+            if (rb < pb) rb = pb;
+            if (rb < eb) rb = eb;
+            total = r + rb;
+        }
     }
 };
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel

@@ -1391,8 +1391,8 @@ __device__ __forceinline__ void pyr_tail(const LkLaunchArgs &A, uint8_t *smem) {
 // prologue landed, 51 Scharr of all levels, 52 A products + reduction, 53
 // solver table; per level L*10+0 start, +1 J staged, +2 window loaded, +7
 // iterations done, +8 iteration count; 40..45 accumulated iteration phases.
-template <int NT, int EPT, int E>
-__global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
+template <int NT, int EPT, int E, int OCC = 1>
+__global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1418,7 +1418,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     int *RI = (int *)(smem + lay.ri);
     float *LV = (float *)(smem + lay.lv);
     uint32_t *JP = (uint32_t *)(smem + lay.jp);
-    float *R = (float *)(smem + lay.r);
+    float *R = (float *)(smem + lay.r);    // b chain planes / err row (iterations)
+    float *RA = (float *)(smem + lay.ra);  // A-phase chain planes (prologue; == R outside the one-wave layout)
     const ChainGeo GA = chain_geo_A(w, h, sse), GB = chain_geo_B(w, h, sse);
 
     // ---- per-thread window pixels (fixed for the whole kernel). Idle lanes
@@ -1445,7 +1446,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
     if (A.pyr_ntiles > 0) __builtin_amdgcn_s_setprio(2);
     // ---- prologue: zero the A planes' chain padding (ordered by the barrier
     // after the DMA); level geometry comes from the kernel arguments ----
-    zero_pads<NT>(R, GA, 3 * nlev);
+    zero_pads<NT>(RA, GA, 3 * nlev);
     const JWalk wk_int = jwalk_t(tid, JRW >> 2, NT, Q.dv_jrw4), wk_bord = jwalk_t(tid, JRW, NT, Q.dv_jrw);  // J staging walks
     LK_STAMP(60);
 
@@ -1542,7 +1543,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
             const uint8_t *P = smem + lay.pim + l * lay.pim_stride + ((gg.ipx - 1) & 3);
             const short2 *Dg = (const short2 *)(smem + lay.dg + l * lay.dg_stride);
             int2 *IW = (int2 *)(smem + lay.iw + l * lay.iw_stride);
-            float *PA = R + l * 3 * GA.P;
+            float *PA = RA + l * 3 * GA.P;
 #pragma unroll
             for (int k = 0; k < EPT; k++) {
                 const uint8_t *p = P + ofsP[k];
@@ -1598,7 +1599,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_st(LkLaunchArgs A) {
                 if (bound > (unsigned)kExact) {
                     const int base = (l * 3 + s) * GA.P + (ch < 4 ? ch * GA.S : 4 * GA.S);
                     const int nb = (ch < 4 ? GA.S : GA.T) >> 4;
-                    acc = chain_sum16(R + base, nb);
+                    acc = chain_sum16(RA + base, nb);
                 }
                 CH[q] = acc;
             }
@@ -2297,6 +2298,11 @@ hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_
             case 18562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 16>), grid, dim3(256), lds_bytes, s, a); break;
             case 18564: hipLaunchKernelGGL((lk_kernel_st<256, 4, 16>), grid, dim3(256), lds_bytes, s, a); break;
             case 2564: hipLaunchKernelGGL((lk_kernel_st<256, 4, 0>), grid, dim3(256), lds_bytes, s, a); break;
+            // one-wave kernels held to 168 VGPRs: three workgroups per CU when the
+            // launch has more points than two per CU can hold (+200000)
+            case 206562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 4, 3>), grid, dim3(256), lds_bytes, s, a); break;
+            case 209562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 7, 3>), grid, dim3(256), lds_bytes, s, a); break;
+            case 210562: hipLaunchKernelGGL((lk_kernel_st<256, 2, 8, 3>), grid, dim3(256), lds_bytes, s, a); break;
             default: return hipErrorInvalidValue;
         }
     } else {
@@ -2321,7 +2327,9 @@ hipError_t lk_kernels_init() {
                         (const void *)lk_kernel_st<512, 1, 0>,  (const void *)lk_kernel_st<512, 2, 0>,
                         (const void *)lk_kernel_st<256, 2, 4>,  (const void *)lk_kernel_st<256, 2, 7>,
                         (const void *)lk_kernel_st<256, 2, 8>,  (const void *)lk_kernel_st<256, 4, 8>,
-                        (const void *)lk_kernel_st<256, 2, 16>, (const void *)lk_kernel_st<256, 4, 16>};
+                        (const void *)lk_kernel_st<256, 2, 16>, (const void *)lk_kernel_st<256, 4, 16>,
+                        (const void *)lk_kernel_st<256, 2, 4, 3>,  (const void *)lk_kernel_st<256, 2, 7, 3>,
+                        (const void *)lk_kernel_st<256, 2, 8, 3>};
     for (const void *f : st)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)pyramid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
