@@ -157,6 +157,13 @@ class LKContext:
                                                        ctypes.c_uint32(seed & 0xffffffff), d_xy, d_count, d_total),
                     "gridfast_detect_device")
 
+    def track_device_counted(self, queries: list[LkQuery], d_counts: int, d_prev: int, d_next: int, d_status: int,
+                             d_err: int | None):
+        """Queries sized num_pts (capacity); query i processes d_counts[i] points (device int32)."""
+        arr = (LkQuery * max(len(queries), 1))(*queries)
+        self._check(self._L.psn_lk_track_device_counted(self._h, arr, len(queries), d_counts, d_prev, d_next,
+                                                        d_status, d_err), "track_device_counted")
+
     def enable_timing(self, capacity: int = 1024, every: int = 1):
         """HIP-event timing of every `every`-th push (pyramid launch) / track (LK launch) call."""
         self._check(self._L.psn_lk_enable_timing(self._h, int(capacity), int(every)), "enable_timing")

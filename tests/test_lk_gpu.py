@@ -308,3 +308,37 @@ def test_lk_kernel_variants(oracle_mod, monkeypatch, env, flags):
         ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
         gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
         assert_same(gpu, ref, f"{env} {win}")
+
+
+@pytest.mark.parametrize("win", [(21, 21), (64, 64)])
+def test_lk_counted_launch(oracle_mod, win):
+    """psn_lk_track_device_counted: queries sized for 50 points each process
+    the count found on the device (0, 17, 50); the points inside a count match
+    the oracle bit for bit, the rest of the outputs stay untouched (single-tile
+    and tiled kernels)."""
+    import hiprt
+
+    sc, f0, f1 = scene_pair(12, 640, 480, 150)
+    pts = sc.points_at(0)
+    counts = np.array([0, 17, 50], np.int32)
+    d_f0, d_f1 = hiprt.DeviceBuffer.from_array(f0), hiprt.DeviceBuffer.from_array(f1)
+    d_p = hiprt.DeviceBuffer.from_array(pts)
+    sentinel = np.full(pts.shape, -7.0, np.float32)
+    d_n = hiprt.DeviceBuffer.from_array(sentinel)
+    d_s, d_e = hiprt.DeviceBuffer.from_array(np.full(len(pts), 9, np.uint8)), hiprt.DeviceBuffer(4 * len(pts))
+    d_c = hiprt.DeviceBuffer.from_array(counts)
+    with glk.LKContext(640, 480, ring_slots=2, max_level_cap=3) as ctx:
+        ctx.push_frame_device(0, d_f0.addr, 640, 1)
+        ctx.push_frame_device(1, d_f1.addr, 640, 1)
+        qs = [glk.make_query(0, 1, 50 * i, 50, glk.make_params(win, 3)) for i in range(3)]
+        ctx.track_device_counted(qs, d_c.addr, d_p.addr, d_n.addr, d_s.addr, d_e.addr)
+        ctx.sync()
+    g_n, g_s = d_n.to_array(pts.shape, np.float32), d_s.to_array(len(pts), np.uint8)
+    g_e = d_e.to_array(len(pts), np.float32)
+    for i, c in enumerate(counts):
+        lo = 50 * i
+        if c:
+            ref = oracle_ref(oracle_mod, f0, f1, pts[lo:lo + c], win, 3)
+            assert_same((g_n[lo:lo + c], g_s[lo:lo + c], g_e[lo:lo + c]), ref, f"query {i}")
+        np.testing.assert_array_equal(g_n[lo + c:lo + 50], sentinel[lo + c:lo + 50])
+        assert (g_s[lo + c:lo + 50] == 9).all()
