@@ -57,6 +57,7 @@ struct psn_lk_ctx {
     int force_threads = 0;
     bool force_generic = false;
     bool onewave = true;  // PSN_LK_ONEWAVE=0: multi-wave iterations in the single-tile kernel
+    bool box = true;      // PSN_LK_BOX=0: box windows run the row-tiled kernel instead of lk_kernel_bx
     // PSN_LK_TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
     // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
     int tiled_lds = 76 * 1024;
@@ -152,6 +153,7 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (const char *e = getenv("PSN_LK_THREADS")) c->force_threads = atoi(e);
     if (const char *e = getenv("PSN_LK_GENERIC")) c->force_generic = atoi(e) != 0;
     if (const char *e = getenv("PSN_LK_ONEWAVE")) c->onewave = atoi(e) != 0;
+    if (const char *e = getenv("PSN_LK_BOX")) c->box = atoi(e) != 0;
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
@@ -426,8 +428,10 @@ int psn_lk_push_frame(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, 
 
 // Validate and plan one query into its device descriptor.
 static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::LkQueryDev &d, int &lds, bool &single,
-                      bool allow_scratch, int &ow_rows, int &ow_lds) {
+                      bool allow_scratch, int &ow_rows, int &ow_lds, int &bx_upt, int &bx_lds) {
     single = false;
+    bx_upt = 0;
+    bx_lds = 0;
     ow_rows = 1 << 30;
     ow_lds = 0;
     const psn_lk_params &p = q.params;
@@ -487,6 +491,17 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     d.dv_jrw4 = psn::div_magic(jrw / 4);
     d.dv_g = psn::div_magic(d.ow_g);
     d.dv_cw = psn::div_magic(nc);
+    {  // box-window kernel: units of 4 pixels, <= kBxMaxUPT per thread
+        const int need = (h * psn::bx_qw(w) + psn::kBxNT - 1) / psn::kBxNT;
+        const psn::BxLayout bl(w, h);
+        if (need <= psn::kBxMaxUPT && bl.total <= psn::kBxMaxLds) {
+            bx_upt = need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : 12;
+            bx_lds = bl.total;
+            psn::bx_tiles(w, h, (p.flags & PSN_LK_ACCUM_SCALAR) == 0, bl.pb, d.bx_tra, d.bx_trb, d.bx_tre);
+            d.dv_bxpm = psn::div_magic(psn::bx_pm(w));
+            d.dv_bxjr = psn::div_magic(psn::bx_jrp(w) / 4);
+        }
+    }
     lds = single ? st.total : psn::lk_lds_bytes(w, h, tr);
     return PSN_LK_OK;
 }
@@ -522,8 +537,8 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         a.err = d_err;
         a.stamps = c->d_stamps;
         a.counts = d_counts;
-        int wgs = 0, lds = 0, maxpx = 0, nqd = 0, rows_ow = 0, lds_ow = 0;
-        bool all_single = true;
+        int wgs = 0, lds = 0, maxpx = 0, nqd = 0, rows_ow = 0, lds_ow = 0, upt_bx = 0, lds_bx = 0;
+        bool all_single = true, all_box = true;
         for (int i = 0; i < n; i++) {
             const psn_lk_query &qq = q[base + i];
             if (qq.num_pts == 0) {
@@ -531,10 +546,13 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                     return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", qq.params.win_w, qq.params.win_h);
                 continue;
             }
-            int l = 0, orows = 0, olds = 0;
+            int l = 0, orows = 0, olds = 0, bupt = 0, blds = 0;
             bool single = false;
-            int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch, orows, olds);
+            int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch, orows, olds, bupt, blds);
             if (rc) return rc;
+            all_box &= bupt > 0;
+            upt_bx = std::max(upt_bx, bupt);
+            lds_bx = std::max(lds_bx, blds);
             a.q[nqd].qidx = base + i;
             all_single &= single;
             rows_ow = std::max(rows_ow, orows);
@@ -588,6 +606,10 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         } else if (c->pend) {
             int rc = flush_pending(c);
             if (rc) return rc;
+        }
+        if (!all_single && all_box && c->box && !c->force_generic && !forced) {
+            HIPCHK(c, psn::launch_lk_bx(a, wgs, upt_bx, lds_bx, c->stream));
+            continue;
         }
         if (!all_single) {  // the generic kernel runs every query of this launch: re-plan its LDS
             lds = 0;

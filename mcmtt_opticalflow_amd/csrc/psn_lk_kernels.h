@@ -47,6 +47,10 @@ struct LkQueryDev {
     unsigned dv_w, dv_dw, dv_pm, dv_jrw, dv_jrw4, dv_g, dv_cw;
     int ow_g, ow_rg;
     int qidx;             // the caller's query index (LkLaunchArgs::counts)
+    // box-window kernel: row tiles of the ordered-chain fallbacks (A, b, err)
+    // and the division magics of its I-patch / J-region dword rows
+    int bx_tra, bx_trb, bx_tre;
+    unsigned dv_bxpm, dv_bxjr;
 };
 __host__ __device__ inline unsigned div_magic(int d) { return d > 0 ? ((1u << 22) + (unsigned)d - 1u) / (unsigned)d : 0u; }
 
@@ -198,6 +202,54 @@ struct LkStLayout {
         }
     }
 };
+// Box-window kernel (lk_kernel_bx, Tracker2D box windows above the single-tile
+// size). The window is cut into UNITS of 4 pixels (row y, quad q: x = 4q..4q+3),
+// QW = ceil(w/4) per row, in row-major order; thread t owns units
+// [t*UPT, t*UPT + UPT). LDS: chain-check scratch | J region (bytes, rows of
+// bx_jrp(w)) | a union of the level's I patch (bytes, rows of bx_pm(w) dwords)
+// and the row-tiled float chain planes of the ordered-sum fallbacks.
+constexpr int kBxNT = 256;
+constexpr int kBxMaxUPT = 12;
+constexpr int kBxRecInts = 3 * 15 + 1;                 // per wave: 15 chains x {total, max, min} + term flag
+constexpr int kBxXInts = 2 * 4 * kBxRecInts;           // two parities x 4 waves
+constexpr int kBxScrBytes = (kBxXInts + 32) * 4 + 64;  // + results / err partials
+constexpr int kBxPlaneMin = 24 * 1024;
+constexpr int kBxMaxLds = 64 * 1024;
+__host__ __device__ inline int bx_qw(int w) { return (w + 3) >> 2; }
+__host__ __device__ inline int bx_pm(int w) { return bx_qw(w) + 2; }      // I patch dwords per row
+__host__ __device__ inline int bx_jrp(int w) { return st_jreg_w(w) + 8; }  // J region row pitch (bytes)
+__host__ __device__ inline int bx_round4(int x) { return (x + 3) & ~3; }
+// One chain region of a fallback plane: n floats rounded to 64, + 4, so the
+// chain bases of one plane start 4 floats apart modulo 64 banks (conflict-free
+// 16-B reads by the chain lanes; a plane is 20 floats mod 64, so up to three
+// planes stay apart too).
+__host__ __device__ inline int bx_region(int n) { return ((n + 63) & ~63) + 4; }
+// floats of one chain-major plane of tr rows: 4 SSE2 lane regions of tr*nq + the tail region
+__host__ __device__ inline int bx_plane(int tr, int nq, int tc) { return 4 * bx_region(tr * nq) + bx_region(tr * tc); }
+struct BxLayout {
+    int jr, un, pb, total;
+    __host__ __device__ BxLayout(int w, int h) {
+        jr = align16(kBxScrBytes);
+        un = jr + align16(st_jreg_h(h) * bx_jrp(w));
+        const int pim = align16((h + 3) * 4 * bx_pm(w));
+        pb = pim > kBxPlaneMin ? pim : kBxPlaneMin;
+        total = un + pb;
+    }
+};
+// Row tiles of the fallback planes within the union (host side): A = 3 planes,
+// b = 2 planes, err = 1 row-major plane.
+inline void bx_tiles(int w, int h, bool sse, int pb, int &tra, int &trb, int &tre) {
+    const int nqa = sse ? w / 4 : 0, ta = w - 4 * nqa;
+    const int nqb = sse ? w / 8 * 2 : 0, tb = w - 4 * nqb;
+    tra = trb = tre = 1;
+    for (int t = h; t >= 1; t--)
+        if (12 * bx_plane(t, nqa, ta) <= pb) { tra = t; break; }
+    for (int t = h; t >= 1; t--)
+        if (8 * bx_plane(t, nqb, tb) <= pb) { trb = t; break; }
+    for (int t = h; t >= 1; t--)
+        if (4 * bx_round4(t * w) <= pb) { tre = t; break; }
+}
+
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel
 constexpr int kStMaxLds = 150 * 1024;
 
@@ -207,6 +259,8 @@ void pyramid_grid(const PyrBuildArgs &a, int &tiles_x, int &tiles_y, int &lds_by
 // threads: tiled kernel = workgroup size; single-tile kernel = NT * 10 + EPT,
 // plus 1000 * E for the one-wave iteration mode (E window rows per lane).
 hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, bool single_tile, hipStream_t s);
+// Box-window kernel with UPT units per thread (4, 8, 10 or 12).
+hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, int lds_bytes, hipStream_t s);
 hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
 
 }  // namespace psn

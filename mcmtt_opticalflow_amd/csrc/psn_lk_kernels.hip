@@ -18,6 +18,7 @@
 // bit-identical to oracle/lk_oracle.c. MFMA is not used: the work is a batch of
 // tiny 2x2 solves, not a contraction.
 #include <float.h>
+#include <limits.h>
 
 #include "psn_lk_kernels.h"
 
@@ -2278,6 +2279,705 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
 #undef PH_MARK
 #undef PH_COUNT
 
+// ---------------------------------------------------------------------------
+// lk_kernel_bx -- box windows (Tracker2D: (int)box.w x (int)box.w backward,
+// PSNWhere_Tracker2D.cpp:776-782; box w x h forward, :871-877) above the
+// single-tile kernel's size. Workgroup = one point, 4 waves. The window is cut
+// into units of 4 pixels (row y, quad q) in row-major order and thread t owns
+// the CONTIGUOUS units [t*UPT, t*UPT + UPT): for every SSE2 lane chain (x & 3,
+// pixels below the 8- resp. 4-pixel-step bound) and the scalar tail chain the
+// thread's terms are one contiguous run of the chain, in chain order. Window
+// values (256 - 512 I, Ix, Iy) stay in registers for the whole level; the I
+// patch and the J region are LDS bytes (J pairs for the packed-dot bilinear are
+// formed with v_perm from two dwords per row).
+// Exactness of every float sum (A11, A12, A22 per level; b1, b2 per iteration),
+// decided per chain: a run's total and its maximum / minimum prefix go through
+// a block scan (DPP within a wave, one LDS record per wave, ONE barrier); when
+// every prefix of every chain is an integer of magnitude <= 2^24 and every term
+// is exact, each chain's float sum IS its integer sum and the chains combine in
+// float in the SSE2 build's order. Otherwise the ordered float chains: terms
+// chain-major into LDS planes, row tile by row tile, one lane per chain.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_max_i(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xa, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Publish this wave's part of NC chains (per-lane run total T, maximum prefix M
+// >= 0 and minimum prefix m <= 0, prefixes relative to the run start): the
+// wave's chain total and its extreme prefixes relative to the wave's start.
+// int32 is enough: a run holds <= 48 terms < 2^25, and any wrap happens only
+// past a prefix that already fails the 2^24 bound.
+template <int NC>
+__device__ __forceinline__ void bx_publish(const int (&T)[NC], const int (&M)[NC], const int (&m)[NC], bool bad,
+                                           int *rec) {
+    const int lane = threadIdx.x & 63;
+    int *xw = rec + (threadIdx.x >> 6) * kBxRecInts;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const int incl = wave_scan(T[c]);
+        const int ex = incl - T[c];
+        const int hi = wave_max_i(ex + M[c]);
+        const int lo = wave_min_i(ex + m[c]);
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        if (lane == 0) {
+            xw[3 * c] = tot;
+            xw[3 * c + 1] = hi;
+            xw[3 * c + 2] = lo;
+        }
+    }
+    const bool anybad = __ballot(bad) != 0ull;
+    if (lane == 0) xw[3 * 15] = anybad ? 1 : 0;
+}
+// After the barrier: lane c < NC checks chain c over the 4 waves' records and
+// returns its total; the wave-uniform verdict is "no lane failed".
+template <int NC>
+__device__ __forceinline__ bool bx_eval(const int *rec, int &total) {
+    const int lane = threadIdx.x & 63;
+    bool ok = true;
+    long long base = 0;
+    const int c = lane < NC ? lane : 0;
+#pragma unroll
+    for (int wv = 0; wv < 4; wv++) {
+        const int *xw = rec + wv * kBxRecInts;
+        const int tot = xw[3 * c], hi = xw[3 * c + 1], lo = xw[3 * c + 2], bad = xw[3 * 15];
+        ok &= (base + hi <= (long long)kExact) & (base + lo >= -(long long)kExact) & (bad == 0);
+        base += tot;
+    }
+    ok |= lane >= NC;
+    total = (int)base;
+    return __ballot(!ok) == 0ull;
+}
+__device__ __forceinline__ float rl_f(int v, int lane) { return (float)__builtin_amdgcn_readlane(v, lane); }
+
+// chain-run update with one term
+__device__ __forceinline__ void run_add(int &T, int &M, int &m, int t) {
+    T += t;
+    M = max(M, T);
+    m = min(m, T);
+}
+
+__device__ __forceinline__ int lo16(unsigned v) { return (int)(short)(v & 0xffffu); }
+__device__ __forceinline__ int hi16(unsigned v) { return (int)v >> 16; }
+// J - I of one unit (4 pixels) from the byte J region: rows jp and jp + JRP4
+// (dwords), pairs selected by the uniform v_perm selectors s0..s3, packed-dot
+// bilinear with the diff folded into the accumulator constant 256 - 512 I
+// (I = the unit's window values, packed pairs ip).
+__device__ __forceinline__ void bx_diffs(const uint32_t *jp, int JRP4, unsigned W0, unsigned W1, unsigned s0,
+                                         unsigned s1, unsigned s2, unsigned s3, const unsigned (&ip)[2], int (&d)[4]) {
+    const uint32_t a0 = jp[0], a1 = jp[1], b0 = jp[JRP4], b1 = jp[JRP4 + 1];
+    const int cw[4] = {256 - 512 * lo16(ip[0]), 256 - 512 * hi16(ip[0]), 256 - 512 * lo16(ip[1]), 256 - 512 * hi16(ip[1])};
+    d[0] = sdot2(__builtin_amdgcn_perm(b1, b0, s0), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s0), W0, cw[0])) >> 9;
+    d[1] = sdot2(__builtin_amdgcn_perm(b1, b0, s1), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s1), W0, cw[1])) >> 9;
+    d[2] = sdot2(__builtin_amdgcn_perm(b1, b0, s2), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s2), W0, cw[2])) >> 9;
+    d[3] = sdot2(__builtin_amdgcn_perm(b1, b0, s3), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s3), W0, cw[3])) >> 9;
+}
+// pair selector: bytes (sj + i, sj + i + 1) of a row's 8-byte window -> J[x] | J[x+1] << 16
+__device__ __forceinline__ unsigned bx_sel(int sj, int i) {
+    return 0x0c000c00u | ((unsigned)(sj + i + 1) << 16) | (unsigned)(sj + i);
+}
+
+// Ordered float sum of `len` LDS floats (16-B aligned) onto acc: 16 floats per
+// step with the next two 16-float blocks already in flight, so the LDS latency
+// hides behind the dependent adds (the lanes of a wave sum different chains).
+__device__ __forceinline__ float chain_sum_pl(const float *p, int len, float acc) {
+    const float4 *q = (const float4 *)p;
+    const int nb = len >> 4;
+    if (nb > 0) {
+        float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+        const int b1 = min(1, nb - 1);
+        float4 c0 = q[4 * b1], c1 = q[4 * b1 + 1], c2 = q[4 * b1 + 2], c3 = q[4 * b1 + 3];
+        for (int b = 0; b < nb; b++) {
+            const int bn = min(b + 2, nb - 1);  // in-bounds prefetch (the last blocks re-read)
+            const float4 e0 = q[4 * bn], e1 = q[4 * bn + 1], e2 = q[4 * bn + 2], e3 = q[4 * bn + 3];
+            acc = add16(acc, a0, a1, a2, a3);
+            a0 = c0, a1 = c1, a2 = c2, a3 = c3;
+            c0 = e0, c1 = e1, c2 = e2, c3 = e3;
+        }
+    }
+    for (int i = nb * 16; i < len; i++) acc = acc + p[i];
+    return acc;
+}
+
+template <int UPT>
+__global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int NT = kBxNT;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int g = blockIdx.x;
+    int qi = 0;
+    while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
+    const LkQueryDev &Q = A.q[qi];
+    if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) return;  // past the query's device count
+    const int pi = Q.pt_begin + (g - Q.wg_begin);
+    const int w = Q.win_w, h = Q.win_h;
+    const int maxL = Q.max_level, flags = Q.flags;
+    const bool sse = (flags & PSN_LK_ACCUM_SCALAR) == 0;
+    const int QW = bx_qw(w), U = h * QW;
+    const int nqB = sse ? (w / 8) * 2 : 0, n8 = 4 * nqB, tB = w - n8;   // b: 8-pixel steps
+    const int nqA = sse ? w / 4 : 0, nA4 = 4 * nqA, tA = w - nA4;        // A: 4-pixel steps
+    const int PM = bx_pm(w), JRW = st_jreg_w(w), JRH = st_jreg_h(h), JRP = bx_jrp(w), JRP4 = JRP >> 2;
+    const BxLayout lay(w, h);
+    int *X = (int *)smem;                      // chain-check records, two parities
+    float *RS = (float *)(X + kBxXInts);       // serial-chain results (wave 0 -> all)
+    int *EP = (int *)(RS + 16);                // err partial sums per wave
+    uint8_t *JR = smem + lay.jr;
+    const uint32_t *JR32 = (const uint32_t *)JR;
+    uint8_t *UN = smem + lay.un;
+    const uint32_t *P32 = (const uint32_t *)UN;
+    float *PL = (float *)UN;
+
+    const int u0 = tid * UPT;
+    const int y0 = u0 / QW, q0 = u0 - y0 * QW;
+
+    const float hwx = __fmul_rn((float)(w - 1), 0.5f), hwy = __fmul_rn((float)(h - 1), 0.5f);
+    const float px0 = A.prev[2 * pi], py0 = A.prev[2 * pi + 1];
+    float NPx = 0.f, NPy = 0.f;
+    if (flags & PSN_LK_USE_INITIAL_FLOW) {
+        NPx = A.next[2 * pi];
+        NPy = A.next[2 * pi + 1];
+    }
+    int status = 1;
+    float errv = 0.f;
+    const float FLT_SCALE = 1.f / (1 << 20);
+    int par = 0;
+
+    unsigned IP[UPT][2], XP[UPT][2], YP[UPT][2];  // I, Ix, Iy as packed 16-bit pairs (pixels 0,1 and 2,3)
+    int gmax = 0;              // max |Ix|, |Iy| of the thread's pixels
+
+    for (int level = maxL; level >= 0; level--) {
+        const LevelDev I = ring_level_u(A.ring, Q.prev_slot, level);
+        const LevelDev J = ring_level_u(A.ring, Q.next_slot, level);
+        const int cols = I.w, rows = I.h;
+        const float scale = ldexpf(1.f, -level);
+        float px = __fmul_rn(px0, scale), py = __fmul_rn(py0, scale);
+        float nx, ny;
+        if (level == maxL) {
+            if (flags & PSN_LK_USE_INITIAL_FLOW) {
+                nx = __fmul_rn(NPx, scale);
+                ny = __fmul_rn(NPy, scale);
+            } else {
+                nx = px;
+                ny = py;
+            }
+        } else {
+            nx = __fmul_rn(NPx, 2.f);
+            ny = __fmul_rn(NPy, 2.f);
+        }
+        NPx = nx;
+        NPy = ny;
+        px = __fsub_rn(px, hwx);
+        py = __fsub_rn(py, hwy);
+        const int ipx = cv_floor(px), ipy = cv_floor(py);
+        if (ipx < -w || ipx >= cols || ipy < -h || ipy >= rows) {
+            if (level == 0) {
+                status = 0;
+                errv = 0.f;
+            }
+            continue;
+        }
+        int iw00, iw01, iw10, iw11;
+        bilin_weights(__fsub_rn(px, (float)ipx), __fsub_rn(py, (float)ipy), iw00, iw01, iw10, iw11);
+        nx = __fsub_rn(nx, hwx);
+        ny = __fsub_rn(ny, hwy);
+        int jr_x0 = (cv_floor(nx) - kStJMargin) & ~3, jr_y0 = cv_floor(ny) - kStJMargin;
+
+        __syncthreads();  // the previous level is done with LDS
+        dma_patch<NT>(UN, I, ipy - 1, ipx - 1, w + 3, h + 3, PM, Q.dv_bxpm);
+        dma_patch<NT>(JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
+        dma_wait();
+        __syncthreads();
+
+        // ---- A phase: Scharr + bilinear window values of the thread's units from
+        // the I patch bytes; the 15 A chains (sum x class) as runs ----
+        float A11, A12, A22;
+        {
+            const int sh = (ipx - 1) & 3;
+            int T11[5] = {0, 0, 0, 0, 0}, T22[5] = {0, 0, 0, 0, 0}, T12[5] = {0, 0, 0, 0, 0};
+            int M12[5] = {0, 0, 0, 0, 0}, m12[5] = {0, 0, 0, 0, 0};
+            gmax = 0;
+            int y = y0, q = q0;
+            asm volatile("" : "+v"(y), "+v"(q));  // opaque: no per-unit address hoisting (VGPRs)
+#pragma unroll
+            for (int k = 0; k < UPT; k++) {
+                const bool uv = u0 + k < U;
+                const int yy = uv ? y : 0, qq = uv ? q : 0;
+                int B[4][7];
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const uint32_t *p = P32 + (yy + r) * PM + qq;
+                    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+                    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                    B[r][0] = lo & 255;
+                    B[r][1] = (lo >> 8) & 255;
+                    B[r][2] = (lo >> 16) & 255;
+                    B[r][3] = lo >> 24;
+                    B[r][4] = hi & 255;
+                    B[r][5] = (hi >> 8) & 255;
+                    B[r][6] = (hi >> 16) & 255;
+                }
+                int DX[2][5], DY[2][5];
+#pragma unroll
+                for (int o = 0; o < 2; o++) {
+                    const bool rin = (unsigned)(ipy + yy + o) < (unsigned)rows;
+                    int sv[7], dv[7];
+#pragma unroll
+                    for (int j = 0; j < 7; j++) {
+                        sv[j] = 3 * (B[o][j] + B[o + 2][j]) + 10 * B[o + 1][j];
+                        dv[j] = B[o + 2][j] - B[o][j];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 5; j++) {
+                        // zero outside the image; branch-free (a select per value keeps the
+                        // unit one basic block)
+                        const int msk = -(int)(rin & ((unsigned)(ipx + 4 * qq + j) < (unsigned)cols));
+                        DX[o][j] = (sv[j + 2] - sv[j]) & msk;
+                        DY[o][j] = (3 * (dv[j] + dv[j + 2]) + 10 * dv[j + 1]) & msk;
+                    }
+                }
+                int ix[4], iy[4], iv[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const bool pv = uv && 4 * qq + i < w;
+                    iv[i] = PSN_DESCALE(__mul24(B[1][i + 1], iw00) + __mul24(B[1][i + 2], iw01) +
+                                                   __mul24(B[2][i + 1], iw10) + __mul24(B[2][i + 2], iw11), 9);
+                    const int gx = PSN_DESCALE(__mul24(DX[0][i], iw00) + __mul24(DX[0][i + 1], iw01) +
+                                                   __mul24(DX[1][i], iw10) + __mul24(DX[1][i + 1], iw11), 14);
+                    const int gy = PSN_DESCALE(__mul24(DY[0][i], iw00) + __mul24(DY[0][i + 1], iw01) +
+                                                   __mul24(DY[1][i], iw10) + __mul24(DY[1][i + 1], iw11), 14);
+                    ix[i] = gx & -(int)pv;
+                    iy[i] = gy & -(int)pv;
+                    gmax = max(gmax, max(abs(ix[i]), abs(iy[i])));
+                }
+                IP[k][0] = pack_w(iv[0], iv[1]);
+                IP[k][1] = pack_w(iv[2], iv[3]);
+                XP[k][0] = pack_w(ix[0], ix[1]);
+                XP[k][1] = pack_w(ix[2], ix[3]);
+                YP[k][0] = pack_w(iy[0], iy[1]);
+                YP[k][1] = pack_w(iy[2], iy[3]);
+                // materialize the unit's results here: no sinking of its arithmetic
+                // past later units (which would keep its patch bytes live)
+                asm volatile("" : "+v"(IP[k][0]), "+v"(IP[k][1]), "+v"(XP[k][0]), "+v"(XP[k][1]), "+v"(YP[k][0]),
+                             "+v"(YP[k][1]), "+v"(gmax));
+                if (++q == QW) {
+                    q = 0;
+                    y++;
+                }
+                __builtin_amdgcn_sched_barrier(0);  // one unit at a time (register pressure)
+            }
+            // A products of the window values, unit by unit (a second pass keeps
+            // the Scharr temporaries and the chain runs apart)
+            q = q0;
+            asm volatile("" : "+v"(q));
+#pragma unroll
+            for (int k = 0; k < UPT; k++) {
+                const bool sA = q < nqA;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int gx = (i & 1) ? hi16(XP[k][i >> 1]) : lo16(XP[k][i >> 1]);
+                    const int gy = (i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]);
+                    // SSE2 unit: pixel i feeds lane chain i; else the tail chain, row-major
+                    // (branch-free: the other chain gets a zero term)
+                    const int ms = -(int)sA;
+                    const int xx = __mul24(gx, gx), yy2 = __mul24(gy, gy), xy = __mul24(gx, gy);
+                    T11[i] += xx & ms;
+                    T22[i] += yy2 & ms;
+                    run_add(T12[i], M12[i], m12[i], xy & ms);
+                    T11[4] += xx & ~ms;
+                    T22[4] += yy2 & ~ms;
+                    run_add(T12[4], M12[4], m12[4], xy & ~ms);
+                }
+                if (++q == QW) q = 0;
+                asm volatile("" : "+v"(T11[0]), "+v"(T11[1]), "+v"(T11[2]), "+v"(T11[3]), "+v"(T11[4]), "+v"(T22[0]),
+                             "+v"(T22[1]), "+v"(T22[2]), "+v"(T22[3]), "+v"(T22[4]));
+                asm volatile("" : "+v"(T12[0]), "+v"(T12[1]), "+v"(T12[2]), "+v"(T12[3]), "+v"(T12[4]), "+v"(M12[0]),
+                             "+v"(M12[1]), "+v"(M12[2]), "+v"(M12[3]), "+v"(M12[4]));
+                asm volatile("" : "+v"(m12[0]), "+v"(m12[1]), "+v"(m12[2]), "+v"(m12[3]), "+v"(m12[4]));
+            }
+            // A11 / A22 terms are >= 0: the maximum prefix is the total
+            int T[15], M[15], m[15];
+#pragma unroll
+            for (int c = 0; c < 5; c++) {
+                T[c] = T11[c], M[c] = T11[c], m[c] = 0;
+                T[5 + c] = T12[c], M[5 + c] = M12[c], m[5 + c] = m12[c];
+                T[10 + c] = T22[c], M[10 + c] = T22[c], m[10 + c] = 0;
+            }
+            int *rec = X + par * 4 * kBxRecInts;
+            par ^= 1;
+            bx_publish<15>(T, M, m, false, rec);
+            __syncthreads();
+            int tot;
+            const bool exact = bx_eval<15>(rec, tot);
+            float s3[3];
+            if (exact) {
+#pragma unroll
+                for (int s = 0; s < 3; s++) {
+                    float t = rl_f(tot, 5 * s + 4);
+                    if (sse)
+                        t = __fadd_rn(t, __fadd_rn(__fadd_rn(__fadd_rn(rl_f(tot, 5 * s), rl_f(tot, 5 * s + 1)),
+                                                             rl_f(tot, 5 * s + 2)), rl_f(tot, 5 * s + 3)));
+                    s3[s] = t;
+                }
+            } else {
+                // ordered float chains: products chain-major into 3 planes per row tile
+                const int TR = Q.bx_tra;
+                float acc = 0.f;
+                for (int r0 = 0; r0 < h; r0 += TR) {
+                    const int tr = min(TR, h - r0);
+                    const int S = bx_region(tr * nqA), P = bx_plane(tr, nqA, tA);
+                    __syncthreads();  // the patch / previous tile is consumed
+                    int yk = y0, qk = q0;
+                    asm volatile("" : "+v"(yk), "+v"(qk));
+#pragma unroll
+                    for (int k = 0; k < UPT; k++) {
+                        if (u0 + k < U && yk >= r0 && yk < r0 + tr) {
+                            unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
+                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));  // no hoisting out of the tile loop
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int x = 4 * qk + i;
+                                if (x < w) {
+                                    const int gx = ((i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]));
+                                    const int gy = ((i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]));
+                                    const int pos = qk < nqA ? i * S + (yk - r0) * nqA + qk : 4 * S + (yk - r0) * tA + (x - nA4);
+                                    PL[pos] = (float)__mul24(gx, gx);
+                                    PL[P + pos] = (float)__mul24(gx, gy);
+                                    PL[2 * P + pos] = (float)__mul24(gy, gy);
+                                }
+                            }
+                        }
+                        if (++qk == QW) {
+                            qk = 0;
+                            yk++;
+                        }
+                    }
+                    __syncthreads();
+                    if (tid < 15) {
+                        const int s = tid / 5, c = tid - 5 * s;
+                        acc = chain_sum_pl(PL + s * P + c * S, c < 4 ? tr * nqA : tr * tA, acc);
+                    }
+                }
+                if (tid < 64) {
+                    const int a = __float_as_int(acc);
+#pragma unroll
+                    for (int s = 0; s < 3; s++) {
+                        float t = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 4));
+                        if (sse) {
+                            const float c0 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s));
+                            const float c1 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 1));
+                            const float c2 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 2));
+                            const float c3 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 3));
+                            t = __fadd_rn(t, __fadd_rn(__fadd_rn(__fadd_rn(c0, c1), c2), c3));
+                        }
+                        if (tid == 0) RS[s] = t;
+                    }
+                }
+                __syncthreads();
+                s3[0] = RS[0];
+                s3[1] = RS[1];
+                s3[2] = RS[2];
+            }
+            A11 = __fmul_rn(s3[0], FLT_SCALE);
+            A12 = __fmul_rn(s3[1], FLT_SCALE);
+            A22 = __fmul_rn(s3[2], FLT_SCALE);
+        }
+        float D = __fsub_rn(__fmul_rn(A11, A22), __fmul_rn(A12, A12));
+        {
+            const float dd = __fsub_rn(A11, A22);
+            const float t = __fadd_rn(__fmul_rn(dd, dd), __fmul_rn(__fmul_rn(4.f, A12), A12));
+            const float minEig = __fdiv_rn(__fsub_rn(__fadd_rn(A22, A11), sqrtf(t)), (float)(2 * w * h));
+            if (flags & PSN_LK_GET_MIN_EIGENVALS) errv = minEig;
+            if (minEig < Q.min_eig || D < FLT_EPSILON) {
+                if (level == 0) status = 0;
+                continue;
+            }
+        }
+        D = __fdiv_rn(1.f, D);
+
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < Q.max_count; j++) {
+            const int inx = cv_floor(nx), iny = cv_floor(ny);
+            if (inx < -w || inx >= cols || iny < -h || iny >= rows) {
+                if (level == 0) status = 0;
+                break;
+            }
+            int w00, w01, w10, w11;
+            bilin_weights(__fsub_rn(nx, (float)inx), __fsub_rn(ny, (float)iny), w00, w01, w10, w11);
+            if (!(inx >= jr_x0 && iny >= jr_y0 && inx + w + 1 <= jr_x0 + JRW && iny + h + 1 <= jr_y0 + JRH)) {
+                // every wave's J reads of the previous iteration precede its barrier
+                jr_x0 = (inx - kStJMargin) & ~3;
+                jr_y0 = iny - kStJMargin;
+                dma_patch<NT>(JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
+                dma_wait();
+                __syncthreads();
+            }
+            const unsigned W0 = pack_w(w00, w01), W1 = pack_w(w10, w11);
+            const int ox = inx - jr_x0, oy = iny - jr_y0, sj = ox & 3;
+            const unsigned s0 = bx_sel(sj, 0), s1 = bx_sel(sj, 1), s2 = bx_sel(sj, 2), s3 = bx_sel(sj, 3);
+            int T1[5] = {0, 0, 0, 0, 0}, M1[5] = {0, 0, 0, 0, 0}, m1[5] = {0, 0, 0, 0, 0};
+            int T2[5] = {0, 0, 0, 0, 0}, M2[5] = {0, 0, 0, 0, 0}, m2[5] = {0, 0, 0, 0, 0};
+            int dmax = 0;
+            {
+                int y = y0, q = q0;
+            asm volatile("" : "+v"(y), "+v"(q));  // opaque: no per-unit address hoisting (VGPRs)
+#pragma unroll
+                for (int k = 0; k < UPT; k++) {
+                    const bool uv = u0 + k < U;
+                    int d[4];
+                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+                    int t1[4], t2[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const int gx = ((i & 1) ? hi16(XP[k][i >> 1]) : lo16(XP[k][i >> 1]));
+                        const int gy = ((i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]));
+                        t1[i] = __mul24(d[i], gx);
+                        t2[i] = __mul24(d[i], gy);
+                        dmax = max(dmax, abs(d[i]));
+                    }
+                    // SSE2 unit -> lane chains 0-3, else the tail chain (branch-free)
+                    const int ms = -(int)(q < nqB);
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        run_add(T1[i], M1[i], m1[i], t1[i] & ms);
+                        run_add(T2[i], M2[i], m2[i], t2[i] & ms);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        run_add(T1[4], M1[4], m1[4], t1[i] & ~ms);
+                        run_add(T2[4], M2[4], m2[4], t2[i] & ~ms);
+                    }
+                    if (++q == QW) {
+                        q = 0;
+                        y++;
+                    }
+                    // materialize the runs per unit (no sinking across units)
+                    asm volatile("" : "+v"(T1[0]), "+v"(T1[1]), "+v"(T1[2]), "+v"(T1[3]), "+v"(T1[4]), "+v"(M1[0]),
+                                 "+v"(M1[1]), "+v"(M1[2]), "+v"(M1[3]), "+v"(M1[4]));
+                    asm volatile("" : "+v"(m1[0]), "+v"(m1[1]), "+v"(m1[2]), "+v"(m1[3]), "+v"(m1[4]), "+v"(T2[0]),
+                                 "+v"(T2[1]), "+v"(T2[2]), "+v"(T2[3]), "+v"(T2[4]));
+                    asm volatile("" : "+v"(M2[0]), "+v"(M2[1]), "+v"(M2[2]), "+v"(M2[3]), "+v"(M2[4]), "+v"(m2[0]),
+                                 "+v"(m2[1]), "+v"(m2[2]), "+v"(m2[3]), "+v"(m2[4]), "+v"(dmax));
+                }
+            }
+            // masked pixels carry zero gradients but any d: only real terms count
+            const bool bad = (long long)dmax * gmax > (long long)kExact;
+            int T[10], M[10], m[10];
+#pragma unroll
+            for (int c = 0; c < 5; c++) {
+                T[c] = T1[c], M[c] = M1[c], m[c] = m1[c];
+                T[5 + c] = T2[c], M[5 + c] = M2[c], m[5 + c] = m2[c];
+            }
+            int *rec = X + par * 4 * kBxRecInts;
+            par ^= 1;
+            bx_publish<10>(T, M, m, bad, rec);
+            __syncthreads();
+            int tot;
+            float b1, b2;
+            if (bx_eval<10>(rec, tot)) {
+                b1 = rl_f(tot, 4);
+                b2 = rl_f(tot, 9);
+                if (sse) {
+                    b1 = __fadd_rn(b1, __fadd_rn(__fadd_rn(rl_f(tot, 0), rl_f(tot, 2)), __fadd_rn(rl_f(tot, 1), rl_f(tot, 3))));
+                    b2 = __fadd_rn(b2, __fadd_rn(__fadd_rn(rl_f(tot, 5), rl_f(tot, 7)), __fadd_rn(rl_f(tot, 6), rl_f(tot, 8))));
+                }
+            } else {
+                // ordered float chains, row tiles of 2 planes, lanes 0-9 of wave 0
+                const int TR = Q.bx_trb;
+                float acc = 0.f;
+                for (int r0 = 0; r0 < h; r0 += TR) {
+                    const int tr = min(TR, h - r0);
+                    const int S = bx_region(tr * nqB), P = bx_plane(tr, nqB, tB);
+                    __syncthreads();  // previous tile consumed
+                    int yk = y0, qk = q0;
+                    asm volatile("" : "+v"(yk), "+v"(qk));
+#pragma unroll
+                    for (int k = 0; k < UPT; k++) {
+                        if (u0 + k < U && yk >= r0 && yk < r0 + tr) {
+                            int d[4];
+                            bx_diffs(JR32 + (oy + (yk)) * JRP4 + (ox >> 2) + (qk), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+                            unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
+                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int x = 4 * qk + i;
+                                if (x < w) {
+                                    const int gx = ((i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]));
+                                    const int gy = ((i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]));
+                                    const int pos = qk < nqB ? i * S + (yk - r0) * nqB + qk : 4 * S + (yk - r0) * tB + (x - n8);
+                                    PL[pos] = (float)__mul24(d[i], gx);
+                                    PL[P + pos] = (float)__mul24(d[i], gy);
+                                }
+                            }
+                        }
+                        if (++qk == QW) {
+                            qk = 0;
+                            yk++;
+                        }
+                    }
+                    __syncthreads();
+                    if (tid < 10) {
+                        const int s = tid / 5, c = tid - 5 * s;
+                        acc = chain_sum_pl(PL + s * P + c * S, c < 4 ? tr * nqB : tr * tB, acc);
+                    }
+                }
+                if (tid < 64) {
+                    const int a = __float_as_int(acc);
+                    float r1 = __int_as_float(__builtin_amdgcn_readlane(a, 4));
+                    float r2 = __int_as_float(__builtin_amdgcn_readlane(a, 9));
+                    if (sse) {
+                        const float bb0 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 0)),
+                                                    __int_as_float(__builtin_amdgcn_readlane(a, 2)));
+                        const float bb2 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 1)),
+                                                    __int_as_float(__builtin_amdgcn_readlane(a, 3)));
+                        const float bb1 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 5)),
+                                                    __int_as_float(__builtin_amdgcn_readlane(a, 7)));
+                        const float bb3 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 6)),
+                                                    __int_as_float(__builtin_amdgcn_readlane(a, 8)));
+                        r1 = __fadd_rn(r1, __fadd_rn(bb0, bb2));
+                        r2 = __fadd_rn(r2, __fadd_rn(bb1, bb3));
+                    }
+                    if (tid == 0) {
+                        RS[4] = r1;
+                        RS[5] = r2;
+                    }
+                }
+                __syncthreads();
+                b1 = RS[4];
+                b2 = RS[5];
+            }
+            b1 = __fmul_rn(b1, FLT_SCALE);
+            b2 = __fmul_rn(b2, FLT_SCALE);
+            const float dx = __fmul_rn(__fsub_rn(__fmul_rn(A12, b2), __fmul_rn(A22, b1)), D);
+            const float dy = __fmul_rn(__fsub_rn(__fmul_rn(A12, b1), __fmul_rn(A11, b2)), D);
+            nx = __fadd_rn(nx, dx);
+            ny = __fadd_rn(ny, dy);
+            NPx = __fadd_rn(nx, hwx);
+            NPy = __fadd_rn(ny, hwy);
+            const double dd = __dadd_rn(__dmul_rn((double)dx, (double)dx), __dmul_rn((double)dy, (double)dy));
+            if (dd <= Q.eps2) break;
+            if (j > 0 && (double)fabsf(__fadd_rn(dx, pdx)) < 0.01 && (double)fabsf(__fadd_rn(dy, pdy)) < 0.01) {
+                NPx = __fsub_rn(NPx, __fmul_rn(dx, 0.5f));
+                NPy = __fsub_rn(NPy, __fmul_rn(dy, 0.5f));
+                break;
+            }
+            pdx = dx;
+            pdy = dy;
+        }
+
+        if (level == 0 && status && A.err && (flags & PSN_LK_GET_MIN_EIGENVALS) == 0) {
+            const float qx = __fsub_rn(NPx, hwx), qy = __fsub_rn(NPy, hwy);
+            const int iqx = cv_floor(qx), iqy = cv_floor(qy);
+            if (iqx < -w || iqx >= cols || iqy < -h || iqy >= rows) {
+                status = 0;
+                continue;
+            }
+            int w00, w01, w10, w11;
+            bilin_weights(__fsub_rn(qx, (float)iqx), __fsub_rn(qy, (float)iqy), w00, w01, w10, w11);
+            if (!(iqx >= jr_x0 && iqy >= jr_y0 && iqx + w + 1 <= jr_x0 + JRW && iqy + h + 1 <= jr_y0 + JRH)) {
+                __syncthreads();  // a serial b pass may still read nothing of JR, but be safe
+                jr_x0 = (iqx - kStJMargin) & ~3;
+                jr_y0 = iqy - kStJMargin;
+                dma_patch<NT>(JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
+                dma_wait();
+                __syncthreads();
+            }
+            const unsigned W0 = pack_w(w00, w01), W1 = pack_w(w10, w11);
+            const int ox = iqx - jr_x0, oy = iqy - jr_y0, sj = ox & 3;
+            const unsigned s0 = bx_sel(sj, 0), s1 = bx_sel(sj, 1), s2 = bx_sel(sj, 2), s3 = bx_sel(sj, 3);
+            unsigned e = 0;
+            {
+                int y = y0, q = q0;
+            asm volatile("" : "+v"(y), "+v"(q));  // opaque: no per-unit address hoisting (VGPRs)
+#pragma unroll
+                for (int k = 0; k < UPT; k++) {
+                    const bool uv = u0 + k < U;
+                    int d[4];
+                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (uv && 4 * q + i < w) e += (unsigned)abs(d[i]);
+                    if (++q == QW) {
+                        q = 0;
+                        y++;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // one unit at a time (register pressure)
+                }
+            }
+            e = (unsigned)wave_sum((int)e);  // <= 64 * 48 * 8160 < 2^31
+            if (lane == 0) EP[tid >> 6] = (int)e;
+            __syncthreads();
+            const unsigned et = (unsigned)EP[0] + (unsigned)EP[1] + (unsigned)EP[2] + (unsigned)EP[3];
+            float errval;
+            if (et <= (unsigned)kExact) {
+                errval = (float)et;  // every partial sum of errval += |diff| is an exact integer
+            } else {  // row-major order, one lane, row tiles
+                const int TR = Q.bx_tre;
+                float acc = 0.f;
+                for (int r0 = 0; r0 < h; r0 += TR) {
+                    const int tr = min(TR, h - r0);
+                    __syncthreads();
+                    int yk = y0, qk = q0;
+                    asm volatile("" : "+v"(yk), "+v"(qk));
+#pragma unroll
+                    for (int k = 0; k < UPT; k++) {
+                        if (u0 + k < U && yk >= r0 && yk < r0 + tr) {
+                            int d[4];
+                            bx_diffs(JR32 + (oy + (yk)) * JRP4 + (ox >> 2) + (qk), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+#pragma unroll
+                            for (int i = 0; i < 4; i++)
+                                if (4 * qk + i < w) PL[(yk - r0) * w + 4 * qk + i] = (float)abs(d[i]);
+                        }
+                        if (++qk == QW) {
+                            qk = 0;
+                            yk++;
+                        }
+                    }
+                    __syncthreads();
+                    if (tid == 0) acc = chain_sum_pl(PL, tr * w, acc);
+                }
+                if (tid == 0) RS[8] = acc;
+                __syncthreads();
+                errval = RS[8];
+            }
+            errv = __fdiv_rn(__fmul_rn(errval, 1.f), (float)(32 * w * h));
+        }
+    }
+
+    if (tid == 0) {
+        A.next[2 * pi] = NPx;
+        A.next[2 * pi + 1] = NPy;
+        A.status[pi] = (uint8_t)status;
+        if (A.err) A.err[pi] = errv;
+    }
+}
+
+hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, int lds_bytes, hipStream_t s) {
+    if (total_wgs <= 0) return hipSuccess;
+    const dim3 grid(total_wgs), block(kBxNT);
+    switch (upt) {
+        case 4: hipLaunchKernelGGL(lk_kernel_bx<4>, grid, block, lds_bytes, s, a); break;
+        case 8: hipLaunchKernelGGL(lk_kernel_bx<8>, grid, block, lds_bytes, s, a); break;
+        case 10: hipLaunchKernelGGL(lk_kernel_bx<10>, grid, block, lds_bytes, s, a); break;
+        case 12: hipLaunchKernelGGL(lk_kernel_bx<12>, grid, block, lds_bytes, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, bool single_tile, hipStream_t s) {
     if (total_wgs <= 0) return hipSuccess;
     const dim3 grid(total_wgs);
@@ -2333,6 +3033,10 @@ hipError_t lk_kernels_init() {
     for (const void *f : st)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)pyramid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
+    const void *bx[] = {(const void *)lk_kernel_bx<4>, (const void *)lk_kernel_bx<8>, (const void *)lk_kernel_bx<10>,
+                        (const void *)lk_kernel_bx<12>};
+    for (const void *f : bx)
+        if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     return hipSuccess;
 }
 

@@ -342,3 +342,21 @@ def test_lk_counted_launch(oracle_mod, win):
             assert_same((g_n[lo:lo + c], g_s[lo:lo + c], g_e[lo:lo + c]), ref, f"query {i}")
         np.testing.assert_array_equal(g_n[lo + c:lo + 50], sentinel[lo + c:lo + 50])
         assert (g_s[lo + c:lo + 50] == 9).all()
+
+
+@pytest.mark.parametrize("kernel", ["box", "tiled"])
+@pytest.mark.parametrize("win,flags", [((33, 33), 0), ((37, 50), 0), ((70, 45), 0), ((66, 100), 0), ((45, 120), 0),
+                                       ((64, 160), 0), ((96, 128), 0), ((64, 64), ACCUM_SCALAR),
+                                       ((45, 120), ACCUM_SCALAR), ((64, 64), GET_MIN_EIGENVALS)])
+def test_lk_box_kernel_windows(oracle_mod, monkeypatch, kernel, win, flags):
+    """Box windows above the single-tile size: lk_kernel_bx (units of 4 pixels,
+    per-chain prefix exactness) and the row-tiled kernel (PSN_LK_BOX=0) against
+    the oracle -- SSE2 tails (w % 8), partial quads (w % 4), the scalar build,
+    border points."""
+    monkeypatch.setenv("PSN_LK_BOX", "1" if kernel == "box" else "0")
+    sc, f0, f1 = scene_pair(6, 1920, 1080, 40)
+    pts = np.concatenate([sc.points_at(0), np.array([[3, 4], [1915.5, 1077.25], [-20, 500], [960, 1079.5]],
+                                                     np.float32)])
+    ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
+    assert_same(gpu, ref, f"{kernel} win {win} flags {flags}")
