@@ -493,11 +493,12 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     d.dv_cw = psn::div_magic(nc);
     {  // box-window kernel: units of 4 pixels, <= kBxMaxUPT per thread
         const int need = (h * psn::bx_qw(w) + psn::kBxNT - 1) / psn::kBxNT;
-        const psn::BxLayout bl(w, h);
+        const int upt = need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : 12;
+        const psn::BxLayout bl(w, h, psn::kBxMaxUPT);  // the launch may run a larger UPT
         if (need <= psn::kBxMaxUPT && bl.total <= psn::kBxMaxLds) {
-            bx_upt = need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : 12;
+            bx_upt = upt;
             bx_lds = bl.total;
-            psn::bx_tiles(w, h, (p.flags & PSN_LK_ACCUM_SCALAR) == 0, bl.pb, d.bx_tra, d.bx_trb, d.bx_tre);
+            d.bx_tre = psn::bx_err_rows(w, h, psn::BxLayout(w, h, 4).pb);
             d.dv_bxpm = psn::div_magic(psn::bx_pm(w));
             d.dv_bxjr = psn::div_magic(psn::bx_jrp(w) / 4);
         }
@@ -608,6 +609,15 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             if (rc) return rc;
         }
         if (!all_single && all_box && c->box && !c->force_generic && !forced) {
+            lds_bx = 0;  // the launch's UPT sizes every query's fallback planes; tiles as large as
+                         // three workgroups per CU allow
+            for (int i = 0; i < nqd; i++) {
+                psn::LkQueryDev &d = a.q[i];
+                d.bx_hw = 1;
+                while (d.bx_hw < 8 && psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw + 1).total <= psn::kBxLdsTarget)
+                    d.bx_hw++;
+                lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw).total);
+            }
             HIPCHK(c, psn::launch_lk_bx(a, wgs, upt_bx, lds_bx, c->stream));
             continue;
         }

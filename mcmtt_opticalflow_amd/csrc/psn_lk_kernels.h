@@ -47,9 +47,9 @@ struct LkQueryDev {
     unsigned dv_w, dv_dw, dv_pm, dv_jrw, dv_jrw4, dv_g, dv_cw;
     int ow_g, ow_rg;
     int qidx;             // the caller's query index (LkLaunchArgs::counts)
-    // box-window kernel: row tiles of the ordered-chain fallbacks (A, b, err)
+    // box-window kernel: row tiles of the err-chain fallback
     // and the division magics of its I-patch / J-region dword rows
-    int bx_tra, bx_trb, bx_tre;
+    int bx_tre, bx_hw;  // + half waves per fallback tile
     unsigned dv_bxpm, dv_bxjr;
 };
 __host__ __device__ inline unsigned div_magic(int d) { return d > 0 ? ((1u << 22) + (unsigned)d - 1u) / (unsigned)d : 0u; }
@@ -210,44 +210,38 @@ struct LkStLayout {
 // and the row-tiled float chain planes of the ordered-sum fallbacks.
 constexpr int kBxNT = 256;
 constexpr int kBxMaxUPT = 12;
-constexpr int kBxRecInts = 3 * 15 + 1;                 // per wave: 15 chains x {total, max, min} + term flag
+constexpr int kBxRecInts = 8 * 15 + 4;                 // per wave and chain: {total, max, min prefix, -} at lanes 31 and 63; term flag
 constexpr int kBxXInts = 2 * 4 * kBxRecInts;           // two parities x 4 waves
 constexpr int kBxScrBytes = (kBxXInts + 32) * 4 + 64;  // + results / err partials
-constexpr int kBxPlaneMin = 24 * 1024;
 constexpr int kBxMaxLds = 64 * 1024;
+constexpr int kBxLdsTarget = 53 * 1024;  // three workgroups per CU
 __host__ __device__ inline int bx_qw(int w) { return (w + 3) >> 2; }
 __host__ __device__ inline int bx_pm(int w) { return bx_qw(w) + 2; }      // I patch dwords per row
 __host__ __device__ inline int bx_jrp(int w) { return st_jreg_w(w) + 8; }  // J region row pitch (bytes)
 __host__ __device__ inline int bx_round4(int x) { return (x + 3) & ~3; }
 // One chain region of a fallback plane: n floats rounded to 64, + 4, so the
 // chain bases of one plane start 4 floats apart modulo 64 banks (conflict-free
-// 16-B reads by the chain lanes; a plane is 20 floats mod 64, so up to three
-// planes stay apart too).
+// 16-B reads by the chain lanes; planes stay apart too).
 __host__ __device__ inline int bx_region(int n) { return ((n + 63) & ~63) + 4; }
-// floats of one chain-major plane of tr rows: 4 SSE2 lane regions of tr*nq + the tail region
-__host__ __device__ inline int bx_plane(int tr, int nq, int tc) { return 4 * bx_region(tr * nq) + bx_region(tr * tc); }
+// Fallback tiles are half-wave unit ranges (32 threads x UPT units): one plane
+// (4 SSE2 lane regions + the tail region) holds at most 4*32*UPT terms + padding.
+__host__ __device__ inline int bx_pc(int upt) { return 128 * upt + 336; }
 struct BxLayout {
     int jr, un, pb, total;
-    __host__ __device__ BxLayout(int w, int h) {
+    __host__ __device__ BxLayout(int w, int h, int upt, int hw = 1) {
         jr = align16(kBxScrBytes);
         un = jr + align16(st_jreg_h(h) * bx_jrp(w));
         const int pim = align16((h + 3) * 4 * bx_pm(w));
-        pb = pim > kBxPlaneMin ? pim : kBxPlaneMin;
-        total = un + pb;
+        const int planes = 16 * bx_pc(upt) * hw;  // tiles of hw half waves; b: 2 buffers x 2 planes; A: 3 planes
+        pb = pim > planes ? pim : planes;
+        total = un + pb + 1024;  // slack: the chain sums read up to 5 blocks past a chain (discarded)
     }
 };
-// Row tiles of the fallback planes within the union (host side): A = 3 planes,
-// b = 2 planes, err = 1 row-major plane.
-inline void bx_tiles(int w, int h, bool sse, int pb, int &tra, int &trb, int &tre) {
-    const int nqa = sse ? w / 4 : 0, ta = w - 4 * nqa;
-    const int nqb = sse ? w / 8 * 2 : 0, tb = w - 4 * nqb;
-    tra = trb = tre = 1;
+// Row tiles of the (rare) err chain fallback: one row-major plane.
+inline int bx_err_rows(int w, int h, int pb) {
     for (int t = h; t >= 1; t--)
-        if (12 * bx_plane(t, nqa, ta) <= pb) { tra = t; break; }
-    for (int t = h; t >= 1; t--)
-        if (8 * bx_plane(t, nqb, tb) <= pb) { trb = t; break; }
-    for (int t = h; t >= 1; t--)
-        if (4 * bx_round4(t * w) <= pb) { tre = t; break; }
+        if (4 * bx_round4(t * w) <= pb) return t;
+    return 1;
 }
 
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel

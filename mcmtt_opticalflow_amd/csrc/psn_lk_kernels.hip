@@ -2298,69 +2298,90 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
 // float in the SSE2 build's order. Otherwise the ordered float chains: terms
 // chain-major into LDS planes, row tile by row tile, one lane per chain.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wave_max_i(int v) {
+// Inclusive max / min scans over the 64 lanes (the wave_scan DPP sequence):
+// lane 31 holds lanes 0-31, lane 63 the whole wave.
+__device__ __forceinline__ int wave_max_scan(int v) {
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xf, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xf, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xf, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xf, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xa, 0xf, false));
     v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xc, 0xf, false));
-    return __builtin_amdgcn_readlane(v, 63);
+    return v;
 }
-__device__ __forceinline__ int wave_min_i(int v) {
+__device__ __forceinline__ int wave_min_scan(int v) {
     v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));
     v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));
     v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));
     v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));
     v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xa, 0xf, false));
     v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xc, 0xf, false));
-    return __builtin_amdgcn_readlane(v, 63);
+    return v;
 }
 
 // Publish this wave's part of NC chains (per-lane run total T, maximum prefix M
-// >= 0 and minimum prefix m <= 0, prefixes relative to the run start): the
-// wave's chain total and its extreme prefixes relative to the wave's start.
-// int32 is enough: a run holds <= 48 terms < 2^25, and any wrap happens only
-// past a prefix that already fails the 2^24 bound.
+// >= 0 and minimum prefix m <= 0, prefixes relative to the run start): per
+// half wave (lanes 0-31, then the whole wave) the chain total and the extreme
+// prefixes, relative to the wave's start. int32 is enough: a run holds <= 48
+// terms < 2^25, and any wrap happens only past a prefix that already fails the
+// 2^24 bound.
 template <int NC>
 __device__ __forceinline__ void bx_publish(const int (&T)[NC], const int (&M)[NC], const int (&m)[NC], bool bad,
-                                           int *rec) {
+                                           int *rec, bool no_tail) {
     const int lane = threadIdx.x & 63;
     int *xw = rec + (threadIdx.x >> 6) * kBxRecInts;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
+        if (no_tail && c % 5 == 4) {  // empty tail chain (uniform)
+            if (lane == 31 || lane == 63) *(int4 *)(xw + 8 * c + (lane == 63 ? 4 : 0)) = make_int4(0, 0, 0, 0);
+            continue;
+        }
         const int incl = wave_scan(T[c]);
         const int ex = incl - T[c];
-        const int hi = wave_max_i(ex + M[c]);
-        const int lo = wave_min_i(ex + m[c]);
-        const int tot = __builtin_amdgcn_readlane(incl, 63);
-        if (lane == 0) {
-            xw[3 * c] = tot;
-            xw[3 * c + 1] = hi;
-            xw[3 * c + 2] = lo;
-        }
+        const int hs = wave_max_scan(ex + M[c]);
+        const int ls = wave_min_scan(ex + m[c]);
+        // lanes 31 and 63 hold the half-wave and wave values: they write them directly
+        if (lane == 31 || lane == 63) *(int4 *)(xw + 8 * c + (lane == 63 ? 4 : 0)) = make_int4(incl, hs, ls, 0);
     }
     const bool anybad = __ballot(bad) != 0ull;
-    if (lane == 0) xw[3 * 15] = anybad ? 1 : 0;
+    if (lane == 0) xw[8 * 15] = anybad ? 1 : 0;
 }
-// After the barrier: lane c < NC checks chain c over the 4 waves' records and
-// returns its total; the wave-uniform verdict is "no lane failed".
+// After the barrier: lane c < NC checks chain c over the 8 half waves in chain
+// order. Returns the wave-uniform verdict "every prefix of every chain is an
+// exact integer"; total = chain c's sum; h0 = the first half wave (0-7) where
+// any chain's prefix leaves the exact range (8: none); base0 = chain c's exact
+// prefix before half wave h0.
 template <int NC>
-__device__ __forceinline__ bool bx_eval(const int *rec, int &total) {
+__device__ __forceinline__ bool bx_eval(const int *rec, int &total, int &h0, int &base0) {
     const int lane = threadIdx.x & 63;
-    bool ok = true;
-    long long base = 0;
     const int c = lane < NC ? lane : 0;
+    long long base = 0;
+    int fh = 8;
+    int t31[4], t63[4];
 #pragma unroll
     for (int wv = 0; wv < 4; wv++) {
-        const int *xw = rec + wv * kBxRecInts;
-        const int tot = xw[3 * c], hi = xw[3 * c + 1], lo = xw[3 * c + 2], bad = xw[3 * 15];
-        ok &= (base + hi <= (long long)kExact) & (base + lo >= -(long long)kExact) & (bad == 0);
-        base += tot;
+        const int *xw = rec + wv * kBxRecInts + 8 * c;
+        const int4 a = *(const int4 *)xw, b = *(const int4 *)(xw + 4);
+        const bool bad = rec[wv * kBxRecInts + 8 * 15] != 0;
+        t31[wv] = a.x;
+        t63[wv] = b.x;
+        const bool ok0 = (base + a.y <= (long long)kExact) & (base + a.z >= -(long long)kExact) & !bad;
+        const bool ok1 = (base + b.y <= (long long)kExact) & (base + b.z >= -(long long)kExact) & !bad;
+        const int f = !ok0 ? 2 * wv : !ok1 ? 2 * wv + 1 : 8;
+        fh = min(fh, f);
+        base += b.x;
     }
-    ok |= lane >= NC;
     total = (int)base;
-    return __ballot(!ok) == 0ull;
+    if (lane >= NC) fh = 8;
+    h0 = __builtin_amdgcn_readlane(wave_min_scan(fh), 63);
+    long long b0 = 0;
+#pragma unroll
+    for (int wv = 0; wv < 4; wv++) {
+        if (2 * wv + 1 < h0) b0 += t63[wv];
+        else if (2 * wv + 1 == h0) b0 += t31[wv];
+    }
+    base0 = (int)b0;
+    return h0 == 8;
 }
 __device__ __forceinline__ float rl_f(int v, int lane) { return (float)__builtin_amdgcn_readlane(v, lane); }
 
@@ -2391,28 +2412,81 @@ __device__ __forceinline__ unsigned bx_sel(int sj, int i) {
     return 0x0c000c00u | ((unsigned)(sj + i + 1) << 16) | (unsigned)(sj + i);
 }
 
-// Ordered float sum of `len` LDS floats (16-B aligned) onto acc: 16 floats per
-// step with the next two 16-float blocks already in flight, so the LDS latency
-// hides behind the dependent adds (the lanes of a wave sum different chains).
-__device__ __forceinline__ float chain_sum_pl(const float *p, int len, float acc) {
-    const float4 *q = (const float4 *)p;
-    const int nb = len >> 4;
-    if (nb > 0) {
-        float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
-        const int b1 = min(1, nb - 1);
-        float4 c0 = q[4 * b1], c1 = q[4 * b1 + 1], c2 = q[4 * b1 + 2], c3 = q[4 * b1 + 3];
-        for (int b = 0; b < nb; b++) {
-            const int bn = min(b + 2, nb - 1);  // in-bounds prefetch (the last blocks re-read)
-            const float4 e0 = q[4 * bn], e1 = q[4 * bn + 1], e2 = q[4 * bn + 2], e3 = q[4 * bn + 3];
-            acc = add16(acc, a0, a1, a2, a3);
-            a0 = c0, a1 = c1, a2 = c2, a3 = c3;
-            c0 = e0, c1 = e1, c2 = e2, c3 = e3;
-        }
+// Ordered float sum of a zero-padded LDS chain (16-B aligned, ceil(len/16)
+// blocks of 16 floats; +0 pads leave an integer-valued sum unchanged) onto acc,
+// with two blocks in flight while one is summed: the LDS latency hides behind
+// the dependent adds. Blocks go to three register sets with fixed roles (the
+// loop is unrolled by 3, so no in-flight register is ever copied); the loads
+// and their lgkmcnt waits are inline asm, because as plain loads the compiler
+// folds the loop-carried registers back into one load at the top of each step
+// and waits there. nbmax = the wave's largest block count (uniform); lanes past
+// their own chain keep acc (the blocks they read are discarded).
+typedef float bxf4 __attribute__((ext_vector_type(4)));
+#define BX_LD(v0, v1, v2, v3, addr, o0, o1, o2, o3)                                                   \
+    asm volatile("ds_read_b128 %0, %4 offset:" #o0 "\n\tds_read_b128 %1, %4 offset:" #o1 "\n\t"           \
+                 "ds_read_b128 %2, %4 offset:" #o2 "\n\tds_read_b128 %3, %4 offset:" #o3                  \
+                 : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)                                              \
+                 : "v"(addr)                                                                           \
+                 : "memory")
+#define BX_WAIT8(v0, v1, v2, v3) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3))
+__device__ __forceinline__ float add16m(float acc, const bxf4 &a, const bxf4 &b, const bxf4 &c, const bxf4 &d, bool on) {
+    float t = acc;
+    t = t + a.x; t = t + a.y; t = t + a.z; t = t + a.w;
+    t = t + b.x; t = t + b.y; t = t + b.z; t = t + b.w;
+    t = t + c.x; t = t + c.y; t = t + c.z; t = t + c.w;
+    t = t + d.x; t = t + d.y; t = t + d.z; t = t + d.w;
+    return on ? t : acc;
+}
+__device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax, float acc) {
+    unsigned ad = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float *)p;
+    const int nb = (len + 15) >> 4;
+    if (nbmax <= 0) return acc;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the counts below are then exact
+    bxf4 a0, a1, a2, a3, c0, c1, c2, c3, e0, e1, e2, e3;
+    BX_LD(a0, a1, a2, a3, ad, 0, 16, 32, 48);
+    BX_LD(c0, c1, c2, c3, ad, 64, 80, 96, 112);
+    for (int b = 0; b < nbmax; b += 3) {
+        BX_LD(e0, e1, e2, e3, ad, 128, 144, 160, 176);
+        BX_WAIT8(a0, a1, a2, a3);
+        acc = add16m(acc, a0, a1, a2, a3, b < nb);
+        BX_LD(a0, a1, a2, a3, ad, 192, 208, 224, 240);
+        BX_WAIT8(c0, c1, c2, c3);
+        acc = add16m(acc, c0, c1, c2, c3, b + 1 < nb);
+        BX_LD(c0, c1, c2, c3, ad, 256, 272, 288, 304);
+        BX_WAIT8(e0, e1, e2, e3);
+        acc = add16m(acc, e0, e1, e2, e3, b + 2 < nb);
+        ad += 192u;
     }
-    for (int i = nb * 16; i < len; i++) acc = acc + p[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
+                 :
+                 : "memory");
     return acc;
 }
 
+// Diagnostic phase clocks (PSN_LK_STAMPS, thread 0's view): accumulated
+// s_memtime ticks per phase, written as stamps[wg][0..15] at the end.
+#ifdef PSN_LK_STAMPS
+#define BX_CLK(t) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory")
+#define BX_BEGIN() BX_CLK(bx_t)
+#define BX_MARK(i)                    \
+    do {                              \
+        unsigned long long t_;        \
+        BX_CLK(t_);                   \
+        bx_acc[i] += t_ - bx_t;       \
+        bx_t = t_;                    \
+    } while (0)
+#define BX_COUNT(i) bx_acc[i]++
+#else
+#define BX_BEGIN() \
+    do {           \
+    } while (0)
+#define BX_MARK(i) \
+    do {           \
+    } while (0)
+#define BX_COUNT(i) \
+    do {            \
+    } while (0)
+#endif
 template <int UPT>
 __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2431,7 +2505,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
     const int nqB = sse ? (w / 8) * 2 : 0, n8 = 4 * nqB, tB = w - n8;   // b: 8-pixel steps
     const int nqA = sse ? w / 4 : 0, nA4 = 4 * nqA, tA = w - nA4;        // A: 4-pixel steps
     const int PM = bx_pm(w), JRW = st_jreg_w(w), JRH = st_jreg_h(h), JRP = bx_jrp(w), JRP4 = JRP >> 2;
-    const BxLayout lay(w, h);
+    const BxLayout lay(w, h, UPT);
     int *X = (int *)smem;                      // chain-check records, two parities
     float *RS = (float *)(X + kBxXInts);       // serial-chain results (wave 0 -> all)
     int *EP = (int *)(RS + 16);                // err partial sums per wave
@@ -2455,6 +2529,11 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
     float errv = 0.f;
     const float FLT_SCALE = 1.f / (1 << 20);
     int par = 0;
+#ifdef PSN_LK_STAMPS
+    unsigned long long bx_acc[16] = {}, bx_t = 0, bx_t0 = 0;
+    BX_CLK(bx_t0);
+    bx_t = bx_t0;
+#endif
 
     unsigned IP[UPT][2], XP[UPT][2], YP[UPT][2];  // I, Ix, Iy as packed 16-bit pairs (pixels 0,1 and 2,3)
     int gmax = 0;              // max |Ix|, |Iy| of the thread's pixels
@@ -2501,6 +2580,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
         dma_patch<NT>(JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
         dma_wait();
         __syncthreads();
+        BX_MARK(0);  // level setup + staging
 
         // ---- A phase: Scharr + bilinear window values of the thread's units from
         // the I patch bytes; the 15 A chains (sum x class) as runs ----
@@ -2616,12 +2696,13 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 T[5 + c] = T12[c], M[5 + c] = M12[c], m[5 + c] = m12[c];
                 T[10 + c] = T22[c], M[10 + c] = T22[c], m[10 + c] = 0;
             }
+            BX_MARK(1);  // A window values + runs
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
-            bx_publish<15>(T, M, m, false, rec);
+            bx_publish<15>(T, M, m, false, rec, tA == 0);
             __syncthreads();
-            int tot;
-            const bool exact = bx_eval<15>(rec, tot);
+            int tot, h0, base0;
+            const bool exact = bx_eval<15>(rec, tot, h0, base0);
             float s3[3];
             if (exact) {
 #pragma unroll
@@ -2633,57 +2714,76 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     s3[s] = t;
                 }
             } else {
-                // ordered float chains: products chain-major into 3 planes per row tile
-                const int TR = Q.bx_tra;
-                float acc = 0.f;
-                for (int r0 = 0; r0 < h; r0 += TR) {
-                    const int tr = min(TR, h - r0);
-                    const int S = bx_region(tr * nqA), P = bx_plane(tr, nqA, tA);
-                    __syncthreads();  // the patch / previous tile is consumed
-                    int yk = y0, qk = q0;
-                    asm volatile("" : "+v"(yk), "+v"(qk));
+                // ordered float chains from half wave h0 on (every earlier prefix is an
+                // exact integer: the chains start from base0): tile g = the units of
+                // threads 32g..32g+31, products chain-major into 3 planes; chain lanes
+                // = lanes 0-14 of wave 3 (lane c holds chain c's base0)
+                const int HW = Q.bx_hw;
+                const bool chl = tid >= 192 && tid < 207;
+                const int cl = chl ? tid - 192 : 0, cs = cl / 5, cc = cl - 5 * cs;
+                float acc = (float)base0;  // |base0| <= 2^24: exact
+                const int g_last = (U - 1) / (32 * UPT);
+                for (int g = h0; g <= g_last; g += HW) {  // tile = half waves g .. g+HW-1
+                    const int ua = 32 * UPT * g, ub = min(ua + 32 * UPT * HW, U);
+                    const int sa = (ua / QW) * nqA + min(ua % QW, nqA), ta = (ua / QW) * tA + min(max(4 * (ua % QW) - nA4, 0), tA);
+                    const int nsse = (ub / QW) * nqA + min(ub % QW, nqA) - sa;
+                    const int ntail = (ub / QW) * tA + min(max(4 * (ub % QW) - nA4, 0), tA) - ta;
+                    const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                    __syncthreads();  // the previous tile (or the patch) is consumed
+                    if (chl) {  // zero the pad of this lane's region up to whole 16-float blocks
+                        const int len = cc < 4 ? nsse : ntail;
+                        float *rg = PL + cs * P + cc * S;
+                        for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
+                    }
+                    if ((tid >> 5) >= g && (tid >> 5) < g + HW) {
+                        int yk = y0, qk = q0;
+                        asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
-                    for (int k = 0; k < UPT; k++) {
-                        if (u0 + k < U && yk >= r0 && yk < r0 + tr) {
-                            unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
-                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));  // no hoisting out of the tile loop
+                        for (int k = 0; k < UPT; k++) {
+                            if (u0 + k < U) {
+                                unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
+                                asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
+                                const bool su = qk < nqA;
+                                const int base = su ? yk * nqA + qk - sa : 4 * S + yk * tA + 4 * qk - nA4 - ta;
 #pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                const int x = 4 * qk + i;
-                                if (x < w) {
-                                    const int gx = ((i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]));
-                                    const int gy = ((i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]));
-                                    const int pos = qk < nqA ? i * S + (yk - r0) * nqA + qk : 4 * S + (yk - r0) * tA + (x - nA4);
-                                    PL[pos] = (float)__mul24(gx, gx);
-                                    PL[P + pos] = (float)__mul24(gx, gy);
-                                    PL[2 * P + pos] = (float)__mul24(gy, gy);
+                                for (int i = 0; i < 4; i++) {
+                                    // pixels past the window width write a dummy slot past the planes
+                                    const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                                    const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                                    const bool on = 4 * qk + i < w;
+                                    float *d1 = on ? PL + (su ? i * S + base : base + i) : PL + 3 * bx_pc(UPT) * HW;
+                                    const int pp = on ? P : 1;
+                                    d1[0] = (float)__mul24(gx, gx);
+                                    d1[pp] = (float)__mul24(gx, gy);
+                                    d1[2 * pp] = (float)__mul24(gy, gy);
                                 }
                             }
-                        }
-                        if (++qk == QW) {
-                            qk = 0;
-                            yk++;
+                            if (++qk == QW) {
+                                qk = 0;
+                                yk++;
+                            }
                         }
                     }
                     __syncthreads();
-                    if (tid < 15) {
-                        const int s = tid / 5, c = tid - 5 * s;
-                        acc = chain_sum_pl(PL + s * P + c * S, c < 4 ? tr * nqA : tr * tA, acc);
+                    if ((tid >> 6) == 3) {
+                        const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
+                        const int nbmax = __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
+                        if (chl) acc = chain_sum_pl(PL + cs * P + cc * S, len, nbmax, acc);
                     }
                 }
-                if (tid < 64) {
-                    const int a = __float_as_int(acc);
+                if (tid >= 192) {  // wave 3 combines in the SSE2 build's order
+                    const int av = __float_as_int(acc);
 #pragma unroll
                     for (int s = 0; s < 3; s++) {
-                        float t = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 4));
+                        float t = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 4));
                         if (sse) {
-                            const float c0 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s));
-                            const float c1 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 1));
-                            const float c2 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 2));
-                            const float c3 = __int_as_float(__builtin_amdgcn_readlane(a, 5 * s + 3));
+                            const float c0 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s));
+                            const float c1 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 1));
+                            const float c2 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 2));
+                            const float c3 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 3));
                             t = __fadd_rn(t, __fadd_rn(__fadd_rn(__fadd_rn(c0, c1), c2), c3));
                         }
-                        if (tid == 0) RS[s] = t;
+                        if (tid == 192) RS[s] = t;
                     }
                 }
                 __syncthreads();
@@ -2691,6 +2791,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 s3[1] = RS[1];
                 s3[2] = RS[2];
             }
+            BX_MARK(2);  // A publish / eval / serial chains
             A11 = __fmul_rn(s3[0], FLT_SCALE);
             A12 = __fmul_rn(s3[1], FLT_SCALE);
             A22 = __fmul_rn(s3[2], FLT_SCALE);
@@ -2725,6 +2826,8 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 dma_wait();
                 __syncthreads();
             }
+            BX_MARK(3);  // iteration head (restage)
+            BX_COUNT(10);
             const unsigned W0 = pack_w(w00, w01), W1 = pack_w(w10, w11);
             const int ox = inx - jr_x0, oy = iny - jr_y0, sj = ox & 3;
             const unsigned s0 = bx_sel(sj, 0), s1 = bx_sel(sj, 1), s2 = bx_sel(sj, 2), s3 = bx_sel(sj, 3);
@@ -2781,13 +2884,16 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 T[c] = T1[c], M[c] = M1[c], m[c] = m1[c];
                 T[5 + c] = T2[c], M[5 + c] = M2[c], m[5 + c] = m2[c];
             }
+            BX_MARK(4);  // b main pass
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
-            bx_publish<10>(T, M, m, bad, rec);
+            bx_publish<10>(T, M, m, bad, rec, tB == 0);
             __syncthreads();
-            int tot;
+            int tot, h0, base0;
             float b1, b2;
-            if (bx_eval<10>(rec, tot)) {
+            const bool bex = bx_eval<10>(rec, tot, h0, base0);
+            BX_MARK(5);  // b publish + barrier + eval
+            if (bex) {
                 b1 = rl_f(tot, 4);
                 b2 = rl_f(tot, 9);
                 if (sse) {
@@ -2795,32 +2901,45 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     b2 = __fadd_rn(b2, __fadd_rn(__fadd_rn(rl_f(tot, 5), rl_f(tot, 7)), __fadd_rn(rl_f(tot, 6), rl_f(tot, 8))));
                 }
             } else {
-                // ordered float chains, row tiles of 2 planes, lanes 0-9 of wave 0
-                const int TR = Q.bx_trb;
-                float acc = 0.f;
-                for (int r0 = 0; r0 < h; r0 += TR) {
-                    const int tr = min(TR, h - r0);
-                    const int S = bx_region(tr * nqB), P = bx_plane(tr, nqB, tB);
-                    __syncthreads();  // previous tile consumed
+                // ordered float chains from half wave h0 on, tiles of 32 threads' units,
+                // double-buffered: the threads of tile g+1 write its products while the
+                // chain lanes (wave 3, lanes 0-9, starting from the exact prefixes
+                // base0) sum tile g
+                const int HW = Q.bx_hw, PC = bx_pc(UPT) * HW;
+                const bool chl = tid >= 192 && tid < 202;
+                const int cl = chl ? tid - 192 : 0, cs = cl / 5, cc = cl - 5 * cs;
+                float acc = (float)base0;
+                const int g_last = (U - 1) / (32 * UPT);
+                auto tile_geo = [&](int g, int &sa, int &ta, int &nsse, int &ntail) {
+                    const int ua = 32 * UPT * g, ub = min(ua + 32 * UPT * HW, U);
+                    sa = (ua / QW) * nqB + min(ua % QW, nqB);
+                    ta = (ua / QW) * tB + min(max(4 * (ua % QW) - n8, 0), tB);
+                    nsse = (ub / QW) * nqB + min(ub % QW, nqB) - sa;
+                    ntail = (ub / QW) * tB + min(max(4 * (ub % QW) - n8, 0), tB) - ta;
+                };
+                auto write_tile = [&](int g, float *buf) {
+                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
+                    int sa, ta, nsse, ntail;
+                    tile_geo(g, sa, ta, nsse, ntail);
+                    const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                     int yk = y0, qk = q0;
                     asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
                     for (int k = 0; k < UPT; k++) {
-                        if (u0 + k < U && yk >= r0 && yk < r0 + tr) {
+                        if (u0 + k < U) {
                             int d[4];
-                            bx_diffs(JR32 + (oy + (yk)) * JRP4 + (ox >> 2) + (qk), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
-                            unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
-                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
+                            bx_diffs(JR32 + (oy + yk) * JRP4 + (ox >> 2) + qk, JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+                            const bool su = qk < nqB;
+                            const int base = su ? yk * nqB + qk - sa : 4 * S + yk * tB + 4 * qk - n8 - ta;
 #pragma unroll
                             for (int i = 0; i < 4; i++) {
-                                const int x = 4 * qk + i;
-                                if (x < w) {
-                                    const int gx = ((i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]));
-                                    const int gy = ((i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]));
-                                    const int pos = qk < nqB ? i * S + (yk - r0) * nqB + qk : 4 * S + (yk - r0) * tB + (x - n8);
-                                    PL[pos] = (float)__mul24(d[i], gx);
-                                    PL[P + pos] = (float)__mul24(d[i], gy);
-                                }
+                                // pixels past the window width write a dummy slot past the buffers (branch-free)
+                                const int gx = (i & 1) ? hi16(XP[k][i >> 1]) : lo16(XP[k][i >> 1]);
+                                const int gy = (i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]);
+                                const bool on = 4 * qk + i < w;
+                                float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 4 * PC;
+                                d1[0] = (float)__mul24(d[i], gx);
+                                d1[on ? P : 1] = (float)__mul24(d[i], gy);
                             }
                         }
                         if (++qk == QW) {
@@ -2828,13 +2947,50 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                             yk++;
                         }
                     }
-                    __syncthreads();
-                    if (tid < 10) {
-                        const int s = tid / 5, c = tid - 5 * s;
-                        acc = chain_sum_pl(PL + s * P + c * S, c < 4 ? tr * nqB : tr * tB, acc);
+                };
+                auto pad_tile = [&](int g, float *buf) {  // chain lanes: zero their region's pad
+                    if (!chl) return;
+                    int sa, ta, nsse, ntail;
+                    tile_geo(g, sa, ta, nsse, ntail);
+                    const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                    const int len = cc < 4 ? nsse : ntail;
+                    float *rg = buf + cs * P + cc * S;
+                    for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
+                };
+                write_tile(h0, PL);
+                pad_tile(h0, PL);
+                __syncthreads();
+                BX_MARK(6);  // serial b: first tile's products
+                for (int g = h0, t = 0; g <= g_last; g += HW, t ^= 1) {  // tile = half waves g .. g+HW-1
+                    float *cur = PL + t * 2 * PC, *nxt = PL + (t ^ 1) * 2 * PC;
+                    if (g + HW <= g_last) write_tile(g + HW, nxt);
+#ifdef PSN_LK_STAMPS
+                    unsigned long long tc0, tc1, tc2;
+                    BX_CLK(tc0);
+#endif
+                    if ((tid >> 6) == 3) {
+                        int sa, ta, nsse, ntail;
+                        tile_geo(g, sa, ta, nsse, ntail);
+                        const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                        const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
+                        const int nbmax = __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
+                        if (chl) acc = chain_sum_pl(cur + cs * P + cc * S, len, nbmax, acc);
+                        if (g + HW <= g_last) pad_tile(g + HW, nxt);
                     }
+#ifdef PSN_LK_STAMPS
+                    BX_CLK(tc1);
+#endif
+                    __syncthreads();
+#ifdef PSN_LK_STAMPS
+                    BX_CLK(tc2);
+                    bx_acc[12] += tc1 - tc0;  // (thread 192's view) chain sums incl. its own tile writes
+                    bx_acc[13] += tc2 - tc1;  // barrier wait
+                    bx_acc[14]++;
+#endif
                 }
-                if (tid < 64) {
+                BX_MARK(7);  // serial b: pipelined products + chains
+                BX_COUNT(11);
+                if (tid >= 192) {  // wave 3 combines in the SSE2 build's order
                     const int a = __float_as_int(acc);
                     float r1 = __int_as_float(__builtin_amdgcn_readlane(a, 4));
                     float r2 = __int_as_float(__builtin_amdgcn_readlane(a, 9));
@@ -2850,7 +3006,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                         r1 = __fadd_rn(r1, __fadd_rn(bb0, bb2));
                         r2 = __fadd_rn(r2, __fadd_rn(bb1, bb3));
                     }
-                    if (tid == 0) {
+                    if (tid == 192) {
                         RS[4] = r1;
                         RS[5] = r2;
                     }
@@ -2859,6 +3015,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 b1 = RS[4];
                 b2 = RS[5];
             }
+            BX_MARK(8);  // b results
             b1 = __fmul_rn(b1, FLT_SCALE);
             b2 = __fmul_rn(b2, FLT_SCALE);
             const float dx = __fmul_rn(__fsub_rn(__fmul_rn(A12, b2), __fmul_rn(A22, b1)), D);
@@ -2947,7 +3104,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                         }
                     }
                     __syncthreads();
-                    if (tid == 0) acc = chain_sum_pl(PL, tr * w, acc);
+                    if (tid == 0) acc = chain_sum(PL, tr * w, acc);
                 }
                 if (tid == 0) RS[8] = acc;
                 __syncthreads();
@@ -2957,6 +3114,18 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
         }
     }
 
+#ifdef PSN_LK_STAMPS
+    {
+        unsigned long long t_end;
+        BX_CLK(t_end);
+        bx_acc[15] = t_end - bx_t0;
+        if (tid == 0 && A.stamps)
+            for (int i = 0; i < 16; i++)
+                if (i < 12 || i > 14) A.stamps[(size_t)blockIdx.x * 64 + i] = bx_acc[i];
+        if (tid == 192 && A.stamps)
+            for (int i = 12; i < 15; i++) A.stamps[(size_t)blockIdx.x * 64 + i] = bx_acc[i];
+    }
+#endif
     if (tid == 0) {
         A.next[2 * pi] = NPx;
         A.next[2 * pi + 1] = NPy;

@@ -112,6 +112,40 @@ static void bsum_classify(const long long *t1, const long long *t2, int w, int h
         }
         g_bsum_log[8] += P1 <= E && N1 <= E && P2 <= E && N2 <= E;
     }
+    {   /* [9] per-mille of the longest chain suffix from the first prefix violation (serial
+         * work of a fallback that starts each chain at its first violation); [10] the same
+         * for a common start (shortest exact prefix over the chains) */
+        const int n8 = sse ? (w / 8) * 8 : 0;
+        long long P[10] = {0};
+        int first[10], len[10] = {0};
+        for (int c = 0; c < 10; c++) first[c] = -1;
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                const int c = x < n8 ? (x & 3) : 4;
+                const long long tt[2] = {t1[y * w + x], t2[y * w + x]};
+                for (int s = 0; s < 2; s++) {
+                    const int cc = 5 * s + c;
+                    P[cc] += tt[s];
+                    if (first[cc] < 0 && (llabs(tt[s]) > E || llabs(P[cc]) > E)) first[cc] = len[cc];
+                    len[cc]++;
+                }
+            }
+        long long worst = 0, common = 0;
+        for (int c = 0; c < 10; c++) {
+            if (!len[c]) continue;
+            const long long suf = first[c] < 0 ? 0 : 1000LL * (len[c] - first[c]) / len[c];
+            if (suf > worst) worst = suf;
+        }
+        int minfirst = 1 << 30;
+        for (int c = 0; c < 10; c++)
+            if (len[c] && first[c] >= 0) {
+                const int f = (int)(1000LL * first[c] / len[c]);
+                if (f < minfirst) minfirst = f;
+            }
+        common = minfirst == (1 << 30) ? 0 : 1000 - minfirst;
+        g_bsum_log[9] += worst;
+        g_bsum_log[10] += common;
+    }
     g_bsum_log[0]++;
     g_bsum_log[1] += (a1 + a2) <= E;
     g_bsum_log[2] += (a1 <= E && a2 <= E);

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Phase clocks of the box-window LK kernel (lk_kernel_bx) from the diagnostic
+build (make -C mcmtt_opticalflow_amd/csrc stamps; run with
+PSN_LK_LIB=.../libpsn_lk_stamps.so). Tracker2D-like windows on the synthetic
+1080p scene, the reference's default criteria (30, 0.01), maxLevel 3.
+Prints per-workgroup mean / slowest cycles per phase (s_memtime ticks, thread
+0's view) and the serial-chain fraction of the iterations.
+
+  WIN=64 WINH=160 NPTS=630 python tools/bx_stamps.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+from mcmtt_opticalflow_amd import _lib, lk, synth  # noqa: E402
+import hiprt  # noqa: E402
+
+PHASES = ["level_setup", "a_window", "a_sums", "iter_head_solve", "b_main_pass", "b_publish_eval",
+          "b_serial_products", "b_serial_chains", "b_results"]
+
+
+def main():
+    npts = int(os.environ.get("NPTS", "630"))
+    w, h = int(os.environ.get("WIN", "64")), int(os.environ.get("WINH", "160"))
+    sc = synth.make_scene(0, 1920, 1080, npts, nboxes=8)
+    f0, f1 = sc.frame(0), sc.frame(1)
+    pts = sc.points_at(1)
+    L = _lib.load()
+    st = hiprt.DeviceBuffer(npts * 64 * 8)
+    with lk.LKContext(1920, 1080, ring_slots=2, max_level_cap=3) as ctx:
+        ctx.push_frame(0, f0)
+        ctx.push_frame(1, f1)
+        rc = L.psn_lk_debug_set_stamps(ctx.handle, st.addr)
+        assert rc == 0, "not a stamps build"
+        q = lk.make_query(1, 0, 0, npts, lk.make_params((w, h), 3))
+        for _ in range(3):
+            ctx.track([q], pts)
+        s = st.to_array((npts, 64), np.uint64).astype(np.int64)
+    tot = s[:, 15]
+    slow = int(np.argmax(tot))
+    ph = s[:, :9]
+    out = {"window": [w, h], "points": npts, "wg_cycles_mean": float(tot.mean()), "wg_cycles_max": int(tot.max()),
+           "iterations_mean": float(s[:, 10].mean()), "iterations_max": int(s[:, 10].max()),
+           "serial_b_fraction": round(float(s[:, 11].sum() / max(s[:, 10].sum(), 1)), 3),
+           "mean": {k: round(float(v), 1) for k, v in zip(PHASES, ph.mean(0))},
+           "slowest_wg": {k: int(v) for k, v in zip(PHASES, ph[slow])} | {"iters": int(s[slow, 10]),
+                                                                            "serial": int(s[slow, 11])}}
+    nt = max(s[:, 14].sum(), 1)
+    out["serial_b_tiles_per_serial_iteration"] = round(float(s[:, 14].sum() / max(s[:, 11].sum(), 1)), 2)
+    out["serial_b_per_tile_chain_lane_view"] = {"chain_sum": round(float(s[:, 12].sum() / nt), 1),
+                                                "barrier_wait": round(float(s[:, 13].sum() / nt), 1)}
+    it = max(s[:, 10].sum(), 1)
+    out["per_iteration"] = {k: round(float(ph[:, i].sum() / it), 1) for i, k in enumerate(PHASES) if i >= 3}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
