@@ -96,6 +96,147 @@ def cpu_baseline(scene, period, npts, win, max_level, budget_s, max_frames):
                       f"oracle/lk_oracle.c with OpenMP over points, {dt:.1f} s"}
 
 
+def tracker_lk_bytes(w, h, win_w, win_h, npts):
+    """Algorithmic bytes of one LK query point over its levels (maxLevel 3, the
+    reference's): per level the I window with its Scharr border ((w+3) x (h+3))
+    and the J window of one bilinear step ((w+1) x (h+1)), + the point I/O."""
+    nlev = 0
+    for lev in range(4):
+        if (w >> lev) < win_w or (h >> lev) < win_h:
+            break
+        nlev += 1
+    return npts * (max(nlev, 1) * ((win_w + 3) * (win_h + 3) + (win_w + 1) * (win_h + 1)) + 8 + 8 + 1 + 4)
+
+
+def cpu_tracker_baseline(scene, period, budget_s, max_frames):
+    """The oracle Tracker2D restatement (oracle/tracker2d_oracle.py: GridFAST,
+    backward chains with LocalSearchKLT, forward LK + matching cost; every
+    calcOpticalFlowPyrLK call rebuilds both pyramids, the reference schedule)
+    on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import oracle  # cpu_baseline leg only
+    import tracker2d_oracle as T2  # cpu_baseline leg only
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    frames = [scene.frame(t) for t in range(period)]
+    ring = [None] * T2.INTERVAL
+    prev = []
+    n, t0 = 0, None
+    for t in range(max_frames + 2):
+        if t == 2:
+            t0 = time.perf_counter()
+        img = frames[ping_pong(t, period)]
+        ring = ring[1:] + [img]
+        boxes = [T2.Rect(float(np.floor(x)), float(np.floor(y)), float(scene.box_w), float(scene.box_h))
+                 for x, y in scene.box_at(ping_pong(t, period))]
+        rois = [(int(b.x), int(b.y), int(b.w), int(b.h)) for b in boxes]
+        feats, _ = oracle.gridfast_detect(img, rois, seed=t)
+        dets = T2.backward_tracking(ring, boxes, feats)
+        trackers = [T2.Tracker([b], f) for b, f in prev]
+        if ring[-2] is not None:
+            T2.forward_tracking(ring, trackers, dets)
+        prev = [(d.box, d.sets[0]) for d in dets if d.sets and len(d.sets[0]) >= 4]
+        if t >= 2:
+            n += 1
+            if time.perf_counter() - t0 >= budget_s:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} Tracker2D frames of the same synthetic video (oracle/tracker2d_oracle.py + "
+                      f"oracle/lk_oracle.c, OpenMP over points; GridFAST restricted to the boxes, cheaper than "
+                      f"the reference's full-frame masked detect), {dt:.1f} s"}
+
+
+def tracker_main(args):
+    """--tracker: the Tracker2D flow stage as CPSNWhere_Tracker2D::Run drives it
+    (box-derived LK windows, not the 21x21 step of the default run): per frame
+    ingest (frames resident in HBM), GridFAST features of every detection,
+    3-step backward chains with device LocalSearchKLT, forward LK of every
+    tracker + matching cost. One camera, one GPU."""
+    import numpy as np
+    import torch
+
+    from mcmtt_opticalflow_amd import _lib, synth
+    from mcmtt_opticalflow_amd import tracker2d as t2d
+
+    torch.cuda.set_device(0)
+    device = torch.device("cuda", 0)
+    W, H, B = args.width, args.height, args.boxes
+    scene = synth.make_scene(0, W, H, 64 * B, nboxes=B)
+    frames = render_frames_torch(scene, args.period, device)
+    torch.cuda.synchronize(device)
+    L = _lib.load()
+    stats = {"features": 0, "lk_bytes": 0}
+    with t2d.FlowTracker(W, H) as ft:
+        lkh = ft.lk_handle()
+        prev = []
+
+        def step(t, count):
+            ft.push_frame_device(frames[ping_pong(t, args.period)].data_ptr(), W, 1)
+            boxes = [(float(np.floor(x)), float(np.floor(y)), float(scene.box_w), float(scene.box_h))
+                     for x, y in scene.box_at(ping_pong(t, args.period))]
+            dets = ft.detect_features([t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in boxes], seed=t)
+            trackers = [t2d.make_tracker([b], f) for b, f in prev]
+            dets_out, trk_out, _ = ft.track_frame(dets, trackers)
+            if count:  # LK points of this frame: backward chain steps (their inputs) + forward
+                for d_in, d in zip(dets, dets_out):
+                    bw = int(d.box.w)
+                    npts = d_in.num_features if d.num_boxes >= 1 else 0
+                    stats["lk_bytes"] += tracker_lk_bytes(W, H, bw, bw, npts)
+                    for k in range(1, min(d.num_boxes, 3)):
+                        stats["lk_bytes"] += tracker_lk_bytes(W, H, bw, bw, d.set_count[k])
+                    stats["features"] += d_in.num_features
+                for tr in trackers:
+                    stats["lk_bytes"] += tracker_lk_bytes(W, H, int(scene.box_w), int(scene.box_h), tr.num_features)
+            prev[:] = [(d.box.tuple(), t2d.points(d.sets[0], d.set_count[0])) for d in dets_out
+                       if d.valid and d.set_count[0] >= 4]
+            ft.rotate()
+
+        t = 0
+        for _ in range(args.warmup):
+            step(t, False)
+            t += 1
+        L.psn_lk_enable_timing(lkh, 4 * args.steps + 8, 1)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(t, True)
+            t += 1
+        torch.cuda.synchronize(device)
+        elapsed = time.perf_counter() - t0
+        import ctypes
+        np_, nt = ctypes.c_int(), ctypes.c_int()
+        pm, tm = ctypes.c_double(), ctypes.c_double()
+        L.psn_lk_timing_stats(lkh, ctypes.byref(np_), ctypes.byref(pm), ctypes.byref(nt), ctypes.byref(tm))
+    fps = args.steps / elapsed
+    lk_ms = tm.value
+    achieved = stats["lk_bytes"] / (lk_ms * 1e-3) / 1e9 if lk_ms > 0 else 0.0
+    out = {
+        "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
+        "config": {"workload": f"Tracker2D mode: 1 camera, {W}x{H} gray, {B} detections/frame "
+                               f"({scene.box_w}x{scene.box_h} boxes), GridFAST features (cap 100), 3-step backward "
+                               "chains + forward LK with box-derived windows, maxLevel 3, LocalSearchKLT on device",
+                   "cameras": 1, "width": W, "height": H, "detections": B, "box": [scene.box_w, scene.box_h],
+                   "parallelism": "camera-per-GPU x1"},
+        "roofline": {"kernel": "lk_kernel_bx (every LK launch of the frame)", "bound": "hbm",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                     "bytes_per_frame": int(stats["lk_bytes"] / args.steps),
+                     "lk_ms_per_frame": round(lk_ms / args.steps, 4), "lk_calls": nt.value},
+        "features_per_frame": round(stats["features"] / args.steps, 1),
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_tracker_baseline(scene, args.period, args.cpu_budget, 400)
+        out["speedup_vs_cpu"] = round(fps / out["cpu_baseline"]["value"], 1)
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,7 +259,12 @@ def main():
                          "stream for more)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01c_pmc_summary.json"),
                     help="rocprofv3 FETCH/WRITE_SIZE summary (tools/profile_round.sh) for roofline.traffic")
+    ap.add_argument("--tracker", action="store_true",
+                    help="Tracker2D mode (box windows, GridFAST, chains; 1 GPU) instead of configs[1]")
+    ap.add_argument("--boxes", type=int, default=8, help="--tracker: detections per frame")
     args = ap.parse_args()
+    if args.tracker:
+        return tracker_main(args)
 
     import numpy as np
     import torch

@@ -72,6 +72,12 @@ const char *psn_t2d_last_error(psn_t2d *t);
 int psn_t2d_set_device_chain(psn_t2d *t, int on);
 /* ingest frame t into the ring's newest slot (cvtColor + resize, :256-263) */
 int psn_t2d_push_frame(psn_t2d *t, const uint8_t *frame, int stride, int channels);
+/* the same from a frame already in device memory (complete on the context's
+ * stream order; psn_lk_push_frame_device semantics) */
+int psn_t2d_push_frame_device(psn_t2d *t, const uint8_t *dev_frame, int stride, int channels);
+/* the flow stage's LK context (a psn_lk_ctx * of include/psn_lk.h: stream,
+ * kernel timing with psn_lk_enable_timing) */
+void *psn_t2d_lk_context(psn_t2d *t);
 /* end of Run: the oldest slot becomes the next frame's slot (:310-316) */
 int psn_t2d_rotate(psn_t2d *t);
 

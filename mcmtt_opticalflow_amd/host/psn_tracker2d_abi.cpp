@@ -183,6 +183,13 @@ int psn_t2d_push_frame(psn_t2d *t, const uint8_t *frame, int stride, int channel
     return set(t, t->flow.PushFrame(frame, stride, channels));
 }
 
+int psn_t2d_push_frame_device(psn_t2d *t, const uint8_t *dev_frame, int stride, int channels) {
+    if (!t || !dev_frame) return PSN_LK_ERR_ARG;
+    return set(t, t->flow.PushFrameDevice(dev_frame, stride, channels));
+}
+
+void *psn_t2d_lk_context(psn_t2d *t) { return t ? (void *)t->flow.LkContext() : nullptr; }
+
 int psn_t2d_rotate(psn_t2d *t) {
     if (!t) return PSN_LK_ERR_ARG;
     t->flow.RotateRing();

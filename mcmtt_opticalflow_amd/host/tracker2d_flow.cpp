@@ -354,6 +354,15 @@ int Tracker2DFlow::PushFrame(const uint8_t *frame, int stride, int channels) {
     return PSN_LK_OK;
 }
 
+int Tracker2DFlow::PushFrameDevice(const uint8_t *dev, int stride, int channels) {
+    if (!lk_) return PSN_LK_ERR_ARG;
+    const int slot = ring_[kT2dInterval - 1];
+    const int rc = psn_lk_push_frame_device(lk_, slot, dev, stride, channels);
+    if (rc) return fail(rc, "psn_lk_push_frame_device");
+    filled_[slot] = true;
+    return PSN_LK_OK;
+}
+
 int Tracker2DFlow::DetectFeatures(const std::vector<Detection> &dets, uint32_t seed,
                                   std::vector<std::vector<Point2f>> &features) {
     if (!lk_) return PSN_LK_ERR_ARG;

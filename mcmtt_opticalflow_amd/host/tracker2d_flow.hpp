@@ -40,6 +40,8 @@ class Tracker2DFlow {
     void Finalize();
     // ingest frame t into the newest ring slot (cvtColor(BGR2GRAY) + resize 1.0)
     int PushFrame(const uint8_t *frame, int stride, int channels);
+    int PushFrameDevice(const uint8_t *dev, int stride, int channels);  // frame already in device memory
+    psn_lk_ctx *LkContext() const { return lk_; }
     // buffer circulation at the end of Run
     void RotateRing();
 

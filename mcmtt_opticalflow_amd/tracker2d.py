@@ -123,6 +123,9 @@ def load():
     L.psn_t2d_last_error.argtypes = [vp]
     L.psn_t2d_last_error.restype = ctypes.c_char_p
     L.psn_t2d_push_frame.argtypes = [vp, vp, ip, ip]
+    L.psn_t2d_push_frame_device.argtypes = [vp, vp, ip, ip]
+    L.psn_t2d_lk_context.argtypes = [vp]
+    L.psn_t2d_lk_context.restype = vp
     L.psn_t2d_rotate.argtypes = [vp]
     L.psn_t2d_write_result_txt.argtypes = [ctypes.c_char_p, ctypes.POINTER(Track2DResult)]
     L.psn_t2d_read_result_txt.argtypes = [ctypes.c_char_p, ctypes.c_uint, ctypes.c_uint, ctypes.POINTER(Track2DResult)]
@@ -219,6 +222,15 @@ class FlowTracker:
         img = np.ascontiguousarray(img, np.uint8)
         ch = 1 if img.ndim == 2 else img.shape[2]
         self._check(self._L.psn_t2d_push_frame(self._h, img.ctypes.data, img.shape[1] * ch, ch), "push_frame")
+
+    def push_frame_device(self, dev_ptr: int, stride: int, channels: int = 1):
+        """Ingest a frame already in device memory (e.g. a torch tensor's data_ptr())."""
+        self._check(self._L.psn_t2d_push_frame_device(self._h, ctypes.c_void_p(dev_ptr), stride, channels),
+                    "push_frame_device")
+
+    def lk_handle(self) -> int:
+        """The flow stage's psn_lk_ctx (kernel timing, stream)."""
+        return self._L.psn_t2d_lk_context(self._h)
 
     def rotate(self):
         self._check(self._L.psn_t2d_rotate(self._h), "rotate")
