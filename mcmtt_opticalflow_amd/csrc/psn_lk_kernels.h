@@ -219,20 +219,20 @@ __host__ __device__ inline int bx_qw(int w) { return (w + 3) >> 2; }
 __host__ __device__ inline int bx_pm(int w) { return bx_qw(w) + 2; }      // I patch dwords per row
 __host__ __device__ inline int bx_jrp(int w) { return st_jreg_w(w) + 8; }  // J region row pitch (bytes)
 __host__ __device__ inline int bx_round4(int x) { return (x + 3) & ~3; }
-// One chain region of a fallback plane: n floats rounded to 64, + 4, so the
-// chain bases of one plane start 4 floats apart modulo 64 banks (conflict-free
-// 16-B reads by the chain lanes; planes stay apart too).
-__host__ __device__ inline int bx_region(int n) { return ((n + 63) & ~63) + 4; }
+// One chain region of a fallback plane: n floats rounded to 16, + 4: with a
+// region stride of 4 (mod 16) floats the chain lanes' 16-B reads of one plane
+// fall into different 4-bank groups (conflict-free).
+__host__ __device__ inline int bx_region(int n) { return ((n + 15) & ~15) + 4; }
 // Fallback tiles are half-wave unit ranges (32 threads x UPT units): one plane
 // (4 SSE2 lane regions + the tail region) holds at most 4*32*UPT terms + padding.
-__host__ __device__ inline int bx_pc(int upt) { return 128 * upt + 336; }
+__host__ __device__ inline int bx_pc(int upt) { return 128 * upt + 96; }
 struct BxLayout {
     int jr, un, pb, total;
     __host__ __device__ BxLayout(int w, int h, int upt, int hw = 1) {
         jr = align16(kBxScrBytes);
         un = jr + align16(st_jreg_h(h) * bx_jrp(w));
         const int pim = align16((h + 3) * 4 * bx_pm(w));
-        const int planes = 16 * bx_pc(upt) * hw;  // tiles of hw half waves; b: 2 buffers x 2 planes; A: 3 planes
+        const int planes = 24 * bx_pc(upt) * hw;  // tiles of hw half waves, 2 buffers x (A: 3, b: 2) planes
         pb = pim > planes ? pim : planes;
         total = un + pb + 1024;  // slack: the chain sums read up to 5 blocks past a chain (discarded)
     }

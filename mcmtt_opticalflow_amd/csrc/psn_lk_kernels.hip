@@ -2442,6 +2442,9 @@ __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax
     const int nb = (len + 15) >> 4;
     if (nbmax <= 0) return acc;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the counts below are then exact
+    // the chain is a dependent add sequence sharing its SIMD with other
+    // workgroups' waves: issue it first
+    __builtin_amdgcn_s_setprio(3);
     bxf4 a0, a1, a2, a3, c0, c1, c2, c3, e0, e1, e2, e3;
     BX_LD(a0, a1, a2, a3, ad, 0, 16, 32, 48);
     BX_LD(c0, c1, c2, c3, ad, 64, 80, 96, 112);
@@ -2460,6 +2463,7 @@ __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
                  :
                  : "memory");
+    __builtin_amdgcn_s_setprio(0);
     return acc;
 }
 
@@ -2715,61 +2719,82 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 }
             } else {
                 // ordered float chains from half wave h0 on (every earlier prefix is an
-                // exact integer: the chains start from base0): tile g = the units of
-                // threads 32g..32g+31, products chain-major into 3 planes; chain lanes
-                // = lanes 0-14 of wave 3 (lane c holds chain c's base0)
-                const int HW = Q.bx_hw;
+                // exact integer: the chains start from base0): tiles of HW half waves
+                // (the units of threads 32g..), products chain-major into 3 planes,
+                // double-buffered: the threads of the next tile write its products
+                // while the chain lanes (lanes 0-14 of wave 3; lane c holds chain c's
+                // base0) sum the current one
+                const int HW = Q.bx_hw, PCA = 3 * bx_pc(UPT) * HW;
                 const bool chl = tid >= 192 && tid < 207;
                 const int cl = chl ? tid - 192 : 0, cs = cl / 5, cc = cl - 5 * cs;
                 float acc = (float)base0;  // |base0| <= 2^24: exact
                 const int g_last = (U - 1) / (32 * UPT);
-                for (int g = h0; g <= g_last; g += HW) {  // tile = half waves g .. g+HW-1
+                auto geoA = [&](int g, int &sa, int &ta, int &nsse, int &ntail) {
                     const int ua = 32 * UPT * g, ub = min(ua + 32 * UPT * HW, U);
-                    const int sa = (ua / QW) * nqA + min(ua % QW, nqA), ta = (ua / QW) * tA + min(max(4 * (ua % QW) - nA4, 0), tA);
-                    const int nsse = (ub / QW) * nqA + min(ub % QW, nqA) - sa;
-                    const int ntail = (ub / QW) * tA + min(max(4 * (ub % QW) - nA4, 0), tA) - ta;
+                    sa = (ua / QW) * nqA + min(ua % QW, nqA);
+                    ta = (ua / QW) * tA + min(max(4 * (ua % QW) - nA4, 0), tA);
+                    nsse = (ub / QW) * nqA + min(ub % QW, nqA) - sa;
+                    ntail = (ub / QW) * tA + min(max(4 * (ub % QW) - nA4, 0), tA) - ta;
+                };
+                auto writeA = [&](int g, float *buf) {
+                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
+                    int sa, ta, nsse, ntail;
+                    geoA(g, sa, ta, nsse, ntail);
                     const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
-                    __syncthreads();  // the previous tile (or the patch) is consumed
-                    if (chl) {  // zero the pad of this lane's region up to whole 16-float blocks
-                        const int len = cc < 4 ? nsse : ntail;
-                        float *rg = PL + cs * P + cc * S;
-                        for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
-                    }
-                    if ((tid >> 5) >= g && (tid >> 5) < g + HW) {
-                        int yk = y0, qk = q0;
-                        asm volatile("" : "+v"(yk), "+v"(qk));
+                    int yk = y0, qk = q0;
+                    asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
-                        for (int k = 0; k < UPT; k++) {
-                            if (u0 + k < U) {
-                                unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
-                                asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
-                                const bool su = qk < nqA;
-                                const int base = su ? yk * nqA + qk - sa : 4 * S + yk * tA + 4 * qk - nA4 - ta;
+                    for (int k = 0; k < UPT; k++) {
+                        if (u0 + k < U) {
+                            unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
+                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
+                            const bool su = qk < nqA;
+                            const int base = su ? yk * nqA + qk - sa : 4 * S + yk * tA + 4 * qk - nA4 - ta;
 #pragma unroll
-                                for (int i = 0; i < 4; i++) {
-                                    // pixels past the window width write a dummy slot past the planes
-                                    const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
-                                    const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
-                                    const bool on = 4 * qk + i < w;
-                                    float *d1 = on ? PL + (su ? i * S + base : base + i) : PL + 3 * bx_pc(UPT) * HW;
-                                    const int pp = on ? P : 1;
-                                    d1[0] = (float)__mul24(gx, gx);
-                                    d1[pp] = (float)__mul24(gx, gy);
-                                    d1[2 * pp] = (float)__mul24(gy, gy);
-                                }
-                            }
-                            if (++qk == QW) {
-                                qk = 0;
-                                yk++;
+                            for (int i = 0; i < 4; i++) {
+                                // pixels past the window width write a dummy slot past the buffers
+                                const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                                const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                                const bool on = 4 * qk + i < w;
+                                float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 2 * PCA;
+                                const int pp = on ? P : 1;
+                                d1[0] = (float)__mul24(gx, gx);
+                                d1[pp] = (float)__mul24(gx, gy);
+                                d1[2 * pp] = (float)__mul24(gy, gy);
                             }
                         }
+                        if (++qk == QW) {
+                            qk = 0;
+                            yk++;
+                        }
                     }
-                    __syncthreads();
+                };
+                auto padA = [&](int g, float *buf) {  // chain lanes: zero their region's pad
+                    if (!chl) return;
+                    int sa, ta, nsse, ntail;
+                    geoA(g, sa, ta, nsse, ntail);
+                    const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                    const int len = cc < 4 ? nsse : ntail;
+                    float *rg = buf + cs * P + cc * S;
+                    for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
+                };
+                // the I patch under PL was consumed before the publish barrier
+                writeA(h0, PL);
+                padA(h0, PL);
+                __syncthreads();
+                for (int g = h0, t = 0; g <= g_last; g += HW, t ^= 1) {
+                    float *cur = PL + t * PCA, *nxt = PL + (t ^ 1) * PCA;
+                    if (g + HW <= g_last) writeA(g + HW, nxt);
                     if ((tid >> 6) == 3) {
+                        int sa, ta, nsse, ntail;
+                        geoA(g, sa, ta, nsse, ntail);
+                        const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                         const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
                         const int nbmax = __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
-                        if (chl) acc = chain_sum_pl(PL + cs * P + cc * S, len, nbmax, acc);
+                        if (chl) acc = chain_sum_pl(cur + cs * P + cc * S, len, nbmax, acc);
+                        if (g + HW <= g_last) padA(g + HW, nxt);
                     }
+                    __syncthreads();
                 }
                 if (tid >= 192) {  // wave 3 combines in the SSE2 build's order
                     const int av = __float_as_int(acc);
