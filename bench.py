@@ -155,7 +155,12 @@ def tracker_main(args):
     (box-derived LK windows, not the 21x21 step of the default run): per frame
     ingest (frames resident in HBM), GridFAST features of every detection,
     3-step backward chains with device LocalSearchKLT, forward LK of every
-    tracker + matching cost. One camera, one GPU."""
+    tracker + matching cost. --cameras C runs C independent cameras on the GPU,
+    one host thread and one flow-stage context (own HIP stream) per camera, so
+    their launches overlap (ctypes releases the GIL in every library call)."""
+    import ctypes
+    import threading
+
     import numpy as np
     import torch
 
@@ -164,75 +169,111 @@ def tracker_main(args):
 
     torch.cuda.set_device(0)
     device = torch.device("cuda", 0)
-    W, H, B = args.width, args.height, args.boxes
-    scene = synth.make_scene(0, W, H, 64 * B, nboxes=B)
-    frames = render_frames_torch(scene, args.period, device)
-    torch.cuda.synchronize(device)
+    W, H, B, C = args.width, args.height, args.boxes, max(1, args.cameras)
     L = _lib.load()
-    stats = {"features": 0, "lk_bytes": 0}
-    with t2d.FlowTracker(W, H) as ft:
-        lkh = ft.lk_handle()
-        prev = []
 
-        def step(t, count):
-            ft.push_frame_device(frames[ping_pong(t, args.period)].data_ptr(), W, 1)
-            boxes = [(float(np.floor(x)), float(np.floor(y)), float(scene.box_w), float(scene.box_h))
-                     for x, y in scene.box_at(ping_pong(t, args.period))]
-            dets = ft.detect_features([t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in boxes], seed=t)
-            trackers = [t2d.make_tracker([b], f) for b, f in prev]
-            dets_out, trk_out, _ = ft.track_frame(dets, trackers)
+    class Camera:
+        def __init__(self, cam):
+            self.scene = synth.make_scene(cam, W, H, 64 * B, nboxes=B)
+            self.frames = render_frames_torch(self.scene, args.period, device)
+            self.ft = t2d.FlowTracker(W, H, cam_id=cam)
+            self.lkh = self.ft.lk_handle()
+            self.prev = []
+            self.lk_bytes = 0
+            self.features = 0
+            self.t = 0
+
+        def step(self, count):
+            sc, t = self.scene, self.t
+            self.ft.push_frame_device(self.frames[ping_pong(t, args.period)].data_ptr(), W, 1)
+            boxes = [(float(np.floor(x)), float(np.floor(y)), float(sc.box_w), float(sc.box_h))
+                     for x, y in sc.box_at(ping_pong(t, args.period))]
+            dets = self.ft.detect_features([t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in boxes],
+                                           seed=t)
+            trackers = [t2d.make_tracker([b], f) for b, f in self.prev]
+            dets_out, _, _ = self.ft.track_frame(dets, trackers)
             if count:  # LK points of this frame: backward chain steps (their inputs) + forward
                 for d_in, d in zip(dets, dets_out):
                     bw = int(d.box.w)
-                    npts = d_in.num_features if d.num_boxes >= 1 else 0
-                    stats["lk_bytes"] += tracker_lk_bytes(W, H, bw, bw, npts)
+                    if d.num_boxes >= 1:
+                        self.lk_bytes += tracker_lk_bytes(W, H, bw, bw, d_in.num_features)
                     for k in range(1, min(d.num_boxes, 3)):
-                        stats["lk_bytes"] += tracker_lk_bytes(W, H, bw, bw, d.set_count[k])
-                    stats["features"] += d_in.num_features
+                        self.lk_bytes += tracker_lk_bytes(W, H, bw, bw, d.set_count[k])
+                    self.features += d_in.num_features
                 for tr in trackers:
-                    stats["lk_bytes"] += tracker_lk_bytes(W, H, int(scene.box_w), int(scene.box_h), tr.num_features)
-            prev[:] = [(d.box.tuple(), t2d.points(d.sets[0], d.set_count[0])) for d in dets_out
-                       if d.valid and d.set_count[0] >= 4]
-            ft.rotate()
+                    self.lk_bytes += tracker_lk_bytes(W, H, int(sc.box_w), int(sc.box_h), tr.num_features)
+            self.prev = [(d.box.tuple(), t2d.points(d.sets[0], d.set_count[0])) for d in dets_out
+                         if d.valid and d.set_count[0] >= 4]
+            self.ft.rotate()
+            self.t += 1
 
-        t = 0
-        for _ in range(args.warmup):
-            step(t, False)
-            t += 1
-        L.psn_lk_enable_timing(lkh, 4 * args.steps + 8, 1)
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step(t, True)
-            t += 1
-        torch.cuda.synchronize(device)
-        elapsed = time.perf_counter() - t0
-        import ctypes
+    cams = [Camera(c) for c in range(C)]
+    torch.cuda.synchronize(device)
+    start = threading.Barrier(C + 1)
+    done = threading.Barrier(C + 1)
+    errors = []
+
+    def run(cam):
+        try:
+            for _ in range(args.warmup):
+                cam.step(False)
+            L.psn_lk_enable_timing(cam.lkh, 4 * args.steps + 8, 1)
+            start.wait()
+            for _ in range(args.steps):
+                cam.step(True)
+        except Exception as e:  # surfaced after the join
+            errors.append(e)
+            start.abort()
+        finally:
+            try:
+                done.wait()
+            except threading.BrokenBarrierError:
+                pass
+
+    threads = [threading.Thread(target=run, args=(c,)) for c in cams]
+    for th in threads:
+        th.start()
+    start.wait()
+    t0 = time.perf_counter()
+    done.wait()
+    elapsed = time.perf_counter() - t0
+    for th in threads:
+        th.join()
+    if errors:
+        raise errors[0]
+    lk_ms, calls = 0.0, 0
+    for cam in cams:
         np_, nt = ctypes.c_int(), ctypes.c_int()
         pm, tm = ctypes.c_double(), ctypes.c_double()
-        L.psn_lk_timing_stats(lkh, ctypes.byref(np_), ctypes.byref(pm), ctypes.byref(nt), ctypes.byref(tm))
-    fps = args.steps / elapsed
-    lk_ms = tm.value
-    achieved = stats["lk_bytes"] / (lk_ms * 1e-3) / 1e9 if lk_ms > 0 else 0.0
+        L.psn_lk_timing_stats(cam.lkh, ctypes.byref(np_), ctypes.byref(pm), ctypes.byref(nt), ctypes.byref(tm))
+        lk_ms += tm.value
+        calls += nt.value
+    lk_bytes = sum(c.lk_bytes for c in cams)
+    fps = C * args.steps / elapsed
+    achieved = lk_bytes / (lk_ms * 1e-3) / 1e9 if lk_ms > 0 else 0.0
+    sc0 = cams[0].scene
     out = {
         "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 5), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
-        "config": {"workload": f"Tracker2D mode: 1 camera, {W}x{H} gray, {B} detections/frame "
-                               f"({scene.box_w}x{scene.box_h} boxes), GridFAST features (cap 100), 3-step backward "
+        "config": {"workload": f"Tracker2D mode: {C} camera(s) per GPU, {W}x{H} gray, {B} detections/frame "
+                               f"({sc0.box_w}x{sc0.box_h} boxes), GridFAST features (cap 100), 3-step backward "
                                "chains + forward LK with box-derived windows, maxLevel 3, LocalSearchKLT on device",
-                   "cameras": 1, "width": W, "height": H, "detections": B, "box": [scene.box_w, scene.box_h],
-                   "parallelism": "camera-per-GPU x1"},
-        "roofline": {"kernel": "lk_kernel_bx (every LK launch of the frame)", "bound": "hbm",
+                   "cameras": C, "cameras_per_gpu": C, "width": W, "height": H, "detections": B,
+                   "box": [sc0.box_w, sc0.box_h],
+                   "parallelism": f"{C} camera(s) per GPU, one stream each" if C > 1 else "camera-per-GPU x1"},
+        "roofline": {"kernel": "lk_kernel_bx (every LK launch of the timed frames)", "bound": "hbm",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
-                     "bytes_per_frame": int(stats["lk_bytes"] / args.steps),
-                     "lk_ms_per_frame": round(lk_ms / args.steps, 4), "lk_calls": nt.value},
-        "features_per_frame": round(stats["features"] / args.steps, 1),
+                     "bytes_per_camera_frame": int(lk_bytes / (C * args.steps)),
+                     "lk_ms_per_camera_frame": round(lk_ms / (C * args.steps), 4), "lk_calls": calls},
+        "features_per_camera_frame": round(sum(c.features for c in cams) / (C * args.steps), 1),
         "cpu_baseline": None,
     }
+    for cam in cams:
+        cam.ft.close()
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_tracker_baseline(scene, args.period, args.cpu_budget, 400)
+        out["cpu_baseline"] = cpu_tracker_baseline(sc0, args.period, args.cpu_budget, 400)
         out["speedup_vs_cpu"] = round(fps / out["cpu_baseline"]["value"], 1)
     print(json.dumps(out), flush=True)
 
