@@ -161,6 +161,10 @@ def tracker_main(args):
     import ctypes
     import threading
 
+    if args.cameras > 1:
+        # every camera's flow stage uses 3 streams (LK, ingest, forward LK); HIP's default of
+        # 4 hardware queues would map several cameras' streams onto one queue and serialize them
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(16, 4 * args.cameras))
     import numpy as np
     import torch
 

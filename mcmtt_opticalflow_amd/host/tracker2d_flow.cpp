@@ -115,6 +115,15 @@ int Tracker2DFlow::Initialize(unsigned camID, int width, int height, int device)
         ring_[i] = i;
         filled_[i] = false;
     }
+    hipStream_t fs = nullptr;
+    hipEvent_t ev = nullptr;
+    if (hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        err_ = "forward stream / event";
+        return PSN_LK_ERR_HIP;
+    }
+    fwd_stream_ = fs;
+    ev_in_ = ev;
     return PSN_LK_OK;
 }
 
@@ -150,6 +159,13 @@ void Tracker2DFlow::Finalize() {
         delete dev_;
         dev_ = nullptr;
     }
+    if (fwd_stream_) {
+        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        (void)hipStreamDestroy((hipStream_t)fwd_stream_);
+        fwd_stream_ = nullptr;
+    }
+    if (ev_in_) (void)hipEventDestroy((hipEvent_t)ev_in_);
+    ev_in_ = nullptr;
     if (lk_) psn_lk_destroy(lk_);
     lk_ = nullptr;
 }
@@ -272,7 +288,10 @@ int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<Detect
                 queries_.push_back(q);
             }
         const size_t nb = queries_.size();
-        if (step == 1) {
+        if (step == 1 && J) {
+            // the forward calls (Track2D_ForwardTrackingAndGetMatchingScore) are independent of the
+            // backward chain: their launch runs on the forward stream, beside the chain's launches
+            fwd_queries_.clear();
             for (size_t j = 0, off = K * cap; j < J; j++) {
                 const Job &jb = (*fwd)[j];
                 psn_lk_query q;
@@ -283,12 +302,22 @@ int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<Detect
                 psn_lk_default_params(&q.params);
                 q.params.win_w = jb.win_w;
                 q.params.win_h = jb.win_h;
-                queries_.push_back(q);
+                fwd_queries_.push_back(q);
                 off += jb.in->size();
             }
-            if (nb == 0 && K) {  // no frame t-1 for the chains: their counts must not be read as the
-                // forward queries' (the counted launch indexes counts by query)
-                chk(hipMemcpyAsync(b.d_cnt, b.h_cnt + K, J * 4, hipMemcpyHostToDevice, st), "forward counts");
+            hipStream_t fs = (hipStream_t)fwd_stream_;
+            chk(hipEventRecord((hipEvent_t)ev_in_, st), "inputs event");
+            chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_in_, 0), "forward wait");
+            if (rc) return rc;
+            rc = psn_lk_set_stream(lk_, fs);
+            if (!rc)
+                rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_cnt + K, b.d_in, b.d_out,
+                                                 b.d_status, b.d_err);
+            const int rs = psn_lk_set_stream(lk_, st);
+            if (rc || rs) return fail(rc ? rc : rs, "forward launch");
+            if (F) {
+                chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
+                chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
             }
         }
         if (queries_.empty()) break;
@@ -297,10 +326,6 @@ int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<Detect
                 : psn_lk_track_device_counted(lk_, queries_.data(), (int)queries_.size(), b.d_cnt, in, b.d_out,
                                               b.d_status, b.d_err);
         if (rc) return fail(rc, "psn_lk_track_device_counted");
-        if (step == 1 && F) {  // the forward results leave before step 2 reuses the buffers
-            chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, st), "forward points");
-            chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, st), "forward status");
-        }
         if (nb == 0) break;
         cd.cur = in;
         cd.nxt = b.d_out;
@@ -315,6 +340,7 @@ int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<Detect
         chk(hipMemcpyAsync(b.h_sets, b.d_sets, K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain sets");
     }
     chk(hipStreamSynchronize(st), "chain sync");
+    chk(hipStreamSynchronize((hipStream_t)fwd_stream_), "forward sync");
     if (rc) return rc;
     for (size_t k = 0; k < K; k++) {
         DetectedObject &ob = out[chains[k].obj];

@@ -61,7 +61,7 @@ class Tracker2DFlow {
     // cost = matchingCostArray [dets x trackers], +inf where not matched.
     int ForwardTrackingAndGetMatchingScore(const std::vector<Tracker2D *> &trackers,
                                            const std::vector<DetectedObject> &dets, std::vector<float> &cost);
-    // both, with backward step 1 and the forward calls in one LK launch
+    // both: the forward calls overlap the backward chain (own stream)
     int TrackFrame(const std::vector<Detection> &dets, const std::vector<std::vector<Point2f>> &features,
                    std::vector<DetectedObject> &out, const std::vector<Tracker2D *> &trackers, std::vector<float> &cost);
 
@@ -95,7 +95,7 @@ class Tracker2DFlow {
     void BackwardEnd(std::vector<Chain> &chains, std::vector<DetectedObject> &out);
     bool StepAvailable(int step) const;
     // every chain step (LK launch + LocalSearchKLT kernel) enqueued back to back,
-    // one host sync at the end; forward jobs share step 1's launch
+    // one host sync at the end; the forward jobs' launch runs beside them
     int ChainsOnDevice(std::vector<Chain> &chains, std::vector<DetectedObject> &out, std::vector<Job> *fwd);
     int EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_jobs);
     void ForwardJobs(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
@@ -104,6 +104,10 @@ class Tracker2DFlow {
                      const std::vector<DetectedObject> &dets, std::vector<float> &cost);
 
     psn_lk_ctx *lk_ = nullptr;
+    // device chain: the forward queries run on their own stream (a hipStream_t),
+    // overlapping the backward chain's launches; ev_in_ orders them after the inputs
+    void *fwd_stream_ = nullptr, *ev_in_ = nullptr;
+    std::vector<psn_lk_query> fwd_queries_;
     unsigned camID_ = 0;
     int width_ = 0, height_ = 0;
     int ring_[kT2dInterval] = {0, 1, 2, 3};  // slot ids, oldest first; ring_[3] = frame t
