@@ -192,10 +192,14 @@ def tracker_main(args):
             self.ft.push_frame_device(self.frames[ping_pong(t, args.period)].data_ptr(), W, 1)
             boxes = [(float(np.floor(x)), float(np.floor(y)), float(sc.box_w), float(sc.box_h))
                      for x, y in sc.box_at(ping_pong(t, args.period))]
-            dets = self.ft.detect_features([t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in boxes],
-                                           seed=t)
+            dets_in = [t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in boxes]
             trackers = [t2d.make_tracker([b], f) for b, f in self.prev]
-            dets_out, _, _ = self.ft.track_frame(dets, trackers)
+            if args.tracker_split:  # psn_t2d_detect_features, then psn_t2d_track_frame
+                dets = self.ft.detect_features(dets_in, seed=t)
+                dets_out, _, _ = self.ft.track_frame(dets, trackers)
+            else:  # one device pass: GridFAST into the chains, forward beside them
+                dets_out, _, _ = self.ft.track_frame_detect(dets_in, trackers, seed=t)
+                dets = dets_out
             if count:  # LK points of this frame: backward chain steps (their inputs) + forward
                 for d_in, d in zip(dets, dets_out):
                     bw = int(d.box.w)
@@ -307,6 +311,8 @@ def main():
     ap.add_argument("--tracker", action="store_true",
                     help="Tracker2D mode (box windows, GridFAST, chains; 1 GPU) instead of configs[1]")
     ap.add_argument("--boxes", type=int, default=8, help="--tracker: detections per frame")
+    ap.add_argument("--tracker-split", action="store_true",
+                    help="--tracker: separate detect_features + track_frame calls (default: track_frame_detect)")
     args = ap.parse_args()
     if args.tracker:
         return tracker_main(args)

@@ -52,6 +52,10 @@ typedef struct psn_t2d_chain_dev {
  * detection, asynchronous on `hip_stream`. Returns 0 or a PSN_LK_ERR_* code. */
 int psn_t2d_chain_step_device(const psn_t2d_chain_dev *c, int step, void *hip_stream);
 
+/* d_cnt[i] = 0 where d_cnt[i] < min_count (the reference skips detections with
+ * fewer than PSN_2D_FEATURE_MIN_NUM_TRACK features, :744), asynchronous. */
+int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

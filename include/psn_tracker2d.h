@@ -127,6 +127,15 @@ int psn_t2d_forward(psn_t2d *t, psn_t2d_tracker *trk, int ntrk, const psn_t2d_de
  * identical to psn_t2d_backward followed by psn_t2d_forward. */
 int psn_t2d_track_frame(psn_t2d *t, psn_t2d_detection *dets, int ndet, psn_t2d_tracker *trk, int ntrk,
                         float *cost);
+/* psn_t2d_detect_features + psn_t2d_track_frame in one device pass (device
+ * chain mode; otherwise the two calls): the forward LK runs first, on its own
+ * stream; GridFAST writes every detection's features straight into the
+ * backward chains' inputs and detections below the feature minimum (:744) are
+ * gated on the device; one host sync. dets[i].features / num_features are
+ * written (the points GridFAST kept), as psn_t2d_detect_features does; the
+ * rest as psn_t2d_track_frame. Identical results. */
+int psn_t2d_track_frame_detect(psn_t2d *t, psn_t2d_detection *dets, int ndet, uint32_t seed, psn_t2d_tracker *trk,
+                               int ntrk, float *cost);
 
 /* ---- stTrack2DResult: the Tracker2D -> Associator3D hand-off ----
  * stObject2DInfo (PSNWhere_Types.h:190-198) and stTrack2DResult (:200-209)

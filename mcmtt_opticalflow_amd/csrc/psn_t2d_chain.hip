@@ -164,8 +164,23 @@ __global__ __launch_bounds__(kLanes) void chain_step_kernel(psn_t2d_chain_dev C,
     }
 }
 
+// Detections whose feature count fails the reference's minimum (:744) get no
+// chain: their count becomes 0, so their workgroups exit at once.
+__global__ void gate_counts_kernel(int *cnt, int n, int min_count) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && cnt[i] < min_count) cnt[i] = 0;
+}
+
 }  // namespace
 }  // namespace psn
+
+extern "C" int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, void *stream) {
+    if (n < 0 || (n > 0 && !d_cnt)) return PSN_LK_ERR_ARG;
+    if (n == 0) return PSN_LK_OK;
+    hipLaunchKernelGGL(psn::gate_counts_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_cnt, n,
+                       min_count);
+    return hipGetLastError() == hipSuccess ? PSN_LK_OK : PSN_LK_ERR_HIP;
+}
 
 extern "C" int psn_t2d_chain_step_device(const psn_t2d_chain_dev *c, int step, void *stream) {
     if (!c || c->ndet < 0 || c->cap <= 0 || c->cap > 128 || step < 1 || step >= PSN_T2D_CHAIN_STEPS)

@@ -260,4 +260,29 @@ int psn_t2d_track_frame(psn_t2d *t, psn_t2d_detection *dets, int ndet, psn_t2d_t
     return trackers_out(tr, trk, ntrk);
 }
 
+int psn_t2d_track_frame_detect(psn_t2d *t, psn_t2d_detection *dets, int ndet, uint32_t seed, psn_t2d_tracker *trk,
+                               int ntrk, float *cost) {
+    if (!t || ntrk < 0 || ndet < 0 || (ntrk > 0 && !trk) || (ndet > 0 && !dets)) return PSN_LK_ERR_ARG;
+    std::vector<psn::Detection> d((size_t)ndet);
+    for (int i = 0; i < ndet; i++) d[(size_t)i].box = to_rect(dets[i].box);
+    std::vector<psn::Tracker2D> tr;
+    int rc = trackers_in(trk, ntrk, tr);
+    if (rc) return rc;
+    std::vector<psn::Tracker2D *> ptr;
+    for (psn::Tracker2D &x : tr) ptr.push_back(&x);
+    std::vector<std::vector<psn::Point2f>> f;
+    std::vector<psn::DetectedObject> objs;
+    std::vector<float> c;
+    rc = t->flow.TrackFrameDetect(d, seed, f, objs, ptr, c);
+    if (rc) return set(t, rc);
+    for (int i = 0; i < ndet; i++) {
+        rc = put_points(f[(size_t)i], dets[i].features, &dets[i].num_features);
+        if (rc) return rc;
+    }
+    rc = detections_out(objs, dets, ndet);
+    if (rc) return rc;
+    if (cost && !c.empty()) std::memcpy(cost, c.data(), c.size() * sizeof(float));
+    return trackers_out(tr, trk, ntrk);
+}
+
 }  // extern "C"

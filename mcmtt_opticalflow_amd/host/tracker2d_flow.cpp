@@ -134,19 +134,19 @@ struct Tracker2DFlow::DeviceBuffers {
     uint8_t *d_status = nullptr;
     double *d_boxes = nullptr, *d_obox = nullptr;
     float *d_sets = nullptr;
-    int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr;
+    int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr, *d_tot = nullptr;
     // pinned staging: inputs, then results
     float *h_in = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
     uint8_t *h_fwd_st = nullptr;
     double *h_boxes = nullptr, *h_obox = nullptr;
-    int *h_cnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr;
+    int *h_cnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr, *h_rawcnt = nullptr;
     void release() {
         for (void *p : {(void *)d_in, (void *)d_out, (void *)d_buf[0], (void *)d_buf[1], (void *)d_err, (void *)d_status,
                         (void *)d_boxes, (void *)d_obox, (void *)d_sets, (void *)d_cnt, (void *)d_setcnt,
-                        (void *)d_nsteps})
+                        (void *)d_nsteps, (void *)d_tot})
             if (p) (void)hipFree(p);
         for (void *p : {(void *)h_in, (void *)h_fwd_out, (void *)h_sets, (void *)h_fwd_st, (void *)h_boxes,
-                        (void *)h_obox, (void *)h_cnt, (void *)h_setcnt, (void *)h_nsteps})
+                        (void *)h_obox, (void *)h_cnt, (void *)h_setcnt, (void *)h_nsteps, (void *)h_rawcnt})
             if (p) (void)hipHostFree(p);
         *this = DeviceBuffers();
     }
@@ -193,6 +193,7 @@ int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_job
     dm((void **)&b.d_cnt, (K + J) * 4);
     dm((void **)&b.d_setcnt, K * S * 4);
     dm((void **)&b.d_nsteps, K * 4);
+    dm((void **)&b.d_tot, K * 4);
     hm((void **)&b.h_in, npt * 8);
     hm((void **)&b.h_fwd_out, F * 8);
     hm((void **)&b.h_sets, K * S * cap * 8);
@@ -202,6 +203,7 @@ int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_job
     hm((void **)&b.h_cnt, (K + J) * 4);
     hm((void **)&b.h_setcnt, K * S * 4);
     hm((void **)&b.h_nsteps, K * 4);
+    hm((void **)&b.h_rawcnt, K * 4);
     if (!ok) {
         b.release();
         err_ = "device-chain buffers: allocation failed";
@@ -671,6 +673,183 @@ int Tracker2DFlow::ForwardTrackingAndGetMatchingScore(const std::vector<Tracker2
     int rc = RunJobs(jobs);
     if (rc) return rc;
     ForwardDone(trackers, status, dets, cost);
+    return PSN_LK_OK;
+}
+
+// GridFAST + backward chains + forward in one device pass (device chain mode):
+// the forward launch goes first on its own stream; GridFAST writes every
+// detection's features straight into the chain inputs (the host never sees
+// them before the chains run); counts below the minimum are gated to 0 on the
+// device; one sync at the end. Results are those of DetectFeatures +
+// TrackFrame.
+int Tracker2DFlow::TrackFrameDetect(const std::vector<Detection> &dets, uint32_t seed,
+                                    std::vector<std::vector<Point2f>> &features, std::vector<DetectedObject> &out,
+                                    const std::vector<Tracker2D *> &trackers, std::vector<float> &cost) {
+    if (!lk_) return PSN_LK_ERR_ARG;
+    if (!device_chain_) {
+        const int rc = DetectFeatures(dets, seed, features);
+        return rc ? rc : TrackFrame(dets, features, out, trackers, cost);
+    }
+    if (!trackers.empty() && !StepAvailable(1)) return PSN_LK_ERR_SLOT;
+    const size_t K = dets.size(), cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
+    std::vector<std::vector<uint8_t>> fstatus;
+    std::vector<Job> fwd;
+    ForwardJobs(trackers, fstatus, fwd);
+    const size_t J = fwd.size();
+    size_t F = 0;
+    for (const Job &jb : fwd) F += jb.in->size();
+    int rc = EnsureDevice(K, F, J);
+    if (rc) return rc;
+    DeviceBuffers &b = *dev_;
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && !rc) {
+            err_ = std::string(what) + ": " + hipGetErrorString(e);
+            rc = PSN_LK_ERR_HIP;
+        }
+    };
+    // 1. the forward calls, first, on the forward stream (after frame t's ingest)
+    if (J) {
+        size_t o = K * cap;
+        fwd_queries_.clear();
+        for (size_t j = 0; j < J; j++) {
+            const std::vector<Point2f> &pts = *fwd[j].in;
+            psn_lk_query q;
+            q.prev_slot = fwd[j].prev_slot;
+            q.next_slot = fwd[j].next_slot;
+            q.first_pt = (int)o;
+            q.num_pts = (int)pts.size();
+            psn_lk_default_params(&q.params);
+            q.params.win_w = fwd[j].win_w;
+            q.params.win_h = fwd[j].win_h;
+            fwd_queries_.push_back(q);
+            for (size_t i = 0; i < pts.size(); i++, o++) {
+                b.h_in[2 * o] = pts[i].x;
+                b.h_in[2 * o + 1] = pts[i].y;
+            }
+            b.h_cnt[K + j] = (int)pts.size();
+        }
+        chk(hipEventRecord((hipEvent_t)ev_in_, st), "ingest event");
+        chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_in_, 0), "forward wait");
+        chk(hipMemcpyAsync(b.d_in + 2 * K * cap, b.h_in + 2 * K * cap, F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
+        chk(hipMemcpyAsync(b.d_cnt + K, b.h_cnt + K, J * 4, hipMemcpyHostToDevice, fs), "forward counts");
+        if (rc) return rc;
+        rc = psn_lk_set_stream(lk_, fs);
+        if (!rc)
+            rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_cnt + K, b.d_in, b.d_out, b.d_status,
+                                             b.d_err);
+        const int rs = psn_lk_set_stream(lk_, st);
+        if (rc || rs) return fail(rc ? rc : rs, "forward launch");
+        if (F) {
+            chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
+            chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
+        }
+    }
+    // 2. GridFAST of every detection into the chain inputs, then the chains
+    if (K) {
+        std::vector<int> rois(4 * K);
+        for (size_t i = 0; i < K; i++) {
+            const Rect r = dets[i].box.scale(kFlowScale).cropWithSize(width_, height_);
+            rois[4 * i] = (int)r.x;
+            rois[4 * i + 1] = (int)r.y;
+            rois[4 * i + 2] = (int)r.w;
+            rois[4 * i + 3] = (int)r.h;
+            const Rect box = dets[i].box.scale(kFlowScale);
+            b.h_boxes[4 * i] = box.x;
+            b.h_boxes[4 * i + 1] = box.y;
+            b.h_boxes[4 * i + 2] = box.w;
+            b.h_boxes[4 * i + 3] = box.h;
+        }
+        psn_gridfast_params p;
+        psn_gridfast_default_params(&p);
+        p.cap = (int)cap;  // kT2dMaxFeatures
+        rc = psn_gridfast_detect_device(lk_, ring_[kT2dInterval - 1], rois.data(), (int)K, &p, seed, b.d_in, b.d_cnt,
+                                        b.d_tot);
+        if (rc) return fail(rc, "psn_gridfast_detect_device");
+        chk(hipMemcpyAsync(b.h_rawcnt, b.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
+        chk(hipMemcpyAsync(b.h_in, b.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
+        if (!rc) rc = psn_t2d_gate_counts_device(b.d_cnt, (int)K, (int)kT2dMinFeatures, st);
+        chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
+        chk(hipMemsetAsync(b.d_nsteps, 0, K * 4, st), "chain steps");
+        chk(hipMemsetAsync(b.d_setcnt, 0, K * S * 4, st), "chain set counts");
+        if (rc) return rc;
+        psn_t2d_chain_dev cd{};
+        cd.ndet = (int)K;
+        cd.cap = (int)cap;
+        cd.boxes = b.d_boxes;
+        cd.cnt = b.d_cnt;
+        cd.out_boxes = b.d_obox;
+        cd.sets = b.d_sets;
+        cd.set_cnt = b.d_setcnt;
+        cd.nsteps = b.d_nsteps;
+        for (int step = 1; step < (int)S && StepAvailable(step); step++) {
+            queries_.clear();
+            for (size_t k = 0; k < K; k++) {
+                psn_lk_query q;
+                q.prev_slot = ring_[kT2dInterval - step];
+                q.next_slot = ring_[kT2dInterval - 1 - step];
+                q.first_pt = (int)(k * cap);
+                q.num_pts = (int)cap;
+                psn_lk_default_params(&q.params);
+                q.params.win_w = q.params.win_h = (int)(b.h_boxes[4 * k + 2] * kWinSizeRatio);
+                queries_.push_back(q);
+            }
+            const float *in = step == 1 ? b.d_in : b.d_buf[step & 1];
+            rc = psn_lk_track_device_counted(lk_, queries_.data(), (int)K, b.d_cnt, in, b.d_out, b.d_status, b.d_err);
+            if (rc) return fail(rc, "psn_lk_track_device_counted");
+            cd.cur = in;
+            cd.nxt = b.d_out;
+            cd.next_in = b.d_buf[(step + 1) & 1];
+            rc = psn_t2d_chain_step_device(&cd, step, st);
+            if (rc) return fail(rc, "psn_t2d_chain_step_device");
+        }
+        chk(hipMemcpyAsync(b.h_nsteps, b.d_nsteps, K * 4, hipMemcpyDeviceToHost, st), "chain steps");
+        chk(hipMemcpyAsync(b.h_obox, b.d_obox, K * S * 32, hipMemcpyDeviceToHost, st), "chain boxes");
+        chk(hipMemcpyAsync(b.h_setcnt, b.d_setcnt, K * S * 4, hipMemcpyDeviceToHost, st), "chain set counts");
+        chk(hipMemcpyAsync(b.h_sets, b.d_sets, K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain sets");
+    }
+    chk(hipStreamSynchronize(st), "chain sync");
+    chk(hipStreamSynchronize(fs), "forward sync");
+    if (rc) return rc;
+    // 3. host: features, the valid detections' objects and chains, forward matching
+    features.assign(K, {});
+    for (size_t i = 0; i < K; i++) {
+        const int n = b.h_rawcnt[i];
+        const float *xy = b.h_in + 2 * cap * i;
+        features[i].resize((size_t)n);
+        for (int k = 0; k < n; k++) features[i][(size_t)k] = Point2f{xy[2 * k], xy[2 * k + 1]};
+    }
+    std::vector<Chain> chains;
+    BackwardBegin(dets, features, out, chains);  // valid detections, in order
+    for (Chain &c : chains) {
+        DetectedObject &ob = out[c.obj];
+        const size_t k = ob.id;  // the detection index = its device chain
+        const int ns = b.h_nsteps[k];
+        for (int s2 = 1; s2 <= ns; s2++) {
+            const double *r = b.h_obox + (k * S + s2) * 4;
+            ob.boxes.push_back(Rect(r[0], r[1], r[2], r[3]).scale(1.0 / kFlowScale));
+        }
+        for (int r = 0; ns > 0 && r <= ns; r++) {
+            const int n = b.h_setcnt[k * S + r];
+            const float *pp = b.h_sets + (k * S + r) * cap * 2;
+            std::vector<Point2f> v((size_t)n);
+            for (int i = 0; i < n; i++) v[(size_t)i] = Point2f{pp[2 * i], pp[2 * i + 1]};
+            ob.vecvecTrackedFeatures.push_back(std::move(v));
+        }
+        c.active = false;
+    }
+    for (size_t j = 0, off = 0; j < J; j++) {
+        Job &jb = fwd[j];
+        const size_t m = jb.in->size();
+        jb.out->resize(m);
+        jb.status->resize(m);
+        for (size_t i = 0; i < m; i++, off++) {
+            (*jb.out)[i] = Point2f{b.h_fwd_out[2 * off], b.h_fwd_out[2 * off + 1]};
+            (*jb.status)[i] = b.h_fwd_st[off];
+        }
+    }
+    BackwardEnd(chains, out);
+    ForwardDone(trackers, fstatus, out, cost);
     return PSN_LK_OK;
 }
 

@@ -65,6 +65,12 @@ class Tracker2DFlow {
     int TrackFrame(const std::vector<Detection> &dets, const std::vector<std::vector<Point2f>> &features,
                    std::vector<DetectedObject> &out, const std::vector<Tracker2D *> &trackers, std::vector<float> &cost);
 
+    // DetectFeatures + TrackFrame as one device pass (device chain mode): GridFAST
+    // writes the chain inputs on the device, the forward launch runs beside it
+    int TrackFrameDetect(const std::vector<Detection> &dets, uint32_t seed,
+                         std::vector<std::vector<Point2f>> &features, std::vector<DetectedObject> &out,
+                         const std::vector<Tracker2D *> &trackers, std::vector<float> &cost);
+
     psn_lk_ctx *lk() const { return lk_; }
     // backward chain steps on the device (default) or on the host (PSN_T2D_HOST_CHAIN=1)
     void SetDeviceChain(bool on) { device_chain_ = on; }

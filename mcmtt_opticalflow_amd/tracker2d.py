@@ -124,6 +124,7 @@ def load():
     L.psn_t2d_last_error.restype = ctypes.c_char_p
     L.psn_t2d_push_frame.argtypes = [vp, vp, ip, ip]
     L.psn_t2d_push_frame_device.argtypes = [vp, vp, ip, ip]
+    L.psn_t2d_track_frame_detect.argtypes = [vp, vp, ip, ctypes.c_uint32, vp, ip, vp]
     L.psn_t2d_lk_context.argtypes = [vp]
     L.psn_t2d_lk_context.restype = vp
     L.psn_t2d_rotate.argtypes = [vp]
@@ -254,6 +255,17 @@ class FlowTracker:
         cost = np.full(max(nvalid * len(trackers), 1), np.nan, np.float32)
         self._check(self._L.psn_t2d_forward(self._h, ta, len(trackers), da, len(dets), cost.ctypes.data), "forward")
         return list(ta)[:len(trackers)], cost[:nvalid * len(trackers)].reshape(nvalid, len(trackers))
+
+    def track_frame_detect(self, dets: list[Detection], trackers: list[Tracker], seed: int = 0):
+        """detect_features + track_frame in one device pass (psn_t2d_track_frame_detect)."""
+        da = (Detection * max(len(dets), 1))(*dets)
+        ta = (Tracker * max(len(trackers), 1))(*trackers)
+        cost = np.full(max(len(dets) * len(trackers), 1), np.nan, np.float32)
+        self._check(self._L.psn_t2d_track_frame_detect(self._h, da, len(dets), seed & 0xffffffff, ta, len(trackers),
+                                                       cost.ctypes.data), "track_frame_detect")
+        dets_out = list(da)[:len(dets)]
+        nvalid = sum(1 for d in dets_out if d.valid)
+        return dets_out, list(ta)[:len(trackers)], cost[:nvalid * len(trackers)].reshape(nvalid, len(trackers))
 
     def track_frame(self, dets: list[Detection], trackers: list[Tracker]):
         da = (Detection * max(len(dets), 1))(*dets)

@@ -153,11 +153,15 @@ def _rect_roi(b, W, H):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("merged,gridfast,device_chain,big", [(False, False, False, False), (True, False, False, False),
-                                                              (False, False, True, False), (True, False, True, False),
-                                                              (True, True, True, False), (True, True, True, True),
-                                                              (True, False, False, True)])
-def test_tracker2d_sequence_matches_oracle(oracle_mod, merged, gridfast, device_chain, big):
+@pytest.mark.parametrize("merged,gridfast,device_chain,big,dev_frames",
+                         [(False, False, False, False, False), (True, False, False, False, False),
+                          (False, False, True, False, False), (True, False, True, False, False),
+                          (True, True, True, False, False), (True, True, True, True, False),
+                          (True, False, False, True, False), (True, True, True, True, True),
+                          ("fused", True, True, False, False), ("fused", True, True, True, True),
+                          ("fused", True, False, False, False)])
+def test_tracker2d_sequence_matches_oracle(oracle_mod, merged, gridfast, device_chain, big, dev_frames):
+    # merged == "fused": psn_t2d_track_frame_detect (GridFAST + chains + forward in one device pass)
     # big: 1080p-class boxes (64 x 160): 64 x 64 backward and 64 x 160 forward
     # windows run the tiled LK kernel (the counted launches included)
     W, H, T = (960, 540, 6) if big else (320, 240, 7)
@@ -167,24 +171,37 @@ def test_tracker2d_sequence_matches_oracle(oracle_mod, merged, gridfast, device_
     ring = [None] * 4
     trackers = []  # oracle trackers (the harness's matching keeps both sides in sync)
     n_cost_finite = n_chain_steps = 0
+    d_frames = []  # device copies of the frames (psn_t2d_push_frame_device), alive to the end
     with t2d.FlowTracker(W, H) as ft:
         ft.set_device_chain(device_chain)
         for t in range(T):
             img = sc.frame(t)
-            ft.push_frame(img)
+            if dev_frames:  # psn_t2d_push_frame_device from a frame already in HBM
+                import hiprt  # tests/hiprt.py: the library's own HIP runtime
+                d_frames.append(hiprt.DeviceBuffer.from_array(np.ascontiguousarray(img)))
+                ft.push_frame_device(d_frames[-1].addr, W, 1)
+            else:
+                ft.push_frame(img)
             ring[-1] = img
             dets, feats = _detections(sc, t, rng, W, H)
             if gridfast:  # the detections' points from GridFAST on frame t (:734-757)
-                g_in = ft.detect_features([t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in dets], seed=t)
                 feats, tots = oracle_mod.gridfast_detect(img, [_rect_roi(b, W, H) for b in dets], seed=t)
-                for d, f, n in zip(g_in, feats, tots):
-                    np.testing.assert_array_equal(t2d.points(d.features, d.num_features), f, err_msg=f"frame {t}")
-                    assert len(f) == min(int(n), 100)
+                if merged != "fused":
+                    g_in = ft.detect_features([t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in dets],
+                                              seed=t)
+                    for d, f, n in zip(g_in, feats, tots):
+                        np.testing.assert_array_equal(t2d.points(d.features, d.num_features), f, err_msg=f"frame {t}")
+                        assert len(f) == min(int(n), 100)
             r_objs = ORC.backward_tracking(ring, [ORC.Rect(*b) for b in dets], feats)
             g_trk_in = [t2d.make_tracker([b.tuple() for b in tr.boxes], tr.features, tr.duration) for tr in trackers]
             r_cost = ORC.forward_tracking(ring, trackers, r_objs) if trackers else np.zeros((len(r_objs), 0), np.float32)
             g_det_in = [t2d.make_detection(b, f) for b, f in zip(dets, feats)]
-            if merged:
+            if merged == "fused":
+                g_box_in = [t2d.make_detection(b, np.zeros((0, 2), np.float32)) for b in dets]
+                g_dets, g_trk, g_cost = ft.track_frame_detect(g_box_in, g_trk_in, seed=t)
+                for d, f in zip(g_dets, feats):
+                    np.testing.assert_array_equal(t2d.points(d.features, d.num_features), f, err_msg=f"frame {t}")
+            elif merged:
                 g_dets, g_trk, g_cost = ft.track_frame(g_det_in, g_trk_in)
             else:
                 g_dets = ft.backward(g_det_in)
