@@ -140,13 +140,23 @@ struct Tracker2DFlow::DeviceBuffers {
     uint8_t *h_fwd_st = nullptr;
     double *h_boxes = nullptr, *h_obox = nullptr;
     int *h_cnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr, *h_rawcnt = nullptr;
+    // the chain's results live in one block per side, [nsteps | set counts | boxes | sets], so that
+    // one memset clears the counters and one copy returns every used byte
+    char *d_res = nullptr, *h_res = nullptr;
+    size_t res_sets_off = 0;
+    void carve(char *base, double *&obox, float *&sets, int *&setcnt, int *&nsteps, size_t K, size_t S) const {
+        nsteps = (int *)base;
+        setcnt = nsteps + K;
+        obox = (double *)(base + res_box_off(K, S));
+        sets = (float *)(base + res_sets_off);
+    }
+    static size_t res_box_off(size_t K, size_t S) { return (K * (1 + S) * 4 + 255) & ~(size_t)255; }
     void release() {
         for (void *p : {(void *)d_in, (void *)d_out, (void *)d_buf[0], (void *)d_buf[1], (void *)d_err, (void *)d_status,
-                        (void *)d_boxes, (void *)d_obox, (void *)d_sets, (void *)d_cnt, (void *)d_setcnt,
-                        (void *)d_nsteps, (void *)d_tot})
+                        (void *)d_boxes, (void *)d_res, (void *)d_cnt, (void *)d_tot})
             if (p) (void)hipFree(p);
-        for (void *p : {(void *)h_in, (void *)h_fwd_out, (void *)h_sets, (void *)h_fwd_st, (void *)h_boxes,
-                        (void *)h_obox, (void *)h_cnt, (void *)h_setcnt, (void *)h_nsteps, (void *)h_rawcnt})
+        for (void *p : {(void *)h_in, (void *)h_fwd_out, (void *)h_fwd_st, (void *)h_boxes, (void *)h_res,
+                        (void *)h_cnt, (void *)h_rawcnt})
             if (p) (void)hipHostFree(p);
         *this = DeviceBuffers();
     }
@@ -188,27 +198,25 @@ int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_job
     dm((void **)&b.d_err, npt * 4);
     dm((void **)&b.d_status, npt);
     dm((void **)&b.d_boxes, K * 4 * 8);
-    dm((void **)&b.d_obox, K * S * 4 * 8);
-    dm((void **)&b.d_sets, K * S * cap * 8);
+    b.res_sets_off = DeviceBuffers::res_box_off(K, S) + K * S * 4 * 8;
+    const size_t res_bytes = b.res_sets_off + K * S * cap * 8;
+    dm((void **)&b.d_res, res_bytes);
     dm((void **)&b.d_cnt, (K + J) * 4);
-    dm((void **)&b.d_setcnt, K * S * 4);
-    dm((void **)&b.d_nsteps, K * 4);
     dm((void **)&b.d_tot, K * 4);
     hm((void **)&b.h_in, npt * 8);
     hm((void **)&b.h_fwd_out, F * 8);
-    hm((void **)&b.h_sets, K * S * cap * 8);
     hm((void **)&b.h_fwd_st, F);
     hm((void **)&b.h_boxes, K * 4 * 8);
-    hm((void **)&b.h_obox, K * S * 4 * 8);
+    hm((void **)&b.h_res, res_bytes);
     hm((void **)&b.h_cnt, (K + J) * 4);
-    hm((void **)&b.h_setcnt, K * S * 4);
-    hm((void **)&b.h_nsteps, K * 4);
     hm((void **)&b.h_rawcnt, K * 4);
     if (!ok) {
         b.release();
         err_ = "device-chain buffers: allocation failed";
         return PSN_LK_ERR_NOMEM;
     }
+    b.carve(b.d_res, b.d_obox, b.d_sets, b.d_setcnt, b.d_nsteps, K, S);
+    b.carve(b.h_res, b.h_obox, b.h_sets, b.h_setcnt, b.h_nsteps, K, S);
     b.nchains = K;
     b.nfwd_pts = F;
     b.nfwd_jobs = J;
@@ -263,8 +271,7 @@ int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<Detect
     chk(hipMemcpyAsync(b.d_in, b.h_in, (K * cap + F) * 8, hipMemcpyHostToDevice, st), "chain inputs");
     chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, std::max<size_t>(K, 1) * 32, hipMemcpyHostToDevice, st), "chain boxes");
     chk(hipMemcpyAsync(b.d_cnt, b.h_cnt, (K + J) * 4, hipMemcpyHostToDevice, st), "chain counts");
-    chk(hipMemsetAsync(b.d_nsteps, 0, std::max<size_t>(K, 1) * 4, st), "chain steps");
-    chk(hipMemsetAsync(b.d_setcnt, 0, std::max<size_t>(K, 1) * S * 4, st), "chain set counts");
+    chk(hipMemsetAsync(b.d_nsteps, 0, b.nchains * (1 + S) * 4, st), "chain steps and set counts");
     if (rc) return rc;
     psn_t2d_chain_dev cd{};
     cd.ndet = (int)K;
@@ -336,10 +343,7 @@ int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<Detect
         if (rc) return fail(rc, "psn_t2d_chain_step_device");
     }
     if (K) {
-        chk(hipMemcpyAsync(b.h_nsteps, b.d_nsteps, K * 4, hipMemcpyDeviceToHost, st), "chain steps");
-        chk(hipMemcpyAsync(b.h_obox, b.d_obox, K * S * 32, hipMemcpyDeviceToHost, st), "chain boxes");
-        chk(hipMemcpyAsync(b.h_setcnt, b.d_setcnt, K * S * 4, hipMemcpyDeviceToHost, st), "chain set counts");
-        chk(hipMemcpyAsync(b.h_sets, b.d_sets, K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain sets");
+        chk(hipMemcpyAsync(b.h_res, b.d_res, b.res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain results");
     }
     chk(hipStreamSynchronize(st), "chain sync");
     chk(hipStreamSynchronize((hipStream_t)fwd_stream_), "forward sync");
@@ -770,8 +774,7 @@ int Tracker2DFlow::TrackFrameDetect(const std::vector<Detection> &dets, uint32_t
         chk(hipMemcpyAsync(b.h_in, b.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
         if (!rc) rc = psn_t2d_gate_counts_device(b.d_cnt, (int)K, (int)kT2dMinFeatures, st);
         chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
-        chk(hipMemsetAsync(b.d_nsteps, 0, K * 4, st), "chain steps");
-        chk(hipMemsetAsync(b.d_setcnt, 0, K * S * 4, st), "chain set counts");
+        chk(hipMemsetAsync(b.d_nsteps, 0, b.nchains * (1 + S) * 4, st), "chain steps and set counts");
         if (rc) return rc;
         psn_t2d_chain_dev cd{};
         cd.ndet = (int)K;
@@ -803,10 +806,7 @@ int Tracker2DFlow::TrackFrameDetect(const std::vector<Detection> &dets, uint32_t
             rc = psn_t2d_chain_step_device(&cd, step, st);
             if (rc) return fail(rc, "psn_t2d_chain_step_device");
         }
-        chk(hipMemcpyAsync(b.h_nsteps, b.d_nsteps, K * 4, hipMemcpyDeviceToHost, st), "chain steps");
-        chk(hipMemcpyAsync(b.h_obox, b.d_obox, K * S * 32, hipMemcpyDeviceToHost, st), "chain boxes");
-        chk(hipMemcpyAsync(b.h_setcnt, b.d_setcnt, K * S * 4, hipMemcpyDeviceToHost, st), "chain set counts");
-        chk(hipMemcpyAsync(b.h_sets, b.d_sets, K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain sets");
+        chk(hipMemcpyAsync(b.h_res, b.d_res, b.res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain results");
     }
     chk(hipStreamSynchronize(st), "chain sync");
     chk(hipStreamSynchronize(fs), "forward sync");
