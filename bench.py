@@ -306,7 +306,7 @@ def main():
                     help="ingest of frame t+1: serial on the LK stream, on a second stream, or fused "
                          "into the tail of frame t's LK launch (auto: fused for 1 camera per GPU, "
                          "stream for more)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01c_pmc_summary.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01f_pmc_summary.json"),
                     help="rocprofv3 FETCH/WRITE_SIZE summary (tools/profile_round.sh) for roofline.traffic")
     ap.add_argument("--tracker", action="store_true",
                     help="Tracker2D mode (box windows, GridFAST, chains; 1 GPU) instead of configs[1]")
