@@ -272,7 +272,9 @@ def tracker_main(args):
                    "parallelism": f"{C} camera(s) per GPU, one stream each" if C > 1 else "camera-per-GPU x1"},
         "roofline": {"kernel": "lk_kernel_bx (every LK launch of the timed frames)", "bound": "hbm",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": tracker_traffic(args.tracker_pmc_summary),
+                     "traffic_unit": "HBM bytes per camera-frame, all lk_kernel_bx launches",
+                     "traffic_source": os.path.relpath(args.tracker_pmc_summary, ROOT),
                      "bytes_per_camera_frame": int(lk_bytes / (C * args.steps)),
                      "lk_ms_per_camera_frame": round(lk_ms / (C * args.steps), 4), "lk_calls": calls},
         "features_per_camera_frame": round(sum(c.features for c in cams) / (C * args.steps), 1),
@@ -285,6 +287,19 @@ def tracker_main(args):
         out["speedup_vs_cpu"] = round(fps / out["cpu_baseline"]["value"], 1)
     print(json.dumps(out), flush=True)
 
+
+
+def tracker_traffic(path):
+    """PMC HBM bytes per camera-frame of every lk_kernel_bx launch (tools/pmc_summary.py output of a
+    --tracker run; one pyramid_kernel launch per camera-frame gives the frame count), or None."""
+    if not path or not os.path.exists(path):
+        return None
+    ks = json.load(open(path)).get("kernels", {})
+    frames = ks.get("pyramid_kernel", {}).get("dispatches", 0)
+    bx = [v for k, v in ks.items() if k.startswith("lk_kernel_bx")]
+    if not frames or not bx:
+        return None
+    return int(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in bx) / frames)
 
 def main():
     ap = argparse.ArgumentParser()
@@ -306,6 +321,9 @@ def main():
                     help="ingest of frame t+1: serial on the LK stream, on a second stream, or fused "
                          "into the tail of frame t's LK launch (auto: fused for 1 camera per GPU, "
                          "stream for more)")
+    ap.add_argument("--tracker-pmc-summary",
+                    default=os.path.join(ROOT, "profiles", "r01f_tracker_mode_pmc_summary.json"),
+                    help="--tracker: FETCH/WRITE_SIZE summary of a --tracker run for roofline.traffic")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01f_pmc_summary.json"),
                     help="rocprofv3 FETCH/WRITE_SIZE summary (tools/profile_round.sh) for roofline.traffic")
     ap.add_argument("--tracker", action="store_true",
