@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PSN_LK_ABI_VERSION 3
+#define PSN_LK_ABI_VERSION 4
 
 #define PSN_LK_OK 0
 #define PSN_LK_ERR_ARG (-1)
@@ -107,6 +107,16 @@ int psn_lk_sync(psn_lk_ctx *ctx);
 int psn_lk_push_frame(psn_lk_ctx *ctx, int slot, const uint8_t *host, int stride, int channels);
 int psn_lk_push_frame_device(psn_lk_ctx *ctx, int slot, const uint8_t *dev, int stride, int channels);
 
+/* Asynchronous host-frame ingest: the frame is copied (hipMemcpy2DAsync, a copy
+ * engine when `host` is pinned) into a staging buffer owned by `slot` and the
+ * pyramid is built from it, both on the context's ingest stream, after every
+ * LK / GridFAST launch that read the slot's previous frame; LK launches that
+ * read the slot wait for the build (slot events, as in STREAM overlap mode,
+ * whatever mode the context is in). Returns once enqueued: `host` must stay
+ * valid and unchanged until psn_lk_sync, or until a later call that reads the
+ * slot has completed. Used to overlap frame t+1's upload with frame t's LK. */
+int psn_lk_push_frame_async(psn_lk_ctx *ctx, int slot, const uint8_t *host, int stride, int channels);
+
 /* Ingest overlap modes (default OFF: builds run on the context stream).
  * STREAM: psn_lk_push_frame* builds the pyramid on the context's internal
  *   ingest stream, ordered only against earlier LK launches that read the same
@@ -165,6 +175,24 @@ int psn_lk_level_size(psn_lk_ctx *ctx, int level, int *w, int *h);
  * milliseconds, and resets. */
 int psn_lk_enable_timing(psn_lk_ctx *ctx, int capacity, int every);
 int psn_lk_timing_stats(psn_lk_ctx *ctx, int *n_push, double *push_ms, int *n_track, double *track_ms);
+
+/* Kernel-variant selection for tests and experiments (never read from the
+ * environment: a product context always runs the planner's choice). Applies
+ * to launches planned after the call. Results are identical in every variant.
+ *   PSN_LK_VARIANT_THREADS     0 = planner; 64/128/256 tiled-kernel workgroup,
+ *                              64..512 single-tile workgroup size
+ *   PSN_LK_VARIANT_GENERIC     1 = always the row-tiled kernel
+ *   PSN_LK_VARIANT_ONEWAVE     0 = multi-wave iterations in the single-tile kernel
+ *   PSN_LK_VARIANT_BOX         0 = box windows run the row-tiled kernel, not lk_kernel_bx
+ *   PSN_LK_VARIANT_TILED_LDS   LDS budget (bytes) of a row-tiled workgroup
+ *   PSN_LK_VARIANT_FUSED_HELPERS  tile-only workgroups per fused-ingest launch */
+#define PSN_LK_VARIANT_THREADS 1
+#define PSN_LK_VARIANT_GENERIC 2
+#define PSN_LK_VARIANT_ONEWAVE 3
+#define PSN_LK_VARIANT_BOX 4
+#define PSN_LK_VARIANT_TILED_LDS 5
+#define PSN_LK_VARIANT_FUSED_HELPERS 6
+int psn_lk_debug_set_variant(psn_lk_ctx *ctx, int key, int value);
 
 /* Diagnostic builds only (libpsn_lk_stamps.so, -DPSN_LK_STAMPS): record
  * shader-clock stamps of every LK workgroup's phases into a device buffer of

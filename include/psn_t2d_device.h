@@ -35,7 +35,10 @@ extern "C" {
  *   sets     [ndet][steps][cap][2], set_cnt [ndet][steps]
  *                            out: vecvecTrackedFeatures; step 1 writes row 0 (inliers at t)
  *                            and row 1, step s row s
- *   nsteps   [ndet]          out: last step that kept >= 4 inliers */
+ *   nsteps   [ndet]          out: last step that kept >= 4 inliers
+ *   last_step[ndet]          in, nullable: the chain's last step (the ring of the
+ *                            detection's camera holds frames back to t - last_step);
+ *                            at that step the count is cleared after the results */
 typedef struct psn_t2d_chain_dev {
     int ndet, cap;
     const double *boxes;
@@ -46,6 +49,7 @@ typedef struct psn_t2d_chain_dev {
     float *sets;
     int *set_cnt;
     int *nsteps;
+    const int *last_step;
 } psn_t2d_chain_dev;
 
 /* LocalSearchKLT + inlier compaction of chain step `step` (1..3) for every
@@ -53,8 +57,9 @@ typedef struct psn_t2d_chain_dev {
 int psn_t2d_chain_step_device(const psn_t2d_chain_dev *c, int step, void *hip_stream);
 
 /* d_cnt[i] = 0 where d_cnt[i] < min_count (the reference skips detections with
- * fewer than PSN_2D_FEATURE_MIN_NUM_TRACK features, :744), asynchronous. */
-int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, void *hip_stream);
+ * fewer than PSN_2D_FEATURE_MIN_NUM_TRACK features, :744) or where
+ * d_last_step[i] < 1 (nullable: no frame t-1 in that camera's ring), asynchronous. */
+int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -12,10 +12,16 @@
  * The LK calls of one frame are batched into as few launches as the chain
  * dependencies allow (backward step 1 and the forward calls share a launch).
  *
+ * After the flow: Track2D_MatchingAndUpdating (:1038-1164) -- the
+ * assignment, the tracker update and life cycle -- and ResultWithTracker
+ * (:1231-1257), which produce the stTrack2DResult handed to Associator3D.
+ * psn_t2d_group_* runs the whole per-frame CPSNWhere_Tracker2D::Run of several
+ * cameras (CPSNWhere::TrackPeople's camera loop, PSNWhere.cpp:257-266) with
+ * every camera's LK work batched into the same launches.
+ *
  * Out of this stage (the caller's, as in the reference): the detection height
- * gate (camera calibration, :711-715), GridFAST feature detection + shuffle
- * (:735-758; the caller passes each detection's points), the Hungarian
- * matching and tracker life cycle (:1038-1182).
+ * gate and the 3D location/height estimate (camera calibration, :711-718; the
+ * caller passes them in the detection records).
  *
  * Plain C, fixed-capacity records (the reference caps a detection at
  * PSN_2D_FEATURE_MAX_NUM_TRACK = 100 points, :13, and the chain at
@@ -38,6 +44,8 @@ extern "C" {
 #define PSN_T2D_MAX_BOXES 16     /* tracker box history kept in the C record */
 
 #define PSN_T2D_ERR_CAPACITY (-20) /* a fixed-capacity record would overflow */
+#define PSN_T2D_ABI_VERSION 2
+int psn_t2d_abi_version(void);
 
 /* PSN_Rect: double x, y, w, h (PSNWhere_Types.h:112) */
 typedef struct psn_rect {
@@ -84,6 +92,9 @@ int psn_t2d_rotate(psn_t2d *t);
 /* stDetectedObject of the backward chain (PSNWhere_Tracker2D.h:17-29). */
 typedef struct psn_t2d_detection {
     psn_rect box;                                   /* in: detection box (height-validated) */
+    psn_rect head;                                  /* in: stDetection::vecPartBoxes.front() (tracker heads) */
+    double location[3];                             /* in: 3D foot location (EstimateDetectionHeight, :711-718) */
+    double height;                                  /* in: 3D height, mm */
     int num_features;                               /* in: points at t after shuffle + cap */
     float features[PSN_T2D_MAX_FEATURES][2];        /* in */
     int valid;                                      /* out: >= 4 points (kept in m_vecDetection2D) */
@@ -95,17 +106,47 @@ typedef struct psn_t2d_detection {
     float sets[PSN_T2D_INTERVAL][PSN_T2D_MAX_FEATURES][2];
 } psn_t2d_detection;
 
-/* stTracker2D fields the forward step reads and writes (.h:31-47). */
+/* stTracker2D (.h:31-47): the fields the forward step and the update read and write. */
 typedef struct psn_t2d_tracker {
+    unsigned id;                                    /* m_nNewTrackerID at creation (:1119) */
+    unsigned time_start, time_end, time_last_update;
     unsigned duration;                              /* in */
     int num_boxes;                                  /* in/out: box history, oldest first */
     psn_rect boxes[PSN_T2D_MAX_BOXES];
+    psn_rect heads[PSN_T2D_MAX_BOXES];              /* in/out: one per box; the forward step repeats the last (:896) */
+    double last_position[3];                        /* lastPosition (the matched detection's location) */
+    double height;
+    double confidence;
     int num_features;                               /* in/out: featurePoints */
     float features[PSN_T2D_MAX_FEATURES][2];
     int num_tracked;                                /* out: trackedPoints */
     float tracked[PSN_T2D_MAX_FEATURES][2];
     int updated;                                    /* out: >= 4 points tracked, box pushed */
 } psn_t2d_tracker;
+
+/* ---- stTrack2DResult: the Tracker2D -> Associator3D hand-off ----
+ * stObject2DInfo (PSNWhere_Types.h:190-198) and stTrack2DResult (:200-209)
+ * as plain C records with caller-owned arrays (cap_* = capacity, used by the
+ * readers; matMatchingCost is not part of either format). */
+typedef struct psn_object2d {
+    unsigned id;
+    psn_rect box, head;
+    double score;
+    int num_prev;                                   /* featurePointsPrev */
+    float prev[PSN_T2D_MAX_FEATURES][2];
+    int num_curr;                                   /* featurePointsCurr */
+    float curr[PSN_T2D_MAX_FEATURES][2];
+} psn_object2d;
+
+typedef struct psn_track2d_result {
+    unsigned cam_id, frame_idx;
+    int num_objects, cap_objects;
+    psn_object2d *objects;
+    int num_detection_rects, cap_detection_rects;
+    psn_rect *detection_rects;
+    int num_tracker_rects, cap_tracker_rects;
+    psn_rect *tracker_rects;
+} psn_track2d_result;
 
 /* Feature extraction of the backward chain (PSNWhere_Tracker2D.cpp:734-757) on
  * frame t (call after psn_t2d_push_frame): GridFAST (psn_gridfast_detect with
@@ -137,29 +178,34 @@ int psn_t2d_track_frame(psn_t2d *t, psn_t2d_detection *dets, int ndet, psn_t2d_t
 int psn_t2d_track_frame_detect(psn_t2d *t, psn_t2d_detection *dets, int ndet, uint32_t seed, psn_t2d_tracker *trk,
                                int ntrk, float *cost);
 
-/* ---- stTrack2DResult: the Tracker2D -> Associator3D hand-off ----
- * stObject2DInfo (PSNWhere_Types.h:190-198) and stTrack2DResult (:200-209)
- * as plain C records with caller-owned arrays (cap_* = capacity, used by the
- * readers; matMatchingCost is not part of either format). */
-typedef struct psn_object2d {
-    unsigned id;
-    psn_rect box, head;
-    double score;
-    int num_prev;                                   /* featurePointsPrev */
-    float prev[PSN_T2D_MAX_FEATURES][2];
-    int num_curr;                                   /* featurePointsCurr */
-    float curr[PSN_T2D_MAX_FEATURES][2];
-} psn_object2d;
+/* ---- after the flow: matching, tracker update, result (:1038-1164, :1231-1257) ---- */
 
-typedef struct psn_track2d_result {
-    unsigned cam_id, frame_idx;
-    int num_objects, cap_objects;
-    psn_object2d *objects;
-    int num_detection_rects, cap_detection_rects;
-    psn_rect *detection_rects;
-    int num_tracker_rects, cap_tracker_rects;
-    psn_rect *tracker_rects;
-} psn_track2d_result;
+/* The assignment of Track2D_MatchingAndUpdating (:1040-1064 + CPSNWhere_Hungarian::Match):
+ * cost = [rows x cols] row-major (the forward step's matchingCostArray);
+ * non-finite entries become max(finite) + 100, a minimum-total-cost matching of
+ * min(rows, cols) pairs is taken, and pairs at that substitute cost are dropped.
+ * match[r] = the column matched to row r, or -1. Exact when the optimum is
+ * unique (ties may be broken differently from the reference's Munkres). */
+int psn_t2d_assign(const float *cost, int rows, int cols, int *match);
+
+/* ResultWithTracker (:1231-1257): id, last box and head, score 0,
+ * featurePointsPrev = features, featurePointsCurr = tracked. */
+int psn_t2d_result_with_tracker(const psn_t2d_tracker *trk, psn_object2d *out);
+
+/* Track2D_MatchingAndUpdating (:1038-1164) on caller-owned records: dets =
+ * the backward step's records (the valid ones are m_vecDetection2D, in order),
+ * trk = m_queueActiveTracker2D after psn_t2d_forward, cost = its [valid dets x
+ * ntrk] matrix, match = per valid detection the tracker index or -1 (NULL:
+ * psn_t2d_assign(cost)). Validation (3D distance <= 600 mm, height difference
+ * <= 400 mm, duration <= 3) uses the records' location / height. out_trk
+ * receives the new active queue (matched trackers in detection order, then
+ * one new tracker per unmatched valid detection, ids from *next_id);
+ * result->objects the packed objects in the same order (result capacity
+ * cap_objects), result->frame_idx = frame_idx, no detection / tracker rects
+ * (the reference never fills them). */
+int psn_t2d_matching_and_updating(const psn_t2d_detection *dets, int ndet, const psn_t2d_tracker *trk, int ntrk,
+                                  const float *cost, const int *match, unsigned frame_idx, unsigned *next_id,
+                                  psn_t2d_tracker *out_trk, int cap_trk, int *n_out, psn_track2d_result *result);
 
 /* CPSNWhere_Tracker2D::FilePrintResult (PSNWhere_Tracker2D.cpp:1268-1334):
  * writes <dir>/track2D_result_cam%d_frame%04d.txt in the reference's text
@@ -170,6 +216,39 @@ int psn_t2d_write_result_txt(const char *dir, const psn_track2d_result *r);
  * file (values pass through float, as the reference's fscanf "%f" does).
  * Returns 0, PSN_LK_ERR_ARG (cannot open / malformed) or PSN_T2D_ERR_CAPACITY. */
 int psn_t2d_read_result_txt(const char *dir, unsigned cam_id, unsigned frame_idx, psn_track2d_result *r);
+
+/* ---- CPSNWhere_Tracker2D::Run over several cameras, batched ----
+ * One group = C cameras on one device (camera c = index c, cam_ids[c] its
+ * camID). Per frame:
+ *   psn_t2d_group_push_frame(g, c, frame t)    for every camera (async upload)
+ *   psn_t2d_group_launch(g, t, dets, ...)      enqueue the frame's device work
+ *   [psn_t2d_group_push_frame(g, c, frame t+1) may overlap it here]
+ *   psn_t2d_group_complete(g, dets, results)   wait; matching, update, results
+ * (psn_t2d_group_run = launch + complete). dets[c] / ndet[c]: camera c's
+ * height-validated detections with head box and 3D estimate; with
+ * PSN_T2D_FEATURES_GIVEN their features (after shuffle + cap), with
+ * PSN_T2D_FEATURES_GRIDFAST the group runs GridFAST on the device and writes
+ * them. The backward outputs are written into dets as psn_t2d_track_frame does;
+ * results[c] receives camera c's stTrack2DResult (caller-owned arrays). The
+ * dets arrays must stay valid from launch to complete; host frames until the
+ * next complete (pinned memory makes the upload asynchronous). */
+typedef struct psn_t2d_group psn_t2d_group;
+#define PSN_T2D_FEATURES_GIVEN 0
+#define PSN_T2D_FEATURES_GRIDFAST 1
+int psn_t2d_group_create(int device, int ncams, const unsigned *cam_ids, int width, int height, psn_t2d_group **out);
+void psn_t2d_group_destroy(psn_t2d_group *g);
+const char *psn_t2d_group_last_error(psn_t2d_group *g);
+void *psn_t2d_group_lk_context(psn_t2d_group *g);
+int psn_t2d_group_push_frame(psn_t2d_group *g, int cam, const uint8_t *frame, int stride, int channels);
+int psn_t2d_group_push_frame_device(psn_t2d_group *g, int cam, const uint8_t *dev_frame, int stride, int channels);
+int psn_t2d_group_launch(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *const *dets, const int *ndet,
+                         int feature_mode, uint32_t seed);
+int psn_t2d_group_complete(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,
+                           psn_track2d_result *results);
+int psn_t2d_group_run(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *const *dets, const int *ndet,
+                      int feature_mode, uint32_t seed, psn_track2d_result *results);
+/* camera c's active trackers (m_queueActiveTracker2D) after the last complete */
+int psn_t2d_group_trackers(psn_t2d_group *g, int cam, psn_t2d_tracker *out, int cap, int *n);
 
 /* Fixed-size binary slot of one camera's result for the per-frame RCCL
  * all-gather into Associator3D (psn_comm_allgather, psn_lk.h): exact (no

@@ -36,6 +36,8 @@ TERM_COUNT = 1
 TERM_EPS = 2
 MAX_WIN_PIXELS = 16384
 COMM_UNIQUE_ID_BYTES = 128
+# psn_lk_debug_set_variant keys (tests / experiments; never read from the environment)
+VARIANTS = {"threads": 1, "generic": 2, "onewave": 3, "box": 4, "tiled_lds": 5, "fused_helpers": 6}
 
 
 class PsnLkError(RuntimeError):
@@ -111,6 +113,8 @@ def load():
     L.psn_lk_sync.argtypes = [vp]
     L.psn_lk_push_frame.argtypes = [vp, ip, u8p, ip, ip]
     L.psn_lk_push_frame_device.argtypes = [vp, ip, vp, ip, ip]
+    L.psn_lk_push_frame_async.argtypes = [vp, ip, u8p, ip, ip]
+    L.psn_lk_debug_set_variant.argtypes = [vp, ip, ip]
     L.psn_lk_track.argtypes = [vp, ctypes.POINTER(LkQuery), ip, fp, fp, u8p, fp]
     L.psn_lk_track_device.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp]
     L.psn_lk_track_device_counted.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp, vp]

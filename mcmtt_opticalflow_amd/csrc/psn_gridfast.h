@@ -32,5 +32,6 @@ struct GridFastArgs {
 int gridfast_lds_bytes(int rw_max, int strip, int list_cap);
 // Both launches (per-cell detection, per-roi selection) on stream s.
 hipError_t launch_gridfast(const GridFastArgs &a, hipStream_t s);
+hipError_t gridfast_kernels_init();
 
 }  // namespace psn

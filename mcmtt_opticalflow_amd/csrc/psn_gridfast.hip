@@ -385,15 +385,14 @@ int gridfast_lds_bytes(int rw_max, int strip, int list_cap) {
     return (strip + 8) * pc + (((strip + 2) * sc + 15) & ~15) + ((strip * rw_max + 15) & ~15) + 4 * list_cap;
 }
 
+// Raises the per-cell kernel's dynamic-LDS limit on the current device; called
+// by lk_kernels_init at every context creation (per device, no shared state).
+hipError_t gridfast_kernels_init() {
+    return hipFuncSetAttribute((const void *)gridfast_cell_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kGfMaxLds);
+}
+
 hipError_t launch_gridfast(const GridFastArgs &a, hipStream_t s) {
     if (a.nroi <= 0) return hipSuccess;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)gridfast_cell_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           kGfMaxLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
     const int lds = gridfast_lds_bytes(a.rw_max, a.strip, a.list_cap);
     hipLaunchKernelGGL(gridfast_cell_kernel, dim3(a.grid_rows * a.grid_cols, a.nroi), dim3(kGfThreads), lds, s, a);
     hipError_t e = hipGetLastError();

@@ -29,7 +29,10 @@ struct psn_lk_ctx {
     int nlevels = 0;                 // max_level_cap + 1
     hipStream_t own_stream = nullptr, stream = nullptr;
     // ingest overlap: pyramid builds on their own stream, ordered against the
-    // LK launches by per-slot events (ready after a build, free after a read)
+    // LK launches by per-slot events: ready after every build (waited for by
+    // every launch that reads the slot, on whatever stream it runs), free after
+    // the reads (one event per reading stream, all waited for by the next build
+    // into the slot)
     hipStream_t ingest_stream = nullptr;
     int overlap = PSN_LK_OVERLAP_OFF;
     // PSN_LK_OVERLAP_FUSED: the last pushed build is deferred and run inside
@@ -38,10 +41,15 @@ struct psn_lk_ctx {
     int pend_slot = -1;
     psn::PyrBuildArgs pend_args{};
     unsigned *d_ctr = nullptr;  // [2] fused-build work counter + finished workgroups
-    int fused_helpers = 0;      // PSN_LK_FUSED_HELPERS: tile-only workgroups per fused launch
+    int fused_helpers = 0;      // FUSED_HELPERS variant: tile-only workgroups per fused launch
     psn::RingGeo ring{};        // slot/level geometry passed to the single-tile kernel
-    std::vector<hipEvent_t> slot_ready, slot_free;
-    std::vector<char> ready_rec, free_rec;
+    std::vector<hipEvent_t> slot_ready;
+    std::vector<char> ready_rec;
+    std::vector<std::vector<std::pair<hipStream_t, hipEvent_t>>> slot_free;
+    // psn_lk_push_frame_async: per-slot staging buffer of the uploaded frame
+    std::vector<uint8_t *> d_stage;
+    std::vector<size_t> stage_cap;
+    std::vector<int> used_slots;  // scratch of track_device_impl
     uint8_t *d_pyr = nullptr;
     LevelDev *d_slots = nullptr;
     std::vector<LevelDev> h_slots;  // [nslots][kMaxLevels]
@@ -52,13 +60,13 @@ struct psn_lk_ctx {
     float *d_prev = nullptr, *d_next = nullptr, *d_err = nullptr;
     uint8_t *d_status = nullptr;
     size_t d_pts_cap = 0;
-    // tuning / test overrides read at create time: PSN_LK_THREADS=64|128|256,
-    // PSN_LK_GENERIC=1 (always the tiled kernel)
+    // kernel-variant overrides (psn_lk_debug_set_variant; tests and experiments only):
+    // THREADS = workgroup size, GENERIC = always the tiled kernel
     int force_threads = 0;
     bool force_generic = false;
-    bool onewave = true;  // PSN_LK_ONEWAVE=0: multi-wave iterations in the single-tile kernel
-    bool box = true;      // PSN_LK_BOX=0: box windows run the row-tiled kernel instead of lk_kernel_bx
-    // PSN_LK_TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
+    bool onewave = true;  // ONEWAVE 0: multi-wave iterations in the single-tile kernel
+    bool box = true;      // BOX 0: box windows run the row-tiled kernel instead of lk_kernel_bx
+    // TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
     // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
     int tiled_lds = 76 * 1024;
     int num_cus = 256;  // compute units of the device (launch shaping)
@@ -81,13 +89,13 @@ struct psn_lk_ctx {
 };
 
 static int set_err(psn_lk_ctx *c, int code, const char *fmt, ...);
-static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s);
+static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s, int slot);
 
 // Run a deferred (fused-mode) build now, as its own launch on the LK stream.
 static int flush_pending(psn_lk_ctx *c) {
     if (!c->pend) return PSN_LK_OK;
     c->pend = false;
-    return launch_build(c, c->pend_args, c->stream);
+    return launch_build(c, c->pend_args, c->stream, c->pend_slot);
 }
 
 static int set_err(psn_lk_ctx *c, int code, const char *fmt, ...) {
@@ -101,6 +109,9 @@ static int set_err(psn_lk_ctx *c, int code, const char *fmt, ...) {
     }
     return code;
 }
+
+// slot events only order streams of one device: a device-scope release suffices
+static const unsigned kSlotEventFlags = hipEventDisableTiming | hipEventReleaseToDevice;
 
 #define HIPCHK(c, expr)                                                                       \
     do {                                                                                      \
@@ -150,17 +161,11 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     c->user_slots = ring_slots;
     c->nslots = ring_slots + 2;
     c->nlevels = max_level_cap + 1;
-    if (const char *e = getenv("PSN_LK_THREADS")) c->force_threads = atoi(e);
-    if (const char *e = getenv("PSN_LK_GENERIC")) c->force_generic = atoi(e) != 0;
-    if (const char *e = getenv("PSN_LK_ONEWAVE")) c->onewave = atoi(e) != 0;
-    if (const char *e = getenv("PSN_LK_BOX")) c->box = atoi(e) != 0;
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
             c->num_cus = cus;
     }
-    if (const char *e = getenv("PSN_LK_TILED_LDS")) c->tiled_lds = std::max(16 * 1024, std::min(atoi(e), 160 * 1024 - 1024));
-    if (const char *e = getenv("PSN_LK_FUSED_HELPERS")) c->fused_helpers = std::max(0, atoi(e));
     auto fail = [&](int rc) {
         psn_lk_destroy(c);
         return rc;
@@ -210,15 +215,12 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
         return fail(PSN_LK_ERR_HIP);
     c->filled.assign(c->nslots, 0);
     c->slot_ready.assign(c->nslots, nullptr);
-    c->slot_free.assign(c->nslots, nullptr);
+    c->slot_free.assign(c->nslots, {});
     c->ready_rec.assign(c->nslots, 0);
-    c->free_rec.assign(c->nslots, 0);
-    // slot events only order two streams of one device: a device-scope release suffices
-    const unsigned evf = hipEventDisableTiming | hipEventReleaseToDevice;
-    for (int i = 0; i < c->nslots; i++) {
-        if (hipEventCreateWithFlags(&c->slot_ready[i], evf) != hipSuccess) return fail(PSN_LK_ERR_HIP);
-        if (hipEventCreateWithFlags(&c->slot_free[i], evf) != hipSuccess) return fail(PSN_LK_ERR_HIP);
-    }
+    c->d_stage.assign(c->nslots, nullptr);
+    c->stage_cap.assign(c->nslots, 0);
+    for (int i = 0; i < c->nslots; i++)
+        if (hipEventCreateWithFlags(&c->slot_ready[i], kSlotEventFlags) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     *out = c;
     return PSN_LK_OK;
 }
@@ -230,9 +232,13 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->ingest_stream) (void)hipStreamSynchronize(c->ingest_stream);
-    for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready, &c->slot_free})
+    for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready})
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
+    for (auto &v : c->slot_free)
+        for (auto &se : v) (void)hipEventDestroy(se.second);
+    for (uint8_t *p : c->d_stage)
+        if (p) (void)hipFree(p);
     for (void *p : {(void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status, (void *)c->d_gf_kp, (void *)c->d_gf_cnt, (void *)c->d_gf_xy,
                     (void *)c->d_gf_oc, (void *)c->d_gf_ot})
@@ -331,8 +337,9 @@ int psn_lk_level_size(psn_lk_ctx *c, int level, int *w, int *h) {
     return PSN_LK_OK;
 }
 
-// One standalone pyramid launch on stream s (timed when timing is enabled).
-static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s) {
+// One standalone pyramid launch of `slot` on stream s (timed when timing is
+// enabled); the slot's ready event is recorded after it.
+static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s, int slot) {
     const bool timed = c->tcap && (c->calls_push++ % c->every) == 0;
     const long ti = timed ? (c->n_push % c->tcap) : 0;
     if (timed) HIPCHK(c, hipEventRecord(c->ev_push[2 * ti], s));
@@ -341,21 +348,43 @@ static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s
         HIPCHK(c, hipEventRecord(c->ev_push[2 * ti + 1], s));
         c->n_push++;
     }
+    HIPCHK(c, hipEventRecord(c->slot_ready[slot], s));
+    c->ready_rec[slot] = 1;
     return PSN_LK_OK;
 }
 
-// Make the LK stream wait for a build of `slot` running on the ingest stream.
+// Make the current stream wait for the last build of `slot` (a no-op on the
+// device when the build ran earlier on the same stream or has completed).
 static int wait_slot_ready(psn_lk_ctx *c, int slot) {
-    if (slot >= 0 && slot < c->nslots && c->ready_rec[slot]) {
+    if (slot >= 0 && slot < c->nslots && c->ready_rec[slot])
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot_ready[slot], 0));
-        c->ready_rec[slot] = 0;
-    }
     return PSN_LK_OK;
 }
 
-static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
-    int rc = flush_pending(c);  // at most one deferred build
-    if (rc) return rc;
+// After a launch on the current stream read `slot`: record that stream's free event.
+static int record_slot_free(psn_lk_ctx *c, int slot) {
+    if (slot < 0 || slot >= c->nslots) return PSN_LK_OK;
+    for (auto &se : c->slot_free[slot])
+        if (se.first == c->stream) {
+            HIPCHK(c, hipEventRecord(se.second, c->stream));
+            return PSN_LK_OK;
+        }
+    hipEvent_t e = nullptr;
+    HIPCHK(c, hipEventCreateWithFlags(&e, kSlotEventFlags));
+    c->slot_free[slot].emplace_back(c->stream, e);
+    HIPCHK(c, hipEventRecord(e, c->stream));
+    return PSN_LK_OK;
+}
+
+// Make stream s wait until every recorded read of `slot` is done (before a new build into it).
+static int wait_slot_free(psn_lk_ctx *c, int slot, hipStream_t s) {
+    for (auto &se : c->slot_free[slot])
+        if (se.first != s) HIPCHK(c, hipStreamWaitEvent(s, se.second, 0));
+    return PSN_LK_OK;
+}
+
+// Pyramid-build arguments of `slot` from a device source frame.
+static psn::PyrBuildArgs build_args(const psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
     psn::PyrBuildArgs a{};
     a.src = dev;
     a.src_stride = stride;
@@ -363,28 +392,51 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
     a.nlevels = c->nlevels;
     a.tile = (c->nlevels - 1) <= 4 ? 8 : 4;
     for (int l = 0; l < c->nlevels; l++) a.lv[l] = c->h_slots[(size_t)slot * psn::kMaxLevels + l];
+    return a;
+}
+
+static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
+    int rc = flush_pending(c);  // at most one deferred build
+    if (rc) return rc;
+    const psn::PyrBuildArgs a = build_args(c, slot, dev, stride, channels);
     c->filled[slot] = 1;
     if (c->overlap == PSN_LK_OVERLAP_FUSED && c->nlevels > 1) {
-        c->ready_rec[slot] = 0;
+        c->ready_rec[slot] = 0;  // readers wait for the build by stream order (it runs first on the LK stream)
         c->pend = true;
         c->pend_slot = slot;
         c->pend_args = a;
         return PSN_LK_OK;
     }
     hipStream_t s = c->stream;
-    if (c->overlap == PSN_LK_OVERLAP_STREAM) {  // build on the ingest stream once the slot's last readers are done
-        s = c->ingest_stream;
-        if (c->free_rec[slot]) HIPCHK(c, hipStreamWaitEvent(s, c->slot_free[slot], 0));
-    }
-    rc = launch_build(c, a, s);
+    if (c->overlap == PSN_LK_OVERLAP_STREAM) s = c->ingest_stream;  // once the slot's last readers are done
+    rc = wait_slot_free(c, slot, s);
     if (rc) return rc;
-    if (c->overlap == PSN_LK_OVERLAP_STREAM) {
-        HIPCHK(c, hipEventRecord(c->slot_ready[slot], s));
-        c->ready_rec[slot] = 1;
-    } else {
-        c->ready_rec[slot] = 0;
+    return launch_build(c, a, s, slot);
+}
+
+int psn_lk_push_frame_async(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, int channels) {
+    if (!c || !host || (channels != 1 && channels != 3) || stride < c->width * channels) return PSN_LK_ERR_ARG;
+    if (slot < 0 || slot >= c->user_slots) return set_err(c, PSN_LK_ERR_SLOT, "slot %d out of range", slot);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc = flush_pending(c);
+    if (rc) return rc;
+    const size_t row = (size_t)c->width * channels, need = row * c->height;
+    if (c->stage_cap[slot] < need) {
+        HIPCHK(c, hipStreamSynchronize(c->ingest_stream));  // the old buffer may still be read
+        if (c->d_stage[slot]) (void)hipFree(c->d_stage[slot]);
+        c->d_stage[slot] = nullptr;
+        c->stage_cap[slot] = 0;
+        HIPCHK(c, hipMalloc(&c->d_stage[slot], need));
+        c->stage_cap[slot] = need;
     }
-    return PSN_LK_OK;
+    hipStream_t s = c->ingest_stream;
+    // the staging buffer is read only by this slot's previous build, which
+    // precedes every read of the slot that wait_slot_free orders against
+    rc = wait_slot_free(c, slot, s);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpy2DAsync(c->d_stage[slot], row, host, stride, row, c->height, hipMemcpyHostToDevice, s));
+    c->filled[slot] = 1;
+    return launch_build(c, build_args(c, slot, c->d_stage[slot], (int)row, channels), s, slot);
 }
 
 int psn_lk_push_frame_device(psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
@@ -409,7 +461,6 @@ static int push_host_impl(psn_lk_ctx *c, int slot, const uint8_t *host, int stri
     const int mode = c->overlap;
     if (mode == PSN_LK_OVERLAP_FUSED) c->overlap = PSN_LK_OVERLAP_OFF;
     hipStream_t s = c->overlap == PSN_LK_OVERLAP_STREAM ? c->ingest_stream : c->stream;
-    if (c->overlap == PSN_LK_OVERLAP_STREAM && c->free_rec[slot]) HIPCHK(c, hipStreamWaitEvent(s, c->slot_free[slot], 0));
     hipError_t ce = hipMemcpy2DAsync(c->d_src, row, host, stride, row, c->height, hipMemcpyHostToDevice, s);
     int rc = ce == hipSuccess ? push_device_impl(c, slot, c->d_src, (int)row, channels)
                               : set_err(c, PSN_LK_ERR_HIP, "hipMemcpy2DAsync: %s", hipGetErrorString(ce));
@@ -515,15 +566,19 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
     }
     // slots built on the ingest stream must be complete before the LK reads them;
     // a deferred build of a slot this call reads runs first, as its own launch
+    std::vector<int> &used = c->used_slots;  // distinct slots this call reads
+    used.clear();
     for (int i = 0; i < nq; i++)
-        for (int sl : {q[i].prev_slot, q[i].next_slot}) {
-            if (c->pend && sl == c->pend_slot) {
-                int rc = flush_pending(c);
-                if (rc) return rc;
-            }
-            int rc = wait_slot_ready(c, sl);
+        for (int sl : {q[i].prev_slot, q[i].next_slot})
+            if (std::find(used.begin(), used.end(), sl) == used.end()) used.push_back(sl);
+    for (int sl : used) {
+        if (c->pend && sl == c->pend_slot) {
+            int rc = flush_pending(c);
             if (rc) return rc;
         }
+        int rc = wait_slot_ready(c, sl);
+        if (rc) return rc;
+    }
     const bool timed = c->tcap && (c->calls_track++ % c->every) == 0;
     const long ti = timed ? (c->n_track % c->tcap) : 0;
     if (timed) HIPCHK(c, hipEventRecord(c->ev_track[2 * ti], c->stream));
@@ -589,6 +644,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                 if (oept == 2 && E <= 8 && lds_ow <= 53 * 1024 && wgs > 2 * c->num_cus) threads += 200000;
             }
         }
+        int fused_slot = -1;
         if (c->pend && all_single) {  // fuse the deferred build into this launch's tail
             int tx, ty, plds;
             psn::pyramid_grid(c->pend_args, tx, ty, plds);
@@ -604,6 +660,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             wgs += helpers;
             lds = std::max(lds, psn::kStScratchBytes + plds);
             c->pend = false;
+            fused_slot = c->pend_slot;
         } else if (c->pend) {
             int rc = flush_pending(c);
             if (rc) return rc;
@@ -635,6 +692,10 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             }
         }
         HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, all_single, c->stream));
+        if (fused_slot >= 0) {  // readers on other streams wait for the launch that built it
+            HIPCHK(c, hipEventRecord(c->slot_ready[fused_slot], c->stream));
+            c->ready_rec[fused_slot] = 1;
+        }
     }
     if (c->pend) {  // no launch took it (no points)
         int rc = flush_pending(c);
@@ -644,13 +705,10 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         HIPCHK(c, hipEventRecord(c->ev_track[2 * ti + 1], c->stream));
         c->n_track++;
     }
-    if (c->overlap == PSN_LK_OVERLAP_STREAM)  // the next build into these slots waits for this launch
-        for (int i = 0; i < nq; i++)
-            for (int sl : {q[i].prev_slot, q[i].next_slot})
-                if (sl >= 0 && sl < c->nslots) {
-                    HIPCHK(c, hipEventRecord(c->slot_free[sl], c->stream));
-                    c->free_rec[sl] = 1;
-                }
+    for (int sl : used) {  // the next build into these slots waits for this launch
+        int rc = record_slot_free(c, sl);
+        if (rc) return rc;
+    }
     return PSN_LK_OK;
 }
 
@@ -741,6 +799,22 @@ int psn_calc_optical_flow_pyr_lk(psn_lk_ctx *c, const uint8_t *prev_img, const u
     q.num_pts = npts;
     q.params = p;
     return track_host_impl(c, &q, 1, prev_pts, next_pts, status, err, true);
+}
+
+int psn_lk_debug_set_variant(psn_lk_ctx *c, int key, int value) {
+    if (!c) return PSN_LK_ERR_ARG;
+    switch (key) {
+    case PSN_LK_VARIANT_THREADS:
+        if (value != 0 && value != 64 && value != 128 && value != 256 && value != 512) return PSN_LK_ERR_ARG;
+        c->force_threads = value;
+        return PSN_LK_OK;
+    case PSN_LK_VARIANT_GENERIC: c->force_generic = value != 0; return PSN_LK_OK;
+    case PSN_LK_VARIANT_ONEWAVE: c->onewave = value != 0; return PSN_LK_OK;
+    case PSN_LK_VARIANT_BOX: c->box = value != 0; return PSN_LK_OK;
+    case PSN_LK_VARIANT_TILED_LDS: c->tiled_lds = std::max(16 * 1024, std::min(value, 160 * 1024 - 1024)); return PSN_LK_OK;
+    case PSN_LK_VARIANT_FUSED_HELPERS: c->fused_helpers = std::max(0, value); return PSN_LK_OK;
+    default: return PSN_LK_ERR_ARG;
+    }
 }
 
 int psn_lk_debug_set_stamps(psn_lk_ctx *c, void *d_stamps) {
@@ -862,11 +936,7 @@ static int gridfast_impl(psn_lk_ctx *c, int slot, const int *rois, int nroi, con
         }
         HIPCHK(c, psn::launch_gridfast(a, c->stream));
     }
-    if (c->overlap == PSN_LK_OVERLAP_STREAM) {  // a later build into this slot waits for these reads
-        HIPCHK(c, hipEventRecord(c->slot_free[slot], c->stream));
-        c->free_rec[slot] = 1;
-    }
-    return PSN_LK_OK;
+    return record_slot_free(c, slot);  // a later build into this slot waits for these reads
 }
 
 int psn_gridfast_detect_device(psn_lk_ctx *c, int slot, const int *rois, int nroi, const psn_gridfast_params *p,

@@ -20,6 +20,7 @@
 #include <float.h>
 #include <limits.h>
 
+#include "psn_gridfast.h"
 #include "psn_lk_kernels.h"
 
 namespace psn {
@@ -3231,7 +3232,7 @@ hipError_t lk_kernels_init() {
                         (const void *)lk_kernel_bx<12>};
     for (const void *f : bx)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
-    return hipSuccess;
+    return gridfast_kernels_init();
 }
 
 }  // namespace psn

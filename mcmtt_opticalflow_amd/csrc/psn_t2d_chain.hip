@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kLanes) void chain_step_kernel(psn_t2d_chain_dev C,
         ob[1] = by + esty;
         ob[2] = bw;
         ob[3] = bh;
-        C.cnt[k] = ninl;
+        C.cnt[k] = (C.last_step && step >= C.last_step[k]) ? 0 : ninl;  // no older frame: the chain ends
         C.nsteps[k] = step;
         if (step == 1) C.set_cnt[k * S] = ninl;
         C.set_cnt[k * S + step] = ninl;
@@ -166,19 +166,19 @@ __global__ __launch_bounds__(kLanes) void chain_step_kernel(psn_t2d_chain_dev C,
 
 // Detections whose feature count fails the reference's minimum (:744) get no
 // chain: their count becomes 0, so their workgroups exit at once.
-__global__ void gate_counts_kernel(int *cnt, int n, int min_count) {
+__global__ void gate_counts_kernel(int *cnt, int n, int min_count, const int *last_step) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && cnt[i] < min_count) cnt[i] = 0;
+    if (i < n && (cnt[i] < min_count || (last_step && last_step[i] < 1))) cnt[i] = 0;
 }
 
 }  // namespace
 }  // namespace psn
 
-extern "C" int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, void *stream) {
+extern "C" int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *stream) {
     if (n < 0 || (n > 0 && !d_cnt)) return PSN_LK_ERR_ARG;
     if (n == 0) return PSN_LK_OK;
     hipLaunchKernelGGL(psn::gate_counts_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_cnt, n,
-                       min_count);
+                       min_count, d_last_step);
     return hipGetLastError() == hipSuccess ? PSN_LK_OK : PSN_LK_ERR_HIP;
 }
 

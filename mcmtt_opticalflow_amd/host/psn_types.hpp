@@ -61,7 +61,12 @@ struct Rect {  // PSN_Rect (PSNWhere_Types.h:112-182)
 
 struct Detection {  // stDetection
     Rect box;
-    std::vector<Rect> vecPartBoxes;
+    std::vector<Rect> vecPartBoxes;  // .front() = the head box (PETS part boxes)
+    // the caller's 3D estimate of the detection (EstimateDetectionHeight with the
+    // camera calibration, PSNWhere_Tracker2D.cpp:711-718; calibration is not on
+    // the flow path): stDetectedObject::location / height
+    double location[3] = {0, 0, 0};
+    double height = 0.0;
 };
 
 struct DetectedObject {  // stDetectedObject (PSNWhere_Tracker2D.h:17-29)

@@ -99,47 +99,51 @@ int Tracker2DFlow::fail(int rc, const char *what) {
 }
 
 int Tracker2DFlow::Initialize(unsigned camID, int width, int height, int device) {
+    return InitializeCameras(std::vector<unsigned>{camID}, width, height, device);
+}
+
+int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int width, int height, int device) {
     Finalize();
-    if (const char *e = std::getenv("PSN_T2D_HOST_CHAIN")) device_chain_ = std::atoi(e) == 0;
-    camID_ = camID;
+    if (camIDs.empty() || width <= 0 || height <= 0) return PSN_LK_ERR_ARG;
     width_ = width;
     height_ = height;
-    // 4 slots of full pyramids; the reference's default maxLevel 3 needs 4 levels
-    const int rc = psn_lk_create(device, width, height, kT2dInterval, 3, &lk_);
+    const int nslots = (int)camIDs.size() * kSlotsPerCam;
+    // full pyramids of every camera's slots; the reference's default maxLevel 3 needs 4 levels
+    const int rc = psn_lk_create(device, width, height, nslots, 3, &lk_);
     if (rc) {
         lk_ = nullptr;
         err_ = "psn_lk_create failed (" + std::to_string(rc) + ")";
         return rc;
     }
-    for (int i = 0; i < kT2dInterval; i++) {
-        ring_[i] = i;
-        filled_[i] = false;
+    cams_.assign(camIDs.size(), Cam());
+    for (size_t c = 0; c < camIDs.size(); c++) {
+        cams_[c].camID = camIDs[c];
+        for (int i = 0; i < kT2dInterval; i++) cams_[c].ring[i] = (int)c * kSlotsPerCam + i;
+        cams_[c].spare = (int)c * kSlotsPerCam + kT2dInterval;
     }
+    filled_.assign((size_t)nslots, 0);
     hipStream_t fs = nullptr;
-    hipEvent_t ev = nullptr;
-    if (hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-        err_ = "forward stream / event";
+    if (hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) != hipSuccess) {
+        err_ = "forward stream";
         return PSN_LK_ERR_HIP;
     }
     fwd_stream_ = fs;
-    ev_in_ = ev;
     return PSN_LK_OK;
 }
 
-// Device and pinned-host buffers of the device-side chain (grown on demand).
+// Device and pinned-host buffers of a device pass (grown on demand).
 struct Tracker2DFlow::DeviceBuffers {
     size_t nchains = 0, nfwd_pts = 0, nfwd_jobs = 0;
     float *d_in = nullptr, *d_out = nullptr, *d_buf[2] = {nullptr, nullptr}, *d_err = nullptr;
     uint8_t *d_status = nullptr;
     double *d_boxes = nullptr, *d_obox = nullptr;
     float *d_sets = nullptr;
-    int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr, *d_tot = nullptr;
+    int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr, *d_tot = nullptr, *d_last = nullptr;
     // pinned staging: inputs, then results
     float *h_in = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
     uint8_t *h_fwd_st = nullptr;
     double *h_boxes = nullptr, *h_obox = nullptr;
-    int *h_cnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr, *h_rawcnt = nullptr;
+    int *h_cnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr, *h_rawcnt = nullptr, *h_last = nullptr;
     // the chain's results live in one block per side, [nsteps | set counts | boxes | sets], so that
     // one memset clears the counters and one copy returns every used byte
     char *d_res = nullptr, *h_res = nullptr;
@@ -153,10 +157,10 @@ struct Tracker2DFlow::DeviceBuffers {
     static size_t res_box_off(size_t K, size_t S) { return (K * (1 + S) * 4 + 255) & ~(size_t)255; }
     void release() {
         for (void *p : {(void *)d_in, (void *)d_out, (void *)d_buf[0], (void *)d_buf[1], (void *)d_err, (void *)d_status,
-                        (void *)d_boxes, (void *)d_res, (void *)d_cnt, (void *)d_tot})
+                        (void *)d_boxes, (void *)d_res, (void *)d_cnt, (void *)d_tot, (void *)d_last})
             if (p) (void)hipFree(p);
         for (void *p : {(void *)h_in, (void *)h_fwd_out, (void *)h_fwd_st, (void *)h_boxes, (void *)h_res,
-                        (void *)h_cnt, (void *)h_rawcnt})
+                        (void *)h_cnt, (void *)h_rawcnt, (void *)h_last})
             if (p) (void)hipHostFree(p);
         *this = DeviceBuffers();
     }
@@ -165,6 +169,7 @@ struct Tracker2DFlow::DeviceBuffers {
 void Tracker2DFlow::Finalize() {
     if (dev_) {
         if (lk_) psn_lk_sync(lk_);
+        if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
         dev_->release();
         delete dev_;
         dev_ = nullptr;
@@ -174,10 +179,9 @@ void Tracker2DFlow::Finalize() {
         (void)hipStreamDestroy((hipStream_t)fwd_stream_);
         fwd_stream_ = nullptr;
     }
-    if (ev_in_) (void)hipEventDestroy((hipEvent_t)ev_in_);
-    ev_in_ = nullptr;
     if (lk_) psn_lk_destroy(lk_);
     lk_ = nullptr;
+    cams_.clear();
 }
 
 int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_jobs) {
@@ -185,6 +189,7 @@ int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_job
     DeviceBuffers &b = *dev_;
     if (b.nchains >= nchains && b.nfwd_pts >= nfwd_pts && b.nfwd_jobs >= nfwd_jobs && b.d_in) return PSN_LK_OK;
     if (lk_) psn_lk_sync(lk_);
+    if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
     b.release();
     const size_t K = std::max<size_t>(nchains, 16), F = std::max<size_t>(nfwd_pts, 1024), J = std::max<size_t>(nfwd_jobs, 16);
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, npt = K * cap + F;
@@ -203,6 +208,7 @@ int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_job
     dm((void **)&b.d_res, res_bytes);
     dm((void **)&b.d_cnt, (K + J) * 4);
     dm((void **)&b.d_tot, K * 4);
+    dm((void **)&b.d_last, K * 4);
     hm((void **)&b.h_in, npt * 8);
     hm((void **)&b.h_fwd_out, F * 8);
     hm((void **)&b.h_fwd_st, F);
@@ -210,9 +216,10 @@ int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_job
     hm((void **)&b.h_res, res_bytes);
     hm((void **)&b.h_cnt, (K + J) * 4);
     hm((void **)&b.h_rawcnt, K * 4);
+    hm((void **)&b.h_last, K * 4);
     if (!ok) {
         b.release();
-        err_ = "device-chain buffers: allocation failed";
+        err_ = "device-pass buffers: allocation failed";
         return PSN_LK_ERR_NOMEM;
     }
     b.carve(b.d_res, b.d_obox, b.d_sets, b.d_setcnt, b.d_nsteps, K, S);
@@ -223,54 +230,153 @@ int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_job
     return PSN_LK_OK;
 }
 
-// The backward chains of a frame on the device (:763-811): per step one
-// counted LK launch over every chain (capacity PSN_T2D_CHAIN_CAP points each;
-// a stopped chain's count is 0 so its workgroups exit at once) and one
-// LocalSearchKLT + inlier-compaction kernel writing the next step's points and
-// counts. The forward calls ride in step 1's launch. Everything is enqueued on
-// the LK context stream; the host waits once, for the packed results.
-int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<DetectedObject> &out, std::vector<Job> *fwd) {
-    const size_t K = chains.size(), cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
-    size_t F = 0;
-    const size_t J = fwd ? fwd->size() : 0;
-    for (size_t j = 0; j < J; j++) F += (*fwd)[j].in->size();
-    if (K == 0 && F == 0 && J == 0) return PSN_LK_OK;
+// Error of a chain whose square window (box width, :782) the LK cannot run:
+// CV_Assert(winSize > 2) in the reference, or above this build's window limit.
+static int window_error(int win) {
+    if (win <= 2) return PSN_LK_ERR_WINSIZE;
+    if ((long)win * win > PSN_LK_MAX_WIN_PIXELS) return PSN_LK_ERR_UNSUPPORTED;
+    return PSN_LK_OK;
+}
+
+// Enqueue one device pass over the cameras in pc (everything asynchronous, one
+// host sync in PassComplete):
+//   1. the forward calls of every camera's trackers (:871-877): one counted LK
+//      launch on the forward stream, beside the chains;
+//   2. each detection's features at t: given (host points) or GridFAST on the
+//      device straight into the chain inputs (:734-757), detections below the
+//      feature minimum (:744) gated to count 0 on the device;
+//   3. the backward chains (:763-811): per step ONE counted LK launch over every
+//      detection of every camera (capacity PSN_T2D_CHAIN_CAP points each; a
+//      stopped chain's count is 0, its workgroups exit at once) and one
+//      LocalSearchKLT + inlier-compaction kernel writing the next step's points
+//      and counts. A camera whose ring holds fewer past frames ends its chains
+//      earlier (per-chain last step); its queries in later steps are empty.
+int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed) {
+    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
+    size_t K = 0, J = 0, F = 0;
+    for (PassCam &p : pc) {
+        p.k0 = K;
+        p.j0 = J;
+        p.f0 = F;
+        K += p.dets->size();
+        if (p.fwd) {
+            J += p.fwd->size();
+            for (const Job &jb : *p.fwd) F += jb.in->size();
+        }
+    }
+    if (K == 0 && J == 0) return PSN_LK_OK;
     int rc = EnsureDevice(K, F, J);
     if (rc) return rc;
     DeviceBuffers &b = *dev_;
-    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_);
-    // inputs: chain k's points at k*cap, then the forward jobs' points
-    for (size_t k = 0; k < K; k++) {
-        const Chain &c = chains[k];
-        const Rect box = out[c.obj].detection.box.scale(kFlowScale);
-        b.h_boxes[4 * k] = box.x;
-        b.h_boxes[4 * k + 1] = box.y;
-        b.h_boxes[4 * k + 2] = box.w;
-        b.h_boxes[4 * k + 3] = box.h;
-        for (size_t i = 0; i < c.curr.size(); i++) {
-            b.h_in[2 * (k * cap + i)] = c.curr[i].x;
-            b.h_in[2 * (k * cap + i) + 1] = c.curr[i].y;
-        }
-        b.h_cnt[k] = (int)c.curr.size();
-    }
-    size_t o = K * cap;
-    for (size_t j = 0; j < J; j++) {
-        const std::vector<Point2f> &pts = *(*fwd)[j].in;
-        for (size_t i = 0; i < pts.size(); i++, o++) {
-            b.h_in[2 * o] = pts[i].x;
-            b.h_in[2 * o + 1] = pts[i].y;
-        }
-        b.h_cnt[K + j] = (int)pts.size();
-    }
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !rc) {
             err_ = std::string(what) + ": " + hipGetErrorString(e);
             rc = PSN_LK_ERR_HIP;
         }
     };
-    chk(hipMemcpyAsync(b.d_in, b.h_in, (K * cap + F) * 8, hipMemcpyHostToDevice, st), "chain inputs");
-    chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, std::max<size_t>(K, 1) * 32, hipMemcpyHostToDevice, st), "chain boxes");
-    chk(hipMemcpyAsync(b.d_cnt, b.h_cnt, (K + J) * 4, hipMemcpyHostToDevice, st), "chain counts");
+    // 1. forward calls (every LK launch waits for the builds of the slots it reads)
+    if (J) {
+        size_t o = K * cap;
+        fwd_queries_.clear();
+        for (PassCam &p : pc) {
+            if (!p.fwd) continue;
+            for (const Job &jb : *p.fwd) {
+                const std::vector<Point2f> &pts = *jb.in;
+                psn_lk_query q;
+                q.prev_slot = jb.prev_slot;
+                q.next_slot = jb.next_slot;
+                q.first_pt = (int)o;
+                q.num_pts = (int)pts.size();
+                psn_lk_default_params(&q.params);  // maxLevel 3, (COUNT|EPS, 30, 0.01), minEig 1e-4
+                q.params.win_w = jb.win_w;
+                q.params.win_h = jb.win_h;
+                b.h_cnt[K + fwd_queries_.size()] = (int)pts.size();
+                fwd_queries_.push_back(q);
+                for (size_t i = 0; i < pts.size(); i++, o++) {
+                    b.h_in[2 * o] = pts[i].x;
+                    b.h_in[2 * o + 1] = pts[i].y;
+                }
+            }
+        }
+        if (F) chk(hipMemcpyAsync(b.d_in + 2 * K * cap, b.h_in + 2 * K * cap, F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
+        chk(hipMemcpyAsync(b.d_cnt + K, b.h_cnt + K, J * 4, hipMemcpyHostToDevice, fs), "forward counts");
+        if (rc) return rc;
+        rc = psn_lk_set_stream(lk_, fs);
+        if (!rc)
+            rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_cnt + K, b.d_in, b.d_out, b.d_status,
+                                             b.d_err);
+        const int rs = psn_lk_set_stream(lk_, st);
+        if (rc || rs) return fail(rc ? rc : rs, "forward launch");
+        if (F) {
+            chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
+            chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
+        }
+    }
+    if (!K) return rc;
+    // 2. chain inputs: boxes, last steps, windows, features
+    win_bad_.assign(K, 0);
+    int max_steps = 0;
+    for (PassCam &p : pc) {
+        const int steps = StepsAvailable(p.cam);
+        for (size_t i = 0; i < p.dets->size(); i++) {
+            const size_t k = p.k0 + i;
+            const Rect box = (*p.dets)[i].box.scale(kFlowScale);
+            b.h_boxes[4 * k] = box.x;
+            b.h_boxes[4 * k + 1] = box.y;
+            b.h_boxes[4 * k + 2] = box.w;
+            b.h_boxes[4 * k + 3] = box.h;
+            win_bad_[k] = window_error((int)(box.w * kWinSizeRatio)) != 0;
+            b.h_last[k] = win_bad_[k] ? 0 : steps;
+            if (!win_bad_[k]) max_steps = std::max(max_steps, steps);
+        }
+    }
+    if (gridfast) {
+        psn_gridfast_params gp;
+        psn_gridfast_default_params(&gp);
+        gp.cap = (int)cap;  // kT2dMaxFeatures
+        std::vector<int> rois;
+        for (PassCam &p : pc) {
+            const size_t n = p.dets->size();
+            if (!n) continue;
+            rois.assign(4 * n, 0);
+            for (size_t i = 0; i < n; i++) {
+                // cv::Rect((int)x, (int)y, (int)w, (int)h) of the cropped, scaled box
+                const Rect r = (*p.dets)[i].box.scale(kFlowScale).cropWithSize(width_, height_);
+                rois[4 * i] = (int)r.x;
+                rois[4 * i + 1] = (int)r.y;
+                rois[4 * i + 2] = (int)r.w;
+                rois[4 * i + 3] = (int)r.h;
+            }
+            rc = psn_gridfast_detect_device(lk_, cams_[p.cam].ring[kT2dInterval - 1], rois.data(), (int)n, &gp, seed,
+                                            b.d_in + 2 * cap * p.k0, b.d_cnt + p.k0, b.d_tot + p.k0);
+            if (rc) return fail(rc, "psn_gridfast_detect_device");
+        }
+        chk(hipMemcpyAsync(b.h_rawcnt, b.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
+        chk(hipMemcpyAsync(b.h_in, b.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
+    } else {
+        for (PassCam &p : pc)
+            for (size_t i = 0; i < p.dets->size(); i++) {
+                const size_t k = p.k0 + i;
+                const std::vector<Point2f> &f = (*p.features)[i];
+                const size_t n = std::min(f.size(), kT2dMaxFeatures);  // :753-757
+                if (f.size() >= kT2dMinFeatures && win_bad_[k]) {
+                    err_ = "detection " + std::to_string(i) + " window";
+                    return window_error((int)(b.h_boxes[4 * k + 2] * kWinSizeRatio));
+                }
+                for (size_t j = 0; j < n; j++) {
+                    b.h_in[2 * (k * cap + j)] = f[j].x;
+                    b.h_in[2 * (k * cap + j) + 1] = f[j].y;
+                }
+                b.h_cnt[k] = (int)n;
+            }
+        // whole rows: a chain row's unused tail is never read (counts)
+        chk(hipMemcpyAsync(b.d_in, b.h_in, K * cap * 8, hipMemcpyHostToDevice, st), "chain inputs");
+        chk(hipMemcpyAsync(b.d_cnt, b.h_cnt, K * 4, hipMemcpyHostToDevice, st), "chain counts");
+    }
+    chk(hipMemcpyAsync(b.d_last, b.h_last, K * 4, hipMemcpyHostToDevice, st), "chain last steps");
+    if (!rc) rc = psn_t2d_gate_counts_device(b.d_cnt, (int)K, (int)kT2dMinFeatures, b.d_last, st);
+    chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
     chk(hipMemsetAsync(b.d_nsteps, 0, b.nchains * (1 + S) * 4, st), "chain steps and set counts");
     if (rc) return rc;
     psn_t2d_chain_dev cd{};
@@ -282,116 +388,149 @@ int Tracker2DFlow::ChainsOnDevice(std::vector<Chain> &chains, std::vector<Detect
     cd.sets = b.d_sets;
     cd.set_cnt = b.d_setcnt;
     cd.nsteps = b.d_nsteps;
-    const bool step1 = StepAvailable(1);
-    for (int step = 1; step < (int)S && (step == 1 || (K && StepAvailable(step))); step++) {
+    cd.last_step = b.d_last;
+    for (int step = 1; step <= max_steps; step++) {
         queries_.clear();
-        if (step > 1 || step1)
-            for (size_t k = 0; k < K; k++) {
+        for (PassCam &p : pc) {
+            const Cam &cam = cams_[p.cam];
+            for (size_t i = 0; i < p.dets->size(); i++) {
+                const size_t k = p.k0 + i;
                 psn_lk_query q;
-                q.prev_slot = ring_[kT2dInterval - step];
-                q.next_slot = ring_[kT2dInterval - 1 - step];
+                psn_lk_default_params(&q.params);
                 q.first_pt = (int)(k * cap);
                 q.num_pts = (int)cap;
-                psn_lk_default_params(&q.params);
-                q.params.win_w = q.params.win_h = (int)(b.h_boxes[4 * k + 2] * kWinSizeRatio);
+                if (step <= b.h_last[k]) {  // frame t-s+1 -> t-s with the square box-width window (:776-782)
+                    q.prev_slot = cam.ring[kT2dInterval - step];
+                    q.next_slot = cam.ring[kT2dInterval - 1 - step];
+                    q.params.win_w = q.params.win_h = (int)(b.h_boxes[4 * k + 2] * kWinSizeRatio);
+                } else {  // the chain has ended (count 0 on the device): an empty query
+                    q.prev_slot = q.next_slot = cam.ring[kT2dInterval - 1];
+                }
                 queries_.push_back(q);
             }
-        const size_t nb = queries_.size();
-        if (step == 1 && J) {
-            // the forward calls (Track2D_ForwardTrackingAndGetMatchingScore) are independent of the
-            // backward chain: their launch runs on the forward stream, beside the chain's launches
-            fwd_queries_.clear();
-            for (size_t j = 0, off = K * cap; j < J; j++) {
-                const Job &jb = (*fwd)[j];
-                psn_lk_query q;
-                q.prev_slot = jb.prev_slot;
-                q.next_slot = jb.next_slot;
-                q.first_pt = (int)off;
-                q.num_pts = (int)jb.in->size();
-                psn_lk_default_params(&q.params);
-                q.params.win_w = jb.win_w;
-                q.params.win_h = jb.win_h;
-                fwd_queries_.push_back(q);
-                off += jb.in->size();
-            }
-            hipStream_t fs = (hipStream_t)fwd_stream_;
-            chk(hipEventRecord((hipEvent_t)ev_in_, st), "inputs event");
-            chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_in_, 0), "forward wait");
-            if (rc) return rc;
-            rc = psn_lk_set_stream(lk_, fs);
-            if (!rc)
-                rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_cnt + K, b.d_in, b.d_out,
-                                                 b.d_status, b.d_err);
-            const int rs = psn_lk_set_stream(lk_, st);
-            if (rc || rs) return fail(rc ? rc : rs, "forward launch");
-            if (F) {
-                chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
-                chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
-            }
         }
-        if (queries_.empty()) break;
         const float *in = step == 1 ? b.d_in : b.d_buf[step & 1];
-        rc = rc ? rc
-                : psn_lk_track_device_counted(lk_, queries_.data(), (int)queries_.size(), b.d_cnt, in, b.d_out,
-                                              b.d_status, b.d_err);
+        rc = psn_lk_track_device_counted(lk_, queries_.data(), (int)K, b.d_cnt, in, b.d_out, b.d_status, b.d_err);
         if (rc) return fail(rc, "psn_lk_track_device_counted");
-        if (nb == 0) break;
         cd.cur = in;
         cd.nxt = b.d_out;
         cd.next_in = b.d_buf[(step + 1) & 1];
         rc = psn_t2d_chain_step_device(&cd, step, st);
         if (rc) return fail(rc, "psn_t2d_chain_step_device");
     }
-    if (K) {
-        chk(hipMemcpyAsync(b.h_res, b.d_res, b.res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain results");
-    }
-    chk(hipStreamSynchronize(st), "chain sync");
+    chk(hipMemcpyAsync(b.h_res, b.d_res, b.res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain results");
+    return rc;
+}
+
+// Wait for the pass and unpack it: features (GridFAST mode), every valid
+// detection's chain (boxes, point sets), the forward outputs.
+int Tracker2DFlow::PassComplete(std::vector<PassCam> &pc, bool gridfast) {
+    int rc = PSN_LK_OK;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && !rc) {
+            err_ = std::string(what) + ": " + hipGetErrorString(e);
+            rc = PSN_LK_ERR_HIP;
+        }
+    };
+    chk(hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_)), "chain sync");
     chk(hipStreamSynchronize((hipStream_t)fwd_stream_), "forward sync");
     if (rc) return rc;
-    for (size_t k = 0; k < K; k++) {
-        DetectedObject &ob = out[chains[k].obj];
-        const int ns = b.h_nsteps[k];
-        for (int s2 = 1; s2 <= ns; s2++) {
-            const double *r = b.h_obox + (k * S + s2) * 4;
-            ob.boxes.push_back(Rect(r[0], r[1], r[2], r[3]).scale(1.0 / kFlowScale));
+    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
+    DeviceBuffers *bp = dev_;
+    for (PassCam &p : pc) {
+        const size_t n = p.dets->size();
+        if (gridfast) {
+            p.features->assign(n, {});
+            for (size_t i = 0; i < n; i++) {
+                const size_t k = p.k0 + i;
+                const int m = bp->h_rawcnt[k];
+                // a window the LK cannot run fails the frame only if the chain had to run it (:744)
+                if (win_bad_[k] && (size_t)m >= kT2dMinFeatures) {
+                    err_ = "detection " + std::to_string(i) + " window";
+                    return window_error((int)(bp->h_boxes[4 * k + 2] * kWinSizeRatio));
+                }
+                const float *xy = bp->h_in + 2 * cap * k;
+                (*p.features)[i].resize((size_t)m);
+                for (int j = 0; j < m; j++) (*p.features)[i][(size_t)j] = Point2f{xy[2 * j], xy[2 * j + 1]};
+            }
         }
-        for (int r = 0; ns > 0 && r <= ns; r++) {
-            const int n = b.h_setcnt[k * S + r];
-            const float *p = b.h_sets + (k * S + r) * cap * 2;
-            std::vector<Point2f> v((size_t)n);
-            for (int i = 0; i < n; i++) v[(size_t)i] = Point2f{p[2 * i], p[2 * i + 1]};
-            ob.vecvecTrackedFeatures.push_back(std::move(v));
+        std::vector<Chain> chains;
+        BackwardBegin(*p.dets, *p.features, *p.out, chains);  // valid detections, in order
+        for (DetectedObject &ob : *p.out) {
+            const size_t k = p.k0 + ob.id;  // the detection index = its device chain
+            const int ns = bp->h_nsteps[k];
+            for (int s2 = 1; s2 <= ns; s2++) {
+                const double *r = bp->h_obox + (k * S + s2) * 4;
+                ob.boxes.push_back(Rect(r[0], r[1], r[2], r[3]).scale(1.0 / kFlowScale));
+            }
+            for (int r = 0; ns > 0 && r <= ns; r++) {
+                const int m = bp->h_setcnt[k * S + r];
+                const float *pp = bp->h_sets + (k * S + r) * cap * 2;
+                std::vector<Point2f> v((size_t)m);
+                for (int i = 0; i < m; i++) v[(size_t)i] = Point2f{pp[2 * i], pp[2 * i + 1]};
+                ob.vecvecTrackedFeatures.push_back(std::move(v));
+            }
         }
-        chains[k].active = false;
-    }
-    for (size_t j = 0, off = 0; j < J; j++) {
-        Job &jb = (*fwd)[j];
-        const size_t m = jb.in->size();
-        jb.out->resize(m);
-        jb.status->resize(m);
-        for (size_t i = 0; i < m; i++, off++) {
-            (*jb.out)[i] = Point2f{b.h_fwd_out[2 * off], b.h_fwd_out[2 * off + 1]};
-            (*jb.status)[i] = b.h_fwd_st[off];
+        if (!p.fwd) continue;
+        for (size_t j = 0, off = p.f0; j < p.fwd->size(); j++) {
+            Job &jb = (*p.fwd)[j];
+            const size_t m = jb.in->size();
+            jb.out->resize(m);
+            jb.status->resize(m);
+            for (size_t i = 0; i < m; i++, off++) {
+                (*jb.out)[i] = Point2f{bp->h_fwd_out[2 * off], bp->h_fwd_out[2 * off + 1]};
+                (*jb.status)[i] = bp->h_fwd_st[off];
+            }
         }
     }
     return PSN_LK_OK;
 }
 
+// One camera (0), one pass, synchronous.
+int Tracker2DFlow::DevicePass(const std::vector<Detection> &dets, std::vector<std::vector<Point2f>> &features,
+                              std::vector<DetectedObject> &out, std::vector<Job> *fwd, bool gridfast, uint32_t seed) {
+    std::vector<PassCam> pc(1);
+    pc[0].cam = 0;
+    pc[0].dets = &dets;
+    pc[0].features = &features;
+    pc[0].out = &out;
+    pc[0].fwd = fwd;
+    out.clear();
+    int rc = PassLaunch(pc, gridfast, seed);
+    if (rc) {  // drain what was enqueued before returning the error
+        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        return rc;
+    }
+    return PassComplete(pc, gridfast);
+}
+
 int Tracker2DFlow::PushFrame(const uint8_t *frame, int stride, int channels) {
     if (!lk_) return PSN_LK_ERR_ARG;
-    const int slot = ring_[kT2dInterval - 1];
+    const int slot = cams_[0].ring[kT2dInterval - 1];
     const int rc = psn_lk_push_frame(lk_, slot, frame, stride, channels);
     if (rc) return fail(rc, "psn_lk_push_frame");
-    filled_[slot] = true;
+    filled_[(size_t)slot] = 1;
     return PSN_LK_OK;
 }
 
 int Tracker2DFlow::PushFrameDevice(const uint8_t *dev, int stride, int channels) {
     if (!lk_) return PSN_LK_ERR_ARG;
-    const int slot = ring_[kT2dInterval - 1];
+    const int slot = cams_[0].ring[kT2dInterval - 1];
     const int rc = psn_lk_push_frame_device(lk_, slot, dev, stride, channels);
     if (rc) return fail(rc, "psn_lk_push_frame_device");
-    filled_[slot] = true;
+    filled_[(size_t)slot] = 1;
+    return PSN_LK_OK;
+}
+
+int Tracker2DFlow::StageFrame(size_t cam, const uint8_t *frame, int stride, int channels, bool on_device) {
+    if (!lk_ || cam >= cams_.size() || !frame) return PSN_LK_ERR_ARG;
+    Cam &c = cams_[cam];
+    const int rc = on_device ? psn_lk_push_frame_device(lk_, c.spare, frame, stride, channels)
+                             : psn_lk_push_frame_async(lk_, c.spare, frame, stride, channels);
+    if (rc) return fail(rc, "stage frame");
+    filled_[(size_t)c.spare] = 1;
+    c.staged = true;
     return PSN_LK_OK;
 }
 
@@ -414,8 +553,8 @@ int Tracker2DFlow::DetectFeatures(const std::vector<Detection> &dets, uint32_t s
     psn_gridfast_default_params(&p);
     p.cap = (int)kT2dMaxFeatures;
     gf_xy_.resize(2 * n * kT2dMaxFeatures);
-    const int rc = psn_gridfast_detect(lk_, ring_[kT2dInterval - 1], rois.data(), (int)n, &p, seed, gf_xy_.data(),
-                                       cnt.data(), tot.data());
+    const int rc = psn_gridfast_detect(lk_, cams_[0].ring[kT2dInterval - 1], rois.data(), (int)n, &p, seed,
+                                       gf_xy_.data(), cnt.data(), tot.data());
     if (rc) return fail(rc, "psn_gridfast_detect");
     for (size_t i = 0; i < n; i++) {
         const float *xy = gf_xy_.data() + 2 * kT2dMaxFeatures * i;
@@ -425,7 +564,14 @@ int Tracker2DFlow::DetectFeatures(const std::vector<Detection> &dets, uint32_t s
     return PSN_LK_OK;
 }
 
-void Tracker2DFlow::RotateRing() { std::rotate(ring_, ring_ + 1, ring_ + kT2dInterval); }
+void Tracker2DFlow::RotateRing() { std::rotate(cams_[0].ring, cams_[0].ring + 1, cams_[0].ring + kT2dInterval); }
+
+// steps s = 1..3 need frame t-s: consecutive filled slots behind the newest
+int Tracker2DFlow::StepsAvailable(size_t cam) const {
+    int s = 0;
+    while (s + 1 < kT2dInterval && filled_[(size_t)cams_[cam].ring[kT2dInterval - 2 - s]]) s++;
+    return s;
+}
 
 // One launch for all jobs: points concatenated, one query per job. err is
 // requested as the reference does (:781, :876): its bounds re-check can clear
@@ -486,6 +632,8 @@ void Tracker2DFlow::BackwardBegin(const std::vector<Detection> &dets,
         DetectedObject o;
         o.id = (unsigned)i;  // detectionID counts every detection past the height gate (:718)
         o.detection = dets[i];
+        for (int k = 0; k < 3; k++) o.location[k] = dets[i].location[k];
+        o.height = dets[i].height;
         o.boxes.push_back(dets[i].box);
         const std::vector<Point2f> &f = features[i];
         if (f.size() < kT2dMinFeatures) continue;  // :744
@@ -498,19 +646,14 @@ void Tracker2DFlow::BackwardBegin(const std::vector<Detection> &dets,
     }
 }
 
-// step s tracks frame t-s+1 -> t-s; it exists while the older ring slot holds a frame
-bool Tracker2DFlow::StepAvailable(int step) const {
-    return step < kT2dInterval && filled_[ring_[kT2dInterval - 1 - step]];
-}
-
 void Tracker2DFlow::BackwardJobs(int step, std::vector<Chain> &chains, const std::vector<DetectedObject> &out,
                                  std::vector<Job> &jobs) {
     for (Chain &c : chains) {
         if (!c.active) continue;
         const Rect box = out[c.obj].detection.box.scale(kFlowScale);
         const int win = (int)(box.w * kWinSizeRatio);  // square window of the box width (:782)
-        jobs.push_back(Job{ring_[kT2dInterval - step], ring_[kT2dInterval - 1 - step], win, win, &c.curr, &c.prev,
-                           &c.status});
+        jobs.push_back(Job{cams_[0].ring[kT2dInterval - step], cams_[0].ring[kT2dInterval - 1 - step], win, win, &c.curr,
+                           &c.prev, &c.status});
     }
 }
 
@@ -539,9 +682,12 @@ void Tracker2DFlow::BackwardStepDone(std::vector<Chain> &chains, std::vector<Det
     }
 }
 
-void Tracker2DFlow::BackwardEnd(std::vector<Chain> &chains, std::vector<DetectedObject> &out) {
-    for (Chain &c : chains)
-        if (out[c.obj].vecvecTrackedFeatures.empty()) out[c.obj].vecvecTrackedFeatures.push_back(c.curr);  // :815-818
+void Tracker2DFlow::BackwardEnd(std::vector<DetectedObject> &out, const std::vector<std::vector<Point2f>> &features) {
+    for (DetectedObject &o : out)  // no step kept >= 4 inliers: the features at t (:815-818)
+        if (o.vecvecTrackedFeatures.empty()) {
+            const std::vector<Point2f> &f = features[o.id];
+            o.vecvecTrackedFeatures.emplace_back(f.begin(), f.begin() + (ptrdiff_t)std::min(f.size(), kT2dMaxFeatures));
+        }
     // overlap flags (:824-835)
     for (size_t a = 0; a < out.size(); a++) {
         if (out[a].bOverlapWithOtherDetection) continue;
@@ -557,14 +703,15 @@ int Tracker2DFlow::BackwardFeatureTracking(const std::vector<Detection> &dets,
                                            const std::vector<std::vector<Point2f>> &features,
                                            std::vector<DetectedObject> &out) {
     if (!lk_ || features.size() != dets.size()) return PSN_LK_ERR_ARG;
-    std::vector<Chain> chains;
-    BackwardBegin(dets, features, out, chains);
     if (device_chain_) {
-        const int rc = ChainsOnDevice(chains, out, nullptr);
+        std::vector<std::vector<Point2f>> f = features;
+        const int rc = DevicePass(dets, f, out, nullptr, false, 0);
         if (rc) return rc;
-        BackwardEnd(chains, out);
+        BackwardEnd(out, features);
         return PSN_LK_OK;
     }
+    std::vector<Chain> chains;
+    BackwardBegin(dets, features, out, chains);
     std::vector<Job> jobs;
     for (int step = 1; StepAvailable(step); step++) {
         jobs.clear();
@@ -574,7 +721,7 @@ int Tracker2DFlow::BackwardFeatureTracking(const std::vector<Detection> &dets,
         if (rc) return rc;
         BackwardStepDone(chains, out);
     }
-    BackwardEnd(chains, out);
+    BackwardEnd(out, features);
     return PSN_LK_OK;
 }
 
@@ -582,14 +729,15 @@ int Tracker2DFlow::BackwardFeatureTracking(const std::vector<Detection> &dets,
 // Forward tracking + matching score (:851-1025)
 // ---------------------------------------------------------------------------
 
-void Tracker2DFlow::ForwardJobs(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
-                                std::vector<Job> &jobs) {
+void Tracker2DFlow::ForwardJobs(size_t cam, const std::vector<Tracker2D *> &trackers,
+                                std::vector<std::vector<uint8_t>> &status, std::vector<Job> &jobs) {
     status.assign(trackers.size(), {});
+    const int *ring = cams_[cam].ring;
     for (size_t t = 0; t < trackers.size(); t++) {
         Tracker2D *tr = trackers[t];
         tr->trackedPoints.clear();
         const Rect cur = tr->boxes.back().scale(kFlowScale);
-        jobs.push_back(Job{ring_[kT2dInterval - 2], ring_[kT2dInterval - 1], (int)(cur.w * kWinSizeRatio),
+        jobs.push_back(Job{ring[kT2dInterval - 2], ring[kT2dInterval - 1], (int)(cur.w * kWinSizeRatio),
                            (int)(cur.h * kWinSizeRatio), &tr->featurePoints, &tr->trackedPoints, &status[t]});
     }
 }
@@ -673,7 +821,7 @@ int Tracker2DFlow::ForwardTrackingAndGetMatchingScore(const std::vector<Tracker2
     std::vector<std::vector<uint8_t>> status;
     std::vector<Job> jobs;
     if (!trackers.empty() && !StepAvailable(1)) return PSN_LK_ERR_SLOT;  // no frame t-1
-    ForwardJobs(trackers, status, jobs);
+    ForwardJobs(0, trackers, status, jobs);
     int rc = RunJobs(jobs);
     if (rc) return rc;
     ForwardDone(trackers, status, dets, cost);
@@ -695,160 +843,12 @@ int Tracker2DFlow::TrackFrameDetect(const std::vector<Detection> &dets, uint32_t
         return rc ? rc : TrackFrame(dets, features, out, trackers, cost);
     }
     if (!trackers.empty() && !StepAvailable(1)) return PSN_LK_ERR_SLOT;
-    const size_t K = dets.size(), cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
     std::vector<std::vector<uint8_t>> fstatus;
     std::vector<Job> fwd;
-    ForwardJobs(trackers, fstatus, fwd);
-    const size_t J = fwd.size();
-    size_t F = 0;
-    for (const Job &jb : fwd) F += jb.in->size();
-    int rc = EnsureDevice(K, F, J);
+    ForwardJobs(0, trackers, fstatus, fwd);
+    const int rc = DevicePass(dets, features, out, &fwd, true, seed);
     if (rc) return rc;
-    DeviceBuffers &b = *dev_;
-    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
-    auto chk = [&](hipError_t e, const char *what) {
-        if (e != hipSuccess && !rc) {
-            err_ = std::string(what) + ": " + hipGetErrorString(e);
-            rc = PSN_LK_ERR_HIP;
-        }
-    };
-    // 1. the forward calls, first, on the forward stream (after frame t's ingest)
-    if (J) {
-        size_t o = K * cap;
-        fwd_queries_.clear();
-        for (size_t j = 0; j < J; j++) {
-            const std::vector<Point2f> &pts = *fwd[j].in;
-            psn_lk_query q;
-            q.prev_slot = fwd[j].prev_slot;
-            q.next_slot = fwd[j].next_slot;
-            q.first_pt = (int)o;
-            q.num_pts = (int)pts.size();
-            psn_lk_default_params(&q.params);
-            q.params.win_w = fwd[j].win_w;
-            q.params.win_h = fwd[j].win_h;
-            fwd_queries_.push_back(q);
-            for (size_t i = 0; i < pts.size(); i++, o++) {
-                b.h_in[2 * o] = pts[i].x;
-                b.h_in[2 * o + 1] = pts[i].y;
-            }
-            b.h_cnt[K + j] = (int)pts.size();
-        }
-        chk(hipEventRecord((hipEvent_t)ev_in_, st), "ingest event");
-        chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_in_, 0), "forward wait");
-        chk(hipMemcpyAsync(b.d_in + 2 * K * cap, b.h_in + 2 * K * cap, F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
-        chk(hipMemcpyAsync(b.d_cnt + K, b.h_cnt + K, J * 4, hipMemcpyHostToDevice, fs), "forward counts");
-        if (rc) return rc;
-        rc = psn_lk_set_stream(lk_, fs);
-        if (!rc)
-            rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_cnt + K, b.d_in, b.d_out, b.d_status,
-                                             b.d_err);
-        const int rs = psn_lk_set_stream(lk_, st);
-        if (rc || rs) return fail(rc ? rc : rs, "forward launch");
-        if (F) {
-            chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
-            chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
-        }
-    }
-    // 2. GridFAST of every detection into the chain inputs, then the chains
-    if (K) {
-        std::vector<int> rois(4 * K);
-        for (size_t i = 0; i < K; i++) {
-            const Rect r = dets[i].box.scale(kFlowScale).cropWithSize(width_, height_);
-            rois[4 * i] = (int)r.x;
-            rois[4 * i + 1] = (int)r.y;
-            rois[4 * i + 2] = (int)r.w;
-            rois[4 * i + 3] = (int)r.h;
-            const Rect box = dets[i].box.scale(kFlowScale);
-            b.h_boxes[4 * i] = box.x;
-            b.h_boxes[4 * i + 1] = box.y;
-            b.h_boxes[4 * i + 2] = box.w;
-            b.h_boxes[4 * i + 3] = box.h;
-        }
-        psn_gridfast_params p;
-        psn_gridfast_default_params(&p);
-        p.cap = (int)cap;  // kT2dMaxFeatures
-        rc = psn_gridfast_detect_device(lk_, ring_[kT2dInterval - 1], rois.data(), (int)K, &p, seed, b.d_in, b.d_cnt,
-                                        b.d_tot);
-        if (rc) return fail(rc, "psn_gridfast_detect_device");
-        chk(hipMemcpyAsync(b.h_rawcnt, b.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
-        chk(hipMemcpyAsync(b.h_in, b.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
-        if (!rc) rc = psn_t2d_gate_counts_device(b.d_cnt, (int)K, (int)kT2dMinFeatures, st);
-        chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
-        chk(hipMemsetAsync(b.d_nsteps, 0, b.nchains * (1 + S) * 4, st), "chain steps and set counts");
-        if (rc) return rc;
-        psn_t2d_chain_dev cd{};
-        cd.ndet = (int)K;
-        cd.cap = (int)cap;
-        cd.boxes = b.d_boxes;
-        cd.cnt = b.d_cnt;
-        cd.out_boxes = b.d_obox;
-        cd.sets = b.d_sets;
-        cd.set_cnt = b.d_setcnt;
-        cd.nsteps = b.d_nsteps;
-        for (int step = 1; step < (int)S && StepAvailable(step); step++) {
-            queries_.clear();
-            for (size_t k = 0; k < K; k++) {
-                psn_lk_query q;
-                q.prev_slot = ring_[kT2dInterval - step];
-                q.next_slot = ring_[kT2dInterval - 1 - step];
-                q.first_pt = (int)(k * cap);
-                q.num_pts = (int)cap;
-                psn_lk_default_params(&q.params);
-                q.params.win_w = q.params.win_h = (int)(b.h_boxes[4 * k + 2] * kWinSizeRatio);
-                queries_.push_back(q);
-            }
-            const float *in = step == 1 ? b.d_in : b.d_buf[step & 1];
-            rc = psn_lk_track_device_counted(lk_, queries_.data(), (int)K, b.d_cnt, in, b.d_out, b.d_status, b.d_err);
-            if (rc) return fail(rc, "psn_lk_track_device_counted");
-            cd.cur = in;
-            cd.nxt = b.d_out;
-            cd.next_in = b.d_buf[(step + 1) & 1];
-            rc = psn_t2d_chain_step_device(&cd, step, st);
-            if (rc) return fail(rc, "psn_t2d_chain_step_device");
-        }
-        chk(hipMemcpyAsync(b.h_res, b.d_res, b.res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain results");
-    }
-    chk(hipStreamSynchronize(st), "chain sync");
-    chk(hipStreamSynchronize(fs), "forward sync");
-    if (rc) return rc;
-    // 3. host: features, the valid detections' objects and chains, forward matching
-    features.assign(K, {});
-    for (size_t i = 0; i < K; i++) {
-        const int n = b.h_rawcnt[i];
-        const float *xy = b.h_in + 2 * cap * i;
-        features[i].resize((size_t)n);
-        for (int k = 0; k < n; k++) features[i][(size_t)k] = Point2f{xy[2 * k], xy[2 * k + 1]};
-    }
-    std::vector<Chain> chains;
-    BackwardBegin(dets, features, out, chains);  // valid detections, in order
-    for (Chain &c : chains) {
-        DetectedObject &ob = out[c.obj];
-        const size_t k = ob.id;  // the detection index = its device chain
-        const int ns = b.h_nsteps[k];
-        for (int s2 = 1; s2 <= ns; s2++) {
-            const double *r = b.h_obox + (k * S + s2) * 4;
-            ob.boxes.push_back(Rect(r[0], r[1], r[2], r[3]).scale(1.0 / kFlowScale));
-        }
-        for (int r = 0; ns > 0 && r <= ns; r++) {
-            const int n = b.h_setcnt[k * S + r];
-            const float *pp = b.h_sets + (k * S + r) * cap * 2;
-            std::vector<Point2f> v((size_t)n);
-            for (int i = 0; i < n; i++) v[(size_t)i] = Point2f{pp[2 * i], pp[2 * i + 1]};
-            ob.vecvecTrackedFeatures.push_back(std::move(v));
-        }
-        c.active = false;
-    }
-    for (size_t j = 0, off = 0; j < J; j++) {
-        Job &jb = fwd[j];
-        const size_t m = jb.in->size();
-        jb.out->resize(m);
-        jb.status->resize(m);
-        for (size_t i = 0; i < m; i++, off++) {
-            (*jb.out)[i] = Point2f{b.h_fwd_out[2 * off], b.h_fwd_out[2 * off + 1]};
-            (*jb.status)[i] = b.h_fwd_st[off];
-        }
-    }
-    BackwardEnd(chains, out);
+    BackwardEnd(out, features);
     ForwardDone(trackers, fstatus, out, cost);
     return PSN_LK_OK;
 }
@@ -858,22 +858,23 @@ int Tracker2DFlow::TrackFrame(const std::vector<Detection> &dets, const std::vec
                               std::vector<float> &cost) {
     if (!lk_ || features.size() != dets.size()) return PSN_LK_ERR_ARG;
     if (!trackers.empty() && !StepAvailable(1)) return PSN_LK_ERR_SLOT;
-    std::vector<Chain> chains;
-    BackwardBegin(dets, features, out, chains);
     std::vector<std::vector<uint8_t>> fstatus;
     std::vector<Job> jobs;
     if (device_chain_) {
-        ForwardJobs(trackers, fstatus, jobs);
-        const int rc = ChainsOnDevice(chains, out, &jobs);
+        ForwardJobs(0, trackers, fstatus, jobs);
+        std::vector<std::vector<Point2f>> f = features;
+        const int rc = DevicePass(dets, f, out, &jobs, false, 0);
         if (rc) return rc;
-        BackwardEnd(chains, out);
+        BackwardEnd(out, features);
         ForwardDone(trackers, fstatus, out, cost);
         return PSN_LK_OK;
     }
+    std::vector<Chain> chains;
+    BackwardBegin(dets, features, out, chains);
     // launch 1: backward step 1 of every detection + every forward call
     if (StepAvailable(1)) BackwardJobs(1, chains, out, jobs);
     const size_t nb = jobs.size();
-    ForwardJobs(trackers, fstatus, jobs);
+    ForwardJobs(0, trackers, fstatus, jobs);
     int rc = RunJobs(jobs);
     if (rc) return rc;
     if (nb) BackwardStepDone(chains, out);
@@ -885,8 +886,75 @@ int Tracker2DFlow::TrackFrame(const std::vector<Detection> &dets, const std::vec
         if (rc) return rc;
         BackwardStepDone(chains, out);
     }
-    BackwardEnd(chains, out);
+    BackwardEnd(out, features);
     ForwardDone(trackers, fstatus, out, cost);
+    return PSN_LK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// CPSNWhere_Tracker2D::Run of every camera (:251-373), batched
+// ---------------------------------------------------------------------------
+
+// Adopt every camera's staged frame as frame t (the ring advances: the oldest
+// slot becomes the next staging slot; Run's buffer circulation, :310-316) and
+// enqueue the frame's device work: one pass over all cameras (forward calls of
+// every active tracker, features, backward chains).
+int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool gridfast, uint32_t seed) {
+    if (!lk_ || io.size() != cams_.size()) return PSN_LK_ERR_ARG;
+    for (size_t c = 0; c < cams_.size(); c++) {
+        if (!cams_[c].staged) {
+            err_ = "camera " + std::to_string(c) + ": no frame staged";
+            return PSN_LK_ERR_SLOT;
+        }
+        if (!gridfast && io[c].features.size() != io[c].dets.size()) return PSN_LK_ERR_ARG;
+    }
+    run_frame_ = frameIdx;
+    run_gridfast_ = gridfast;
+    run_pass_.assign(cams_.size(), PassCam());
+    for (size_t c = 0; c < cams_.size(); c++) {
+        Cam &cam = cams_[c];
+        const int oldest = cam.ring[0];
+        std::rotate(cam.ring, cam.ring + 1, cam.ring + kT2dInterval);
+        cam.ring[kT2dInterval - 1] = cam.spare;
+        cam.spare = oldest;
+        cam.staged = false;
+        cam.trackers.assign(cam.active.begin(), cam.active.end());
+        cam.fwd.clear();
+        ForwardJobs(c, cam.trackers, cam.fstatus, cam.fwd);
+        PassCam &p = run_pass_[c];
+        p.cam = c;
+        p.dets = &io[c].dets;
+        p.features = &io[c].features;
+        p.out = &io[c].objects;
+        p.fwd = &cam.fwd;
+        io[c].objects.clear();
+    }
+    const int rc = PassLaunch(run_pass_, gridfast, seed);
+    if (rc) {
+        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        run_pass_.clear();
+    }
+    return rc;
+}
+
+// Wait for the frame's device work, then per camera: overlap flags (:824-835),
+// matching costs + majority gate (:906-1022), assignment and tracker update
+// (:1038-1164), result packaging (:1099-1101, :1144-1146).
+int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io) {
+    if (!lk_ || io.size() != cams_.size() || run_pass_.size() != cams_.size()) return PSN_LK_ERR_ARG;
+    const int rc = PassComplete(run_pass_, run_gridfast_);
+    run_pass_.clear();
+    if (rc) return rc;
+    for (size_t c = 0; c < cams_.size(); c++) {
+        Cam &cam = cams_[c];
+        CamFrame &f = io[c];
+        BackwardEnd(f.objects, f.features);
+        ForwardDone(cam.trackers, cam.fstatus, f.objects, f.cost);
+        const std::vector<int> match = AssignDetections(f.cost, f.objects.size(), cam.trackers.size());
+        MatchingAndUpdating(f.objects, cam.active, cam.storage, match, run_frame_, cam.newTrackerID, f.result);
+        f.result.camID = cam.camID;
+    }
     return PSN_LK_OK;
 }
 

@@ -4,12 +4,18 @@
 // CPSNWhere_Tracker2D (psn_where/PSNWhere_Tracker2D.{h,cpp}) that drive the
 // optical flow: ingest + ring (Run, :251-263, :310-316), the backward feature
 // tracking chain (:690-838), forward tracking + matching score (:851-1025),
-// LocalSearchKLT (:452-554), BoxMatchingCost (:600-613) and ResultWithTracker
-// (:1231-1257). The LK calls of a frame are batched: every detection's chain
-// step s is one launch, and step 1 shares its launch with the forward calls.
+// LocalSearchKLT (:452-554), BoxMatchingCost (:600-613), and after the flow
+// Track2D_MatchingAndUpdating (:1038-1164) with ResultWithTracker (:1231-1257).
+//
+// One object serves C cameras (CPSNWhere::TrackPeople's per-camera loop,
+// PSNWhere.cpp:257-266): they share one LK context (camera c owns ring slots
+// [c*kSlotsPerCam, c*kSlotsPerCam + kSlotsPerCam)), so a chain step of every
+// detection of every camera is ONE LK launch, and the forward calls of every
+// tracker of every camera are one launch on a second stream beside the chain.
 #pragma once
 
 #include <cstdint>
+#include <list>
 #include <string>
 #include <vector>
 
@@ -19,6 +25,7 @@
 namespace psn {
 
 constexpr int kT2dInterval = 4;          // PSN_2D_BACKTRACKING_INTERVAL (:16)
+constexpr int kSlotsPerCam = kT2dInterval + 1;  // the ring + one slot the next frame is staged in
 constexpr size_t kT2dMinFeatures = 4;    // PSN_2D_FEATURE_MIN_NUM_TRACK (:12)
 constexpr size_t kT2dMaxFeatures = 100;  // PSN_2D_FEATURE_MAX_NUM_TRACK (:13)
 constexpr double kFlowScale = 1.0;       // PSN_2D_OPTICALFLOW_SCALE (:18)
@@ -28,6 +35,12 @@ Rect LocalSearchKLT(Rect preBox, const std::vector<Point2f> &preFeatures, const 
                     std::vector<size_t> &inlierFeatureIndex);
 double BoxMatchingCost(const Rect &box1, const Rect &box2);
 void ResultWithTracker(const Tracker2D &tracker, Object2DInfo &out);
+// tracker2d_match.cpp: the assignment of Track2D_MatchingAndUpdating (inf
+// handling + minimum-cost matching, :1040-1064) and the update (:1066-1164)
+std::vector<int> AssignDetections(const std::vector<float> &cost, size_t rows, size_t cols);
+void MatchingAndUpdating(std::vector<DetectedObject> &dets, std::deque<Tracker2D *> &active,
+                         std::list<Tracker2D> &storage, const std::vector<int> &match, unsigned frameIdx,
+                         unsigned &newTrackerID, Track2DResult &result);
 
 class Tracker2DFlow {
   public:
@@ -36,25 +49,26 @@ class Tracker2DFlow {
     Tracker2DFlow(const Tracker2DFlow &) = delete;
     Tracker2DFlow &operator=(const Tracker2DFlow &) = delete;
 
-    int Initialize(unsigned camID, int width, int height, int device);
+    int Initialize(unsigned camID, int width, int height, int device);  // one camera
+    int InitializeCameras(const std::vector<unsigned> &camIDs, int width, int height, int device);
     void Finalize();
-    // ingest frame t into the newest ring slot (cvtColor(BGR2GRAY) + resize 1.0)
-    int PushFrame(const uint8_t *frame, int stride, int channels);
-    int PushFrameDevice(const uint8_t *dev, int stride, int channels);  // frame already in device memory
+    size_t NumCameras() const { return cams_.size(); }
     psn_lk_ctx *LkContext() const { return lk_; }
-    // buffer circulation at the end of Run
-    void RotateRing();
 
+    // ---- single-camera flow-stage API (camera 0), the reference's call order:
+    // PushFrame (frame t into the newest ring slot), the steps, RotateRing ----
+    int PushFrame(const uint8_t *frame, int stride, int channels);  // cvtColor(BGR2GRAY) + resize 1.0
+    int PushFrameDevice(const uint8_t *dev, int stride, int channels);  // frame already in device memory
+    void RotateRing();  // buffer circulation at the end of Run
     // Feature extraction of the backward chain (:734-757) on frame t (the
     // newest ring slot): GridFAST masked by each detection's rectROI
     // (box.cropWithSize(cols, rows).cv(), :736), then the seeded shuffle + cap
     // to PSN_2D_FEATURE_MAX_NUM_TRACK. features[i] may hold < 4 points (the
     // backward step then skips detection i, :744).
     int DetectFeatures(const std::vector<Detection> &dets, uint32_t seed, std::vector<std::vector<Point2f>> &features);
-
     // Track2D_BackwardFeatureTracking for detections that passed the caller's
-    // height gate; features[i] = detection i's points at t after shuffle + cap
-    // (GridFAST stays with the caller). out = m_vecDetection2D.
+    // height gate; features[i] = detection i's points at t after shuffle + cap.
+    // out = m_vecDetection2D.
     int BackwardFeatureTracking(const std::vector<Detection> &dets, const std::vector<std::vector<Point2f>> &features,
                                 std::vector<DetectedObject> &out);
     // Track2D_ForwardTrackingAndGetMatchingScore over the active trackers;
@@ -64,15 +78,33 @@ class Tracker2DFlow {
     // both: the forward calls overlap the backward chain (own stream)
     int TrackFrame(const std::vector<Detection> &dets, const std::vector<std::vector<Point2f>> &features,
                    std::vector<DetectedObject> &out, const std::vector<Tracker2D *> &trackers, std::vector<float> &cost);
-
     // DetectFeatures + TrackFrame as one device pass (device chain mode): GridFAST
     // writes the chain inputs on the device, the forward launch runs beside it
     int TrackFrameDetect(const std::vector<Detection> &dets, uint32_t seed,
                          std::vector<std::vector<Point2f>> &features, std::vector<DetectedObject> &out,
                          const std::vector<Tracker2D *> &trackers, std::vector<float> &cost);
 
-    psn_lk_ctx *lk() const { return lk_; }
-    // backward chain steps on the device (default) or on the host (PSN_T2D_HOST_CHAIN=1)
+    // ---- multi-camera Run (CPSNWhere_Tracker2D::Run of every camera) ----
+    // StageFrame: frame t of camera `cam` is uploaded (host frames: async, a copy
+    // engine for pinned memory) and its pyramid built on the ingest stream, into
+    // the camera's staging slot; the next RunLaunch adopts it as frame t. May be
+    // called for frame t+1 between RunLaunch(t) and RunComplete(t).
+    int StageFrame(size_t cam, const uint8_t *frame, int stride, int channels, bool on_device);
+    struct CamFrame {  // one camera's inputs and outputs of Run
+        std::vector<Detection> dets;                      // height-validated detections of frame t
+        std::vector<std::vector<Point2f>> features;       // in (given mode) / out (GridFAST mode)
+        std::vector<DetectedObject> objects;              // out: m_vecDetection2D
+        std::vector<float> cost;                          // out: matchingCostArray
+        Track2DResult result;                             // out: m_stTrack2DResult
+    };
+    // Enqueue frame t's device work for every camera (features given, or GridFAST
+    // on the device with `seed` when gridfast); RunComplete waits and runs the host
+    // part: matching, tracker update, result packaging.
+    int RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool gridfast, uint32_t seed);
+    int RunComplete(std::vector<CamFrame> &io);
+    const std::deque<Tracker2D *> &ActiveTrackers(size_t cam) const { return cams_[cam].active; }
+
+    // backward chain steps on the device (default) or on the host (single-camera API)
     void SetDeviceChain(bool on) { device_chain_ = on; }
     bool DeviceChain() const { return device_chain_; }
     const std::string &last_error() const { return err_; }
@@ -84,45 +116,71 @@ class Tracker2DFlow {
         std::vector<Point2f> *out;
         std::vector<uint8_t> *status;
     };
-    int RunJobs(std::vector<Job> &jobs);
-    int fail(int rc, const char *what);
-
-    struct Chain {  // one detection's backward chain
+    struct Chain {  // one detection's backward chain (host-chain mode)
         size_t obj;
         std::vector<Point2f> curr, prev;
         std::vector<uint8_t> status;
         bool active;
     };
+    struct Cam {  // per-camera state
+        unsigned camID = 0;
+        int ring[kT2dInterval];  // slot ids, oldest first; ring[kT2dInterval - 1] = frame t
+        int spare = -1;          // staging slot of the next frame (multi-camera Run)
+        bool staged = false;
+        // Run state: m_listTracker2D, m_queueActiveTracker2D, m_nNewTrackerID
+        std::list<Tracker2D> storage;
+        std::deque<Tracker2D *> active;
+        unsigned newTrackerID = 0;
+        std::vector<Tracker2D *> trackers;               // this frame's forward inputs
+        std::vector<std::vector<uint8_t>> fstatus;
+        std::vector<Job> fwd;
+    };
+    // One device pass over several cameras: GridFAST (optional) + the backward
+    // chains of every detection + the forward calls of every tracker.
+    struct PassCam {
+        size_t cam;
+        const std::vector<Detection> *dets;
+        std::vector<std::vector<Point2f>> *features;  // in, or out with gridfast
+        std::vector<DetectedObject> *out;
+        std::vector<Job> *fwd;
+        size_t k0, j0, f0;  // first chain / forward job / forward point of this camera in the pass
+    };
+    int PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);
+    int PassComplete(std::vector<PassCam> &pc, bool gridfast);
+
+    int RunJobs(std::vector<Job> &jobs);
+    int fail(int rc, const char *what);
     void BackwardBegin(const std::vector<Detection> &dets, const std::vector<std::vector<Point2f>> &features,
                        std::vector<DetectedObject> &out, std::vector<Chain> &chains);
     void BackwardJobs(int step, std::vector<Chain> &chains, const std::vector<DetectedObject> &out,
                       std::vector<Job> &jobs);
     void BackwardStepDone(std::vector<Chain> &chains, std::vector<DetectedObject> &out);
-    void BackwardEnd(std::vector<Chain> &chains, std::vector<DetectedObject> &out);
-    bool StepAvailable(int step) const;
-    // every chain step (LK launch + LocalSearchKLT kernel) enqueued back to back,
-    // one host sync at the end; the forward jobs' launch runs beside them
-    int ChainsOnDevice(std::vector<Chain> &chains, std::vector<DetectedObject> &out, std::vector<Job> *fwd);
+    void BackwardEnd(std::vector<DetectedObject> &out, const std::vector<std::vector<Point2f>> &features);
+    int StepsAvailable(size_t cam) const;  // chain steps the camera's ring holds frames for (0..3)
+    bool StepAvailable(int step) const { return step <= StepsAvailable(0); }
     int EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_jobs);
-    void ForwardJobs(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
+    void ForwardJobs(size_t cam, const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
                      std::vector<Job> &jobs);
     void ForwardDone(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
                      const std::vector<DetectedObject> &dets, std::vector<float> &cost);
+    int DevicePass(const std::vector<Detection> &dets, std::vector<std::vector<Point2f>> &features,
+                   std::vector<DetectedObject> &out, std::vector<Job> *fwd, bool gridfast, uint32_t seed);
 
     psn_lk_ctx *lk_ = nullptr;
-    // device chain: the forward queries run on their own stream (a hipStream_t),
-    // overlapping the backward chain's launches; ev_in_ orders them after the inputs
-    void *fwd_stream_ = nullptr, *ev_in_ = nullptr;
+    void *fwd_stream_ = nullptr;  // hipStream_t of the forward launch, beside the chain's launches
     std::vector<psn_lk_query> fwd_queries_;
-    unsigned camID_ = 0;
+    std::vector<Cam> cams_;
     int width_ = 0, height_ = 0;
-    int ring_[kT2dInterval] = {0, 1, 2, 3};  // slot ids, oldest first; ring_[3] = frame t
-    bool filled_[kT2dInterval] = {false, false, false, false};
+    std::vector<char> filled_;  // per LK slot
     std::string err_;
     // batched-call staging
     std::vector<float> xy_in_, xy_out_, err_out_, gf_xy_;
     std::vector<uint8_t> st_out_;
     std::vector<psn_lk_query> queries_;
+    std::vector<char> win_bad_;  // per chain of a pass: window the LK cannot run (error only if the chain has points)
+    std::vector<PassCam> run_pass_;  // the pass between RunLaunch and RunComplete
+    unsigned run_frame_ = 0;
+    bool run_gridfast_ = false;
     bool device_chain_ = true;
     struct DeviceBuffers;
     DeviceBuffers *dev_ = nullptr;

@@ -4,6 +4,7 @@
 // binary slot exchanged between cameras (ranks) each frame.
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -206,8 +207,12 @@ int psn_t2d_unpack_result(const void *slot, size_t slot_bytes, psn_track2d_resul
     SlotHeader h;
     std::memcpy(&h, p, sizeof h);
     if (h.magic != kMagic || h.version != 1u || h.bytes_used > slot_bytes) return PSN_LK_ERR_ARG;
-    if ((int)h.nobj > r->cap_objects || (int)h.ndet > r->cap_detection_rects || (int)h.ntrk > r->cap_tracker_rects)
+    // unsigned comparisons: a corrupt or foreign count >= 2^31 must not pass as negative
+    auto cap = [](int c) { return (uint32_t)std::max(c, 0); };
+    if (h.nobj > cap(r->cap_objects) || h.ndet > cap(r->cap_detection_rects) || h.ntrk > cap(r->cap_tracker_rects))
         return PSN_T2D_ERR_CAPACITY;
+    if ((h.nobj && !r->objects) || (h.ndet && !r->detection_rects) || (h.ntrk && !r->tracker_rects))
+        return PSN_LK_ERR_ARG;
     r->cam_id = h.cam_id;
     r->frame_idx = h.frame_idx;
     size_t off = sizeof h;
@@ -229,7 +234,7 @@ int psn_t2d_unpack_result(const void *slot, size_t slot_bytes, psn_track2d_resul
         std::memcpy(o.curr, p + off + sizeof so + 8 * (size_t)so.num_prev, 8 * (size_t)so.num_curr);
         off += object_bytes((int)so.num_prev, (int)so.num_curr);
     }
-    if (off + 32 * (size_t)(h.ndet + h.ntrk) > h.bytes_used) return PSN_LK_ERR_ARG;
+    if (off + 32 * ((size_t)h.ndet + (size_t)h.ntrk) > h.bytes_used) return PSN_LK_ERR_ARG;
     for (uint32_t i = 0; i < h.ndet; i++, off += 32) std::memcpy(&r->detection_rects[i], p + off, 32);
     for (uint32_t i = 0; i < h.ntrk; i++, off += 32) std::memcpy(&r->tracker_rects[i], p + off, 32);
     r->num_objects = (int)h.nobj;

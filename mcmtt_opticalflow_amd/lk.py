@@ -52,7 +52,8 @@ def effective_max_level(width, height, win_w, win_h, max_level) -> int:
 class LKContext:
     """One camera: device ring of `ring_slots` pyramids (max_level_cap+1 levels)."""
 
-    def __init__(self, width: int, height: int, ring_slots: int = 4, max_level_cap: int = 3, device: int = 0):
+    def __init__(self, width: int, height: int, ring_slots: int = 4, max_level_cap: int = 3, device: int = 0,
+                 variants: dict | None = None):
         self._L = _lib.load()
         self.width, self.height = width, height
         self.ring_slots, self.max_level_cap = ring_slots, max_level_cap
@@ -61,6 +62,12 @@ class LKContext:
         if rc != 0:
             raise PsnLkError(rc, "psn_lk_create")
         self._h = h
+        for k, v in (variants or {}).items():
+            self.set_variant(k, v)
+
+    def set_variant(self, key: str, value: int):
+        """Kernel-variant override (psn_lk_debug_set_variant): tests and experiments only."""
+        self._check(self._L.psn_lk_debug_set_variant(self._h, _lib.VARIANTS[key], int(value)), f"set_variant {key}")
 
     def _check(self, rc, what):
         if rc != 0:
@@ -103,6 +110,14 @@ class LKContext:
         ch = 1 if img.ndim == 2 else img.shape[2]
         assert img.shape[0] == self.height and img.shape[1] == self.width
         self._check(self._L.psn_lk_push_frame(self._h, slot, img.ctypes.data, img.shape[1] * ch, ch), "push_frame")
+
+    def push_frame_async(self, slot: int, img: np.ndarray):
+        """Asynchronous upload + build (psn_lk_push_frame_async): `img` must stay
+        alive and unchanged until sync() (pinned memory makes the copy async)."""
+        ch = 1 if img.ndim == 2 else img.shape[2]
+        assert img.flags["C_CONTIGUOUS"] and img.dtype == np.uint8
+        self._check(self._L.psn_lk_push_frame_async(self._h, slot, img.ctypes.data, img.shape[1] * ch, ch),
+                    "push_frame_async")
 
     def push_frame_device(self, slot: int, dev_ptr: int, stride: int, channels: int = 1):
         self._check(self._L.psn_lk_push_frame_device(self._h, slot, dev_ptr, stride, channels), "push_frame_device")
@@ -196,11 +211,12 @@ class LKContext:
 
 def calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size=(21, 21), max_level=3,
                              criteria=(3, 30, 0.01), flags=0, min_eig_threshold=1e-4, next_pts=None,
-                             want_err=True, device=0):
-    """cv::calcOpticalFlowPyrLK on MI355X (one-shot; allocates a context)."""
+                             want_err=True, device=0, variants=None):
+    """cv::calcOpticalFlowPyrLK on MI355X (one-shot; allocates a context).
+    `variants`: kernel-variant overrides for tests (LKContext.set_variant)."""
     h, w = np.asarray(prev_img).shape[:2]
     cap = max(0, effective_max_level(w, h, win_size[0], win_size[1], max_level))
-    with LKContext(w, h, ring_slots=1, max_level_cap=min(cap, 5), device=device) as ctx:
+    with LKContext(w, h, ring_slots=1, max_level_cap=min(cap, 5), device=device, variants=variants) as ctx:
         return ctx.calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size, max_level, criteria,
                                             flags, min_eig_threshold, next_pts, want_err)
 

@@ -48,6 +48,9 @@ _PTS = ctypes.c_float * 2 * MAX_FEATURES
 class Detection(ctypes.Structure):
     _fields_ = [
         ("box", Rect),
+        ("head", Rect),
+        ("location", ctypes.c_double * 3),
+        ("height", ctypes.c_double),
         ("num_features", ctypes.c_int),
         ("features", _PTS),
         ("valid", ctypes.c_int),
@@ -62,9 +65,17 @@ class Detection(ctypes.Structure):
 
 class Tracker(ctypes.Structure):
     _fields_ = [
+        ("id", ctypes.c_uint),
+        ("time_start", ctypes.c_uint),
+        ("time_end", ctypes.c_uint),
+        ("time_last_update", ctypes.c_uint),
         ("duration", ctypes.c_uint),
         ("num_boxes", ctypes.c_int),
         ("boxes", Rect * MAX_BOXES),
+        ("heads", Rect * MAX_BOXES),
+        ("last_position", ctypes.c_double * 3),
+        ("height", ctypes.c_double),
+        ("confidence", ctypes.c_double),
         ("num_features", ctypes.c_int),
         ("features", _PTS),
         ("num_tracked", ctypes.c_int),
@@ -139,6 +150,25 @@ def load():
     L.psn_t2d_backward.argtypes = [vp, ctypes.POINTER(Detection), ip]
     L.psn_t2d_forward.argtypes = [vp, ctypes.POINTER(Tracker), ip, ctypes.POINTER(Detection), ip, fp]
     L.psn_t2d_track_frame.argtypes = [vp, ctypes.POINTER(Detection), ip, ctypes.POINTER(Tracker), ip, fp]
+    L.psn_t2d_abi_version.restype = ip
+    L.psn_t2d_assign.argtypes = [fp, ip, ip, vp]
+    L.psn_t2d_result_with_tracker.argtypes = [ctypes.POINTER(Tracker), ctypes.POINTER(Object2D)]
+    L.psn_t2d_matching_and_updating.argtypes = [ctypes.POINTER(Detection), ip, ctypes.POINTER(Tracker), ip, fp, vp,
+                                                ctypes.c_uint, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(Tracker),
+                                                ip, ctypes.POINTER(ip), ctypes.POINTER(Track2DResult)]
+    L.psn_t2d_group_create.argtypes = [ip, ip, vp, ip, ip, ctypes.POINTER(vp)]
+    L.psn_t2d_group_destroy.argtypes = [vp]
+    L.psn_t2d_group_destroy.restype = None
+    L.psn_t2d_group_last_error.argtypes = [vp]
+    L.psn_t2d_group_last_error.restype = ctypes.c_char_p
+    L.psn_t2d_group_lk_context.argtypes = [vp]
+    L.psn_t2d_group_lk_context.restype = vp
+    L.psn_t2d_group_push_frame.argtypes = [vp, ip, vp, ip, ip]
+    L.psn_t2d_group_push_frame_device.argtypes = [vp, ip, vp, ip, ip]
+    L.psn_t2d_group_launch.argtypes = [vp, ctypes.c_uint, vp, vp, ip, ctypes.c_uint32]
+    L.psn_t2d_group_complete.argtypes = [vp, vp, vp, ctypes.POINTER(Track2DResult)]
+    L.psn_t2d_group_run.argtypes = [vp, ctypes.c_uint, vp, vp, ip, ctypes.c_uint32, ctypes.POINTER(Track2DResult)]
+    L.psn_t2d_group_trackers.argtypes = [vp, ip, ctypes.POINTER(Tracker), ip, ctypes.POINTER(ip)]
     _lib = L
     return L
 
@@ -161,9 +191,15 @@ def local_search_klt(pre_box, pre: np.ndarray, cur: np.ndarray):
     return out.tuple(), idx[:ni.value].tolist()
 
 
-def make_detection(box, features) -> Detection:
+def make_detection(box, features, head=None, location=(0.0, 0.0, 0.0), height=0.0) -> Detection:
+    """A detection record: box, features at t, head box (vecPartBoxes.front(); default: the box)
+    and the caller's 3D estimate (location, height)."""
     d = Detection()
     d.box = rect(*box)
+    d.head = rect(*(head if head is not None else box))
+    for k in range(3):
+        d.location[k] = float(location[k])
+    d.height = float(height)
     f = np.asarray(features, np.float32).reshape(-1, 2)
     if len(f) > MAX_FEATURES:
         raise ValueError("more than PSN_T2D_MAX_FEATURES points")
@@ -172,12 +208,15 @@ def make_detection(box, features) -> Detection:
     return d
 
 
-def make_tracker(boxes, features, duration=None) -> Tracker:
+def make_tracker(boxes, features, duration=None, heads=None, id_=0) -> Tracker:
     t = Tracker()
+    t.id = id_
     t.num_boxes = len(boxes)
     for i, b in enumerate(boxes):
         t.boxes[i] = rect(*b)
+        t.heads[i] = rect(*(heads[i] if heads is not None else b))
     t.duration = len(boxes) if duration is None else duration
+    t.confidence = 1.0
     f = np.asarray(features, np.float32).reshape(-1, 2)
     t.num_features = len(f)
     ctypes.memmove(t.features, f.ctypes.data, f.nbytes)
@@ -278,6 +317,137 @@ class FlowTracker:
         return dets_out, list(ta)[:len(trackers)], cost[:nvalid * len(trackers)].reshape(nvalid, len(trackers))
 
 
+def assign(cost: np.ndarray) -> list[int]:
+    """psn_t2d_assign: the Hungarian step of Track2D_MatchingAndUpdating -> column per row or -1."""
+    c = np.ascontiguousarray(cost, np.float32)
+    rows, cols = c.shape
+    m = np.full(max(rows, 1), -2, np.int32)
+    rc = load().psn_t2d_assign(c.ctypes.data, rows, cols, m.ctypes.data)
+    if rc:
+        raise T2dError(rc, "psn_t2d_assign")
+    return m[:rows].tolist()
+
+
+def result_with_tracker(trk: Tracker) -> dict:
+    o = Object2D()
+    rc = load().psn_t2d_result_with_tracker(ctypes.byref(trk), ctypes.byref(o))
+    if rc:
+        raise T2dError(rc, "psn_t2d_result_with_tracker")
+    return object_dict(o)
+
+
+def object_dict(o) -> dict:
+    return {"id": o.id, "box": o.box.tuple(), "head": o.head.tuple(), "score": o.score,
+            "prev": points(o.prev, o.num_prev), "curr": points(o.curr, o.num_curr)}
+
+
+def matching_and_updating(dets: list[Detection], trackers: list[Tracker], cost, frame_idx: int, next_id: int,
+                          match=None, cam_id: int = 0, cap=64):
+    """psn_t2d_matching_and_updating -> (new active trackers, result dict, next id)."""
+    L = load()
+    da = (Detection * max(len(dets), 1))(*dets)
+    ta = (Tracker * max(len(trackers), 1))(*trackers)
+    c = np.ascontiguousarray(cost if cost is not None else np.zeros((0, 0)), np.float32)
+    m = None if match is None else np.ascontiguousarray(match, np.int32)
+    out = (Tracker * cap)()
+    nout, nid = ctypes.c_int(), ctypes.c_uint(next_id)
+    rb = ResultBuffers(cap, 1)
+    rb.r.cam_id = cam_id
+    rc = L.psn_t2d_matching_and_updating(da, len(dets), ta, len(trackers), c.ctypes.data if c.size else None,
+                                         m.ctypes.data if m is not None else None, frame_idx, ctypes.byref(nid),
+                                         out, cap, ctypes.byref(nout), ctypes.byref(rb.r))
+    if rc:
+        raise T2dError(rc, "psn_t2d_matching_and_updating")
+    return list(out)[:nout.value], rb.to_dict(), nid.value
+
+
+class Group:
+    """psn_t2d_group: CPSNWhere_Tracker2D::Run of C cameras on one device,
+    every camera's LK work batched into the same launches."""
+
+    def __init__(self, width: int, height: int, cam_ids, device: int = 0, max_objects: int = 64):
+        self._L = load()
+        ids = (ctypes.c_uint * len(cam_ids))(*cam_ids)
+        h = ctypes.c_void_p()
+        rc = self._L.psn_t2d_group_create(device, len(cam_ids), ids, width, height, ctypes.byref(h))
+        if rc:
+            raise T2dError(rc, "psn_t2d_group_create")
+        self._h = h
+        self.ncams = len(cam_ids)
+        self.width, self.height = width, height
+        self.results = [ResultBuffers(max_objects, 1) for _ in range(self.ncams)]
+        self._res = (Track2DResult * self.ncams)(*[r.r for r in self.results])
+        self._keep = None
+
+    def _check(self, rc, what):
+        if rc:
+            raise T2dError(rc, f"{what}: {self._L.psn_t2d_group_last_error(self._h).decode()}")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psn_t2d_group_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def lk_handle(self) -> int:
+        return self._L.psn_t2d_group_lk_context(self._h)
+
+    def push_frame(self, cam: int, img: np.ndarray):
+        """Asynchronous upload of camera `cam`'s frame t (must stay alive until complete())."""
+        assert img.flags["C_CONTIGUOUS"] and img.dtype == np.uint8
+        ch = 1 if img.ndim == 2 else img.shape[2]
+        self._check(self._L.psn_t2d_group_push_frame(self._h, cam, img.ctypes.data, img.shape[1] * ch, ch),
+                    "push_frame")
+
+    def push_frame_device(self, cam: int, dev_ptr: int, stride: int, channels: int = 1):
+        self._check(self._L.psn_t2d_group_push_frame_device(self._h, cam, ctypes.c_void_p(dev_ptr), stride, channels),
+                    "push_frame_device")
+
+    def launch(self, frame_idx: int, dets_per_cam, gridfast: bool = False, seed: int = 0):
+        """dets_per_cam[c]: list of Detection records of camera c (kept alive until complete())."""
+        arrs = [(Detection * max(len(d), 1))(*d) for d in dets_per_cam]
+        ptrs = (ctypes.c_void_p * self.ncams)(*[ctypes.addressof(a) for a in arrs])
+        nd = (ctypes.c_int * self.ncams)(*[len(d) for d in dets_per_cam])
+        self._keep = (arrs, ptrs, nd)
+        self._check(self._L.psn_t2d_group_launch(self._h, frame_idx, ptrs, nd, int(bool(gridfast)),
+                                                 ctypes.c_uint32(seed & 0xffffffff)), "launch")
+
+    def complete(self):
+        """-> (per camera: list of output Detection records, result dict)."""
+        arrs, ptrs, nd = self._keep
+        self._check(self._L.psn_t2d_group_complete(self._h, ptrs, nd, self._res), "complete")
+        self._keep = None
+        out = []
+        for c in range(self.ncams):
+            self.results[c].r = self._res[c]
+            out.append((list(arrs[c])[:nd[c]], self.results[c].to_dict()))
+        return out
+
+    def complete_raw(self):
+        """complete() without converting the results (the caller packs self.result_struct(c))."""
+        arrs, ptrs, nd = self._keep
+        self._check(self._L.psn_t2d_group_complete(self._h, ptrs, nd, self._res), "complete")
+        self._keep = None
+
+    def result_struct(self, cam: int):
+        return self._res[cam]
+
+    def run(self, frame_idx: int, dets_per_cam, gridfast: bool = False, seed: int = 0):
+        self.launch(frame_idx, dets_per_cam, gridfast, seed)
+        return self.complete()
+
+    def trackers(self, cam: int, cap: int = 256) -> list[Tracker]:
+        out = (Tracker * cap)()
+        n = ctypes.c_int()
+        self._check(self._L.psn_t2d_group_trackers(self._h, cam, out, cap, ctypes.byref(n)), "trackers")
+        return list(out)[:n.value]
+
+
 # ---- stTrack2DResult formats (tracker2d_io.cpp) ----
 
 class ResultBuffers:
@@ -317,14 +487,10 @@ class ResultBuffers:
 
     def to_dict(self):
         r = self.r
-        objs = []
-        for i in range(r.num_objects):
-            o = self.objs[i]
-            objs.append({"id": o.id, "box": o.box.tuple(), "head": o.head.tuple(), "score": o.score,
-                         "prev": points(o.prev, o.num_prev), "curr": points(o.curr, o.num_curr)})
+        objs = [object_dict(r.objects[i]) for i in range(r.num_objects)]
         return {"cam_id": r.cam_id, "frame_idx": r.frame_idx, "objects": objs,
-                "detection_rects": [self.dets[i].tuple() for i in range(r.num_detection_rects)],
-                "tracker_rects": [self.trks[i].tuple() for i in range(r.num_tracker_rects)]}
+                "detection_rects": [r.detection_rects[i].tuple() for i in range(r.num_detection_rects)],
+                "tracker_rects": [r.tracker_rects[i].tuple() for i in range(r.num_tracker_rects)]}
 
 
 def write_result_txt(dirpath: str, result: dict):

@@ -8,14 +8,21 @@ full frames through oracle.calc_optical_flow_pyr_lk):
   box_matching_cost       :600-613
   backward_tracking       :690-838
   forward_tracking        :851-1025
+  assign / matching_and_updating / result_with_tracker   :1038-1164, :1231-1257
+  CameraTracker.run       Run (:251-373) minus ingest and the height gate
 and PSN_Rect arithmetic (PSNWhere_Types.h:112-182). Python floats are IEEE
 doubles (the reference's double math); cv::Point2f differences are float32.
 Only tests import this module.
 
-PARITY UNPINNED (the reference ships no tests or fixtures for this path).
+PARITY UNPINNED (the reference ships no tests or fixtures for this path). The
+assignment is the exhaustive minimum of the reference's cost (the reference's
+own CPSNWhere_Hungarian needs MSVC CRT functions, _isnanf / _finitef, and is
+not built here); where several assignments tie the reference's Munkres order
+is not reproduced.
 """
 from __future__ import annotations
 
+import itertools
 import math
 
 import numpy as np
@@ -133,21 +140,26 @@ def _lk(prev_img, next_img, pts, win):
 
 
 class DetectedObject:
-    def __init__(self, id_, box: Rect):
+    def __init__(self, id_, box: Rect, head=None, location=(0.0, 0.0, 0.0), height=0.0):
         self.id = id_
         self.box = box
+        self.head = head if head is not None else Rect(*box.tuple())
+        self.location = tuple(float(v) for v in location)
+        self.height = float(height)
         self.boxes = [box]
         self.sets = []
         self.overlap_other = False
+        self.matched = False
 
 
-def backward_tracking(ring, dets, features):
+def backward_tracking(ring, dets, features, extra=None):
     """:690-838. ring: 4 gray frames oldest first (None = empty slot), ring[-1]
     = frame t; dets: height-validated boxes; features: points at t per
-    detection (after shuffle + cap). Returns m_vecDetection2D."""
+    detection (after shuffle + cap); extra[i] = (head, location, height) of
+    detection i (the caller's calibration). Returns m_vecDetection2D."""
     out = []
     for i, box in enumerate(dets):
-        obj = DetectedObject(i, box)
+        obj = DetectedObject(i, box, *(extra[i] if extra is not None else ()))
         f = np.asarray(features[i], np.float32).reshape(-1, 2)
         if len(f) < MIN_FEATURES:
             continue
@@ -183,12 +195,18 @@ def backward_tracking(ring, dets, features):
 
 
 class Tracker:
-    def __init__(self, boxes, features, duration=None):
+    def __init__(self, boxes, features, duration=None, heads=None, id_=0):
         self.boxes = [Rect(*b) if not isinstance(b, Rect) else b for b in boxes]
+        self.heads = [Rect(*b.tuple()) for b in self.boxes] if heads is None else \
+            [Rect(*h) if not isinstance(h, Rect) else h for h in heads]
         self.duration = len(self.boxes) if duration is None else duration
         self.features = np.asarray(features, np.float32).reshape(-1, 2)
         self.tracked = np.zeros((0, 2), np.float32)
         self.updated = False
+        self.id = id_
+        self.time_start = self.time_end = self.time_last_update = 0
+        self.last_position = (0.0, 0.0, 0.0)
+        self.height = 0.0
 
 
 def forward_tracking(ring, trackers, dets):
@@ -208,6 +226,7 @@ def forward_tracking(ring, trackers, dets):
         new_box, _ = local_search_klt(tr.boxes[-1].scale(SCALE), v_prev, v_curr)
         new_box = new_box.scale(1.0 / SCALE)
         tr.boxes.append(new_box)
+        tr.heads.append(tr.heads[-1])  # :896
         tr.updated = True
         for d, det in enumerate(dets):
             if not new_box.overlap(det.box):
@@ -253,3 +272,98 @@ def forward_tracking(ring, trackers, dets):
             continue
         cost[d, :] = np.inf
     return cost
+
+
+# ---------------------------------------------------------------------------
+# After the flow: Track2D_MatchingAndUpdating (:1038-1164), ResultWithTracker
+# ---------------------------------------------------------------------------
+
+def assign(cost: np.ndarray) -> list:
+    """:1040-1064: non-finite costs -> max(finite) + 100 (float32), a minimum
+    total-cost set of min(D, T) pairs (exhaustive), pairs at the substitute cost
+    dropped. Returns the tracker index per detection or -1."""
+    c = np.array(cost, np.float32, copy=True)
+    D, T = c.shape
+    if D == 0 or T == 0:
+        return [-1] * D
+    fin = c[np.isfinite(c)]
+    max_cost = np.float32(np.float32(fin.max() if fin.size and fin.max() > -1000.0 else -1000.0) + np.float32(100.0))
+    c[~np.isfinite(c)] = max_cost
+    best, best_pairs = None, None
+    if D <= T:
+        for perm in itertools.permutations(range(T), D):
+            tot = sum(float(c[d, perm[d]]) for d in range(D))
+            if best is None or tot < best:
+                best, best_pairs = tot, [(d, perm[d]) for d in range(D)]
+    else:
+        for perm in itertools.permutations(range(D), T):
+            tot = sum(float(c[perm[t], t]) for t in range(T))
+            if best is None or tot < best:
+                best, best_pairs = tot, [(perm[t], t) for t in range(T)]
+    match = [-1] * D
+    for d, t in best_pairs:
+        if c[d, t] != max_cost:
+            match[d] = t
+    return match
+
+
+def result_with_tracker(tr: Tracker) -> dict:
+    """:1231-1257 (PSN_2D_DEBUG_DISPLAY_SCALE 1.0)."""
+    return {"id": tr.id, "box": tr.boxes[-1].tuple(), "head": tr.heads[-1].tuple(), "score": 0.0,
+            "prev": np.asarray(tr.features, np.float32).reshape(-1, 2).copy(),
+            "curr": np.asarray(tr.tracked, np.float32).reshape(-1, 2).copy()}
+
+
+def matching_and_updating(dets, active, match, frame_idx, next_id):
+    """:1062-1164 -> (new active queue, result objects, next id)."""
+    objects, nxt = [], []
+    for d, det in enumerate(dets):
+        t = match[d]
+        if t < 0:
+            continue
+        tr = active[t]
+        dist = math.sqrt(sum((det.location[k] - tr.last_position[k]) ** 2 for k in range(3)))
+        if dist > 600.0 or abs(det.height - tr.height) > 400.0 or tr.duration > 3:
+            continue
+        det.matched = True
+        tr.time_end = tr.time_last_update = frame_idx
+        tr.duration = tr.time_end - tr.time_start + 1
+        tr.boxes[-1] = det.box
+        tr.heads[-1] = det.head
+        tr.last_position, tr.height = det.location, det.height
+        nxt.append(tr)
+        objects.append(result_with_tracker(tr))
+        tr.features = det.sets[0].copy()
+        tr.tracked = np.zeros((0, 2), np.float32)
+    for det in dets:
+        if det.matched:
+            continue
+        tr = Tracker([det.box], det.sets[0], duration=1, heads=[det.head], id_=next_id)
+        next_id += 1
+        tr.time_start = tr.time_end = tr.time_last_update = frame_idx
+        tr.last_position, tr.height = det.location, det.height
+        nxt.append(tr)
+        objects.append(result_with_tracker(tr))
+    return nxt, objects, next_id
+
+
+class CameraTracker:
+    """One camera's CPSNWhere_Tracker2D::Run state (ring, active trackers,
+    tracker ids) in the reference schedule."""
+
+    def __init__(self, cam_id=0):
+        self.cam_id = cam_id
+        self.ring = [None] * INTERVAL
+        self.active = []
+        self.next_id = 0
+
+    def run(self, frame, dets, features, frame_idx, extra=None):
+        """-> (m_vecDetection2D, matching cost [D x T], result dict)."""
+        self.ring = self.ring[1:] + [frame]
+        objs = backward_tracking(self.ring, dets, features, extra)
+        trackers = list(self.active)
+        cost = forward_tracking(self.ring, trackers, objs) if trackers else np.zeros((len(objs), 0), np.float32)
+        match = assign(cost)
+        self.active, objects, self.next_id = matching_and_updating(objs, trackers, match, frame_idx, self.next_id)
+        return objs, cost, {"cam_id": self.cam_id, "frame_idx": frame_idx, "objects": objects,
+                            "detection_rects": [], "tracker_rects": []}

@@ -241,17 +241,15 @@ def test_lk_device_pointer_path(oracle_mod, overlap):
     assert_same(gpu, ref, "device path")
 
 
-@pytest.mark.parametrize("env", [{}, {"PSN_LK_THREADS": "128"}, {"PSN_LK_THREADS": "64"}, {"PSN_LK_THREADS": "512"}])
+@pytest.mark.parametrize("env", [{}, {"threads": 128}, {"threads": 64}, {"threads": 512}])
 @pytest.mark.parametrize("win", [(21, 21), (9, 9), (64, 64)])
-def test_lk_fused_ingest_pipeline(oracle_mod, monkeypatch, env, win):
+def test_lk_fused_ingest_pipeline(oracle_mod, env, win):
     """Fused ingest (PSN_LK_OVERLAP_FUSED): frame t+1 is pushed before frame t
     is tracked, so its pyramid is built by the tail workgroups of the t-1 -> t
     launch (or, for windows the single-tile kernel does not take, by its own
     launch). Pyramids and propagated points must match the oracle bit for bit."""
     import hiprt
 
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     W, H, R, T = 640, 480, 4, 7
     sc = synth.make_scene(12, W, H, 96)
     frames = [sc.frame(t) for t in range(T)]
@@ -260,7 +258,7 @@ def test_lk_fused_ingest_pipeline(oracle_mod, monkeypatch, env, win):
     n = len(p_ref)
     d_pts = [hiprt.DeviceBuffer.from_array(p_ref), hiprt.DeviceBuffer(p_ref.nbytes)]
     d_s, d_e = hiprt.DeviceBuffer(n), hiprt.DeviceBuffer(4 * n)
-    with glk.LKContext(W, H, ring_slots=R, max_level_cap=3) as ctx:
+    with glk.LKContext(W, H, ring_slots=R, max_level_cap=3, variants=env) as ctx:
         ctx.set_ingest_overlap(2)
         ctx.push_frame_device(0, d_frames[0].addr, W, 1)
         ctx.push_frame_device(1, d_frames[1].addr, W, 1)
@@ -290,15 +288,13 @@ def test_lk_config5_4k_5level(oracle_mod):
     assert_same(gpu, ref, "4k")
 
 
-@pytest.mark.parametrize("env", [{}, {"PSN_LK_ONEWAVE": "0"}, {"PSN_LK_GENERIC": "1"}, {"PSN_LK_THREADS": "64"},
-                                 {"PSN_LK_THREADS": "128"}, {"PSN_LK_THREADS": "512"},
-                                 {"PSN_LK_GENERIC": "1", "PSN_LK_THREADS": "64"}])
+@pytest.mark.parametrize("env", [{}, {"onewave": 0}, {"generic": 1}, {"threads": 64},
+                                 {"threads": 128}, {"threads": 512},
+                                 {"generic": 1, "threads": 64}])
 @pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
-def test_lk_kernel_variants(oracle_mod, monkeypatch, env, flags):
+def test_lk_kernel_variants(oracle_mod, env, flags):
     """The single-tile and the tiled kernel, at every workgroup size, give the
     same bits (both are checked against the oracle)."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
     sc, f0, f1 = scene_pair(10, 640, 480, 96)
     pts = sc.points_at(0)
     # one-wave mode row counts: 21x21 -> 7 rows/lane, 9x15 -> 4, 32x32 -> 16,
@@ -306,7 +302,7 @@ def test_lk_kernel_variants(oracle_mod, monkeypatch, env, flags):
     # 40x20 -> 20 rows: multi-wave iterations
     for win in [(21, 21), (9, 15), (32, 32), (24, 16), (7, 7), (12, 70), (40, 20)]:
         ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
-        gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
+        gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags, variants=env)
         assert_same(gpu, ref, f"{env} {win}")
 
 
@@ -348,15 +344,14 @@ def test_lk_counted_launch(oracle_mod, win):
 @pytest.mark.parametrize("win,flags", [((33, 33), 0), ((37, 50), 0), ((70, 45), 0), ((66, 100), 0), ((45, 120), 0),
                                        ((64, 160), 0), ((96, 128), 0), ((64, 64), ACCUM_SCALAR),
                                        ((45, 120), ACCUM_SCALAR), ((64, 64), GET_MIN_EIGENVALS)])
-def test_lk_box_kernel_windows(oracle_mod, monkeypatch, kernel, win, flags):
+def test_lk_box_kernel_windows(oracle_mod, kernel, win, flags):
     """Box windows above the single-tile size: lk_kernel_bx (units of 4 pixels,
-    per-chain prefix exactness) and the row-tiled kernel (PSN_LK_BOX=0) against
+    per-chain prefix exactness) and the row-tiled kernel (variant box=0) against
     the oracle -- SSE2 tails (w % 8), partial quads (w % 4), the scalar build,
     border points."""
-    monkeypatch.setenv("PSN_LK_BOX", "1" if kernel == "box" else "0")
     sc, f0, f1 = scene_pair(6, 1920, 1080, 40)
     pts = np.concatenate([sc.points_at(0), np.array([[3, 4], [1915.5, 1077.25], [-20, 500], [960, 1079.5]],
                                                      np.float32)])
     ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
-    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags, variants={"box": int(kernel == "box")})
     assert_same(gpu, ref, f"{kernel} win {win} flags {flags}")

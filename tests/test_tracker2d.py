@@ -245,3 +245,95 @@ def test_tracker2d_errors():
         bad = t2d.make_tracker([(10, 10, 20, 40)], np.zeros((5, 2), np.float32), duration=3)
         with pytest.raises(t2d.T2dError):
             ft.forward([bad], [])
+
+
+# ---------------------------------------------------------------------------
+# After the flow: assignment, tracker update, ResultWithTracker (:1038-1257)
+# ---------------------------------------------------------------------------
+
+def _rand_cost(rng, D, T):
+    c = rng.uniform(0.0, 3.0, (D, T)).astype(np.float32)
+    c[rng.random((D, T)) < 0.35] = np.inf
+    return c
+
+
+def test_assign_matches_oracle():
+    rng = np.random.default_rng(31)
+    for trial in range(400):
+        D, T = int(rng.integers(0, 6)), int(rng.integers(0, 6))
+        c = _rand_cost(rng, D, T)
+        assert t2d.assign(c) == ORC.assign(c), (trial, c)
+    # all infinite: every pair sits at the substitute cost, nothing matches
+    assert t2d.assign(np.full((3, 2), np.inf, np.float32)) == [-1, -1, -1]
+    # the substitute (max + 100) can win over several finite pairs, as in the reference
+    c = np.array([[90, np.inf, np.inf], [np.inf, 90, 0.0], [np.inf, 0.0, np.inf]], np.float32)
+    assert t2d.assign(c) == ORC.assign(c)
+
+
+def _rand_tracker(rng, id_, nb):
+    boxes = [(float(rng.uniform(0, 300)), float(rng.uniform(0, 200)), 40.0, 100.0) for _ in range(nb)]
+    heads = [(b[0] + 10, b[1], 20.0, 20.0) for b in boxes]
+    f = rng.uniform(0, 300, (int(rng.integers(0, 30)), 2)).astype(np.float32)
+    tr = t2d.make_tracker(boxes, f, duration=nb, heads=heads, id_=id_)
+    tk = rng.uniform(0, 300, (int(rng.integers(0, len(f) + 1)), 2)).astype(np.float32)
+    tr.num_tracked = len(tk)
+    ctypes.memmove(tr.tracked, tk.ctypes.data, tk.nbytes)
+    o = ORC.Tracker(boxes, f, duration=nb, heads=heads, id_=id_)
+    o.tracked = tk
+    return tr, o
+
+
+def test_result_with_tracker_matches_oracle():
+    rng = np.random.default_rng(8)
+    for k in range(50):
+        tr, o = _rand_tracker(rng, 100 + k, int(rng.integers(1, 6)))
+        g, r = t2d.result_with_tracker(tr), ORC.result_with_tracker(o)
+        assert (g["id"], g["box"], g["head"], g["score"]) == (r["id"], r["box"], r["head"], r["score"])
+        np.testing.assert_array_equal(g["prev"], r["prev"])
+        np.testing.assert_array_equal(g["curr"], r["curr"])
+
+
+def test_matching_and_updating_matches_oracle():
+    """Random post-forward states: matches pass or fail the 3D validation (distance
+    600 mm, height 400 mm, duration 3); new trackers take ids in detection order;
+    unmatched trackers end; result objects in the reference's order."""
+    rng = np.random.default_rng(12)
+    for trial in range(120):
+        D, T = int(rng.integers(0, 6)), int(rng.integers(0, 6))
+        g_trk, o_trk = zip(*[_rand_tracker(rng, 10 + i, int(rng.integers(1, 6))) for i in range(T)]) if T else ((), ())
+        g_trk, o_trk = list(g_trk), list(o_trk)
+        for gt, ot in zip(g_trk, o_trk):
+            pos, h = tuple(rng.uniform(-500, 500, 3)), float(rng.uniform(1500, 2000))
+            gt.last_position[:] = pos
+            gt.height = h
+            ot.last_position, ot.height = pos, h
+            gt.time_start = ot.time_start = int(rng.integers(0, 5))
+        g_det, o_det = [], []
+        for i in range(D):
+            box = (float(rng.uniform(0, 300)), float(rng.uniform(0, 200)), 40.0, 100.0)
+            head = (box[0] + 12, box[1] + 1, 18.0, 22.0)
+            loc, h = tuple(rng.uniform(-700, 700, 3)), float(rng.uniform(1400, 2300))
+            f = rng.uniform(0, 300, (int(rng.integers(4, 40)), 2)).astype(np.float32)
+            d = t2d.make_detection(box, np.zeros((0, 2), np.float32), head=head, location=loc, height=h)
+            d.valid, d.num_boxes, d.num_sets, d.set_count[0] = 1, 1, 1, len(f)
+            d.boxes[0] = t2d.rect(*box)
+            ctypes.memmove(d.sets[0], f.ctypes.data, f.nbytes)
+            g_det.append(d)
+            od = ORC.DetectedObject(i, ORC.Rect(*box), ORC.Rect(*head), loc, h)
+            od.sets = [f]
+            o_det.append(od)
+        cost = _rand_cost(rng, D, T)
+        g_out, g_res, g_next = t2d.matching_and_updating(g_det, g_trk, cost, 7, 50, cam_id=3)
+        o_act, o_objs, o_next = ORC.matching_and_updating(o_det, o_trk, ORC.assign(cost), 7, 50)
+        assert g_next == o_next and len(g_out) == len(o_act) == len(g_res["objects"]) == len(o_objs), trial
+        assert g_res["cam_id"] == 3 and g_res["frame_idx"] == 7
+        for gt, ot in zip(g_out, o_act):
+            assert (gt.id, gt.duration, gt.time_start, gt.time_end) == (ot.id, ot.duration, ot.time_start, ot.time_end)
+            assert [gt.boxes[i].tuple() for i in range(gt.num_boxes)] == [b.tuple() for b in ot.boxes]
+            assert [gt.heads[i].tuple() for i in range(gt.num_boxes)] == [b.tuple() for b in ot.heads]
+            assert tuple(gt.last_position) == tuple(ot.last_position) and gt.height == ot.height
+            np.testing.assert_array_equal(t2d.points(gt.features, gt.num_features), ot.features)
+        for go, oo in zip(g_res["objects"], o_objs):
+            assert (go["id"], go["box"], go["head"], go["score"]) == (oo["id"], oo["box"], oo["head"], oo["score"])
+            np.testing.assert_array_equal(go["prev"], oo["prev"])
+            np.testing.assert_array_equal(go["curr"], oo["curr"])

@@ -1,0 +1,136 @@
+"""CPSNWhere_Tracker2D::Run of several cameras in one group (psn_t2d_group_*,
+include/psn_tracker2d.h): every camera's backward chain steps and forward calls
+share LK launches, frames are uploaded asynchronously into staging slots (frame
+t+1 while frame t runs), and after the flow the matching, tracker update and
+ResultWithTracker produce each camera's stTrack2DResult.
+
+Checked against oracle/tracker2d_oracle.py's CameraTracker (the reference
+schedule: one calcOpticalFlowPyrLK per detection per chain step and per tracker,
+both pyramids rebuilt in each) bit for bit: detections (boxes, point sets),
+result objects (ids, boxes, heads, featurePointsPrev/Curr) and the surviving
+trackers. Parity with OpenCV itself is unpinned.
+"""
+import numpy as np
+import pytest
+
+from mcmtt_opticalflow_amd import synth
+from mcmtt_opticalflow_amd import tracker2d as t2d
+
+ORC = pytest.importorskip("tracker2d_oracle")
+
+pytestmark = pytest.mark.gpu
+
+
+def _bgr(gray, seed):
+    """A BGR frame whose BGR2GRAY is computed by the oracle (exercises the fused ingest)."""
+    rng = np.random.default_rng(seed)
+    d = rng.integers(-6, 7, gray.shape + (3,))
+    return np.clip(gray[..., None].astype(np.int32) + d, 0, 255).astype(np.uint8)
+
+
+def _camera_dets(sc, t, rng, tiny=False):
+    """Detections at frame t: integer boxes, head boxes, a 3D estimate, and
+    stand-in GridFAST points inside the boxes; optionally a 2-px-wide detection
+    with 3 points (dropped before its LK call, :744 -- its 2x2 window must not
+    fail the frame)."""
+    boxes, extra, feats = [], [], []
+    for k, (bx, by) in enumerate(sc.box_at(t)):
+        box = (float(np.floor(bx)), float(np.floor(by)), float(sc.box_w), float(sc.box_h))
+        head = (box[0] + box[2] / 4, box[1], box[2] / 2, box[3] / 8)
+        loc = (box[0] * 10.0, box[1] * 10.0, 0.0)
+        n = int(rng.integers(20, 101))
+        feats.append(np.stack([rng.uniform(box[0] + 2, box[0] + box[2] - 2, n),
+                               rng.uniform(box[1] + 2, box[1] + box[3] - 2, n)], 1).astype(np.float32))
+        boxes.append(box)
+        extra.append((head, loc, 1700.0))
+    if tiny:
+        boxes.append((5.0, 5.0, 2.0, 30.0))
+        extra.append(((5.0, 5.0, 2.0, 4.0), (0.0, 0.0, 0.0), 1700.0))
+        feats.append(np.float32([[5.5, 9], [6, 12], [5.2, 20]]))
+    return boxes, extra, feats
+
+
+def _rois(boxes, W, H):
+    out = []
+    for b in boxes:
+        x, y = max(0.0, b[0]), max(0.0, b[1])
+        out.append((int(x), int(y), int(min(W - x - 1, b[2])), int(min(H - y - 1, b[3]))))
+    return out
+
+
+def _check_result(g_res, r_res, what):
+    assert (g_res["cam_id"], g_res["frame_idx"]) == (r_res["cam_id"], r_res["frame_idx"]), what
+    assert len(g_res["objects"]) == len(r_res["objects"]), what
+    for go, ro in zip(g_res["objects"], r_res["objects"]):
+        assert (go["id"], go["box"], go["head"], go["score"]) == (ro["id"], ro["box"], ro["head"], ro["score"]), what
+        np.testing.assert_array_equal(go["prev"], ro["prev"], err_msg=what)
+        np.testing.assert_array_equal(go["curr"], ro["curr"], err_msg=what)
+    assert g_res["detection_rects"] == [] and g_res["tracker_rects"] == []
+
+
+@pytest.mark.parametrize("gridfast", [False, True])
+@pytest.mark.parametrize("W,H,bw,bh", [(640, 480, 32, 80), (960, 540, 64, 160)])
+def test_group_run_matches_oracle(oracle_mod, gridfast, W, H, bw, bh):
+    C, T = 3, 7
+    scenes = [synth.make_scene(40 + c, W, H, 120, nboxes=3, box_w=bw, box_h=bh, max_speed=3.0) for c in range(C)]
+    refs = [ORC.CameraTracker(cam_id=10 + c) for c in range(C)]
+    rngs = [np.random.default_rng(500 + c) for c in range(C)]
+    grays = [[sc.frame(t) for t in range(T)] for sc in scenes]
+    bgrs = [[_bgr(grays[c][t], 100 * c + t) for t in range(T)] for c in range(C)]
+    n_obj = n_matched = 0
+    with t2d.Group(W, H, [10 + c for c in range(C)]) as g:
+        for c in range(C):  # camera 1 ingests BGR, the others gray
+            g.push_frame(c, bgrs[c][0] if c == 1 else grays[c][0])
+        for t in range(T):
+            per_cam = [_camera_dets(scenes[c], t, rngs[c], tiny=(c == 0)) for c in range(C)]
+            g_dets = [[t2d.make_detection(b, np.zeros((0, 2), np.float32) if gridfast else f, head=e[0],
+                                          location=e[1], height=e[2]) for b, e, f in zip(*per_cam[c])]
+                      for c in range(C)]
+            g.launch(t, g_dets, gridfast=gridfast, seed=t)
+            if t + 1 < T:  # frame t+1 is uploaded while frame t runs
+                for c in range(C):
+                    g.push_frame(c, bgrs[c][t + 1] if c == 1 else grays[c][t + 1])
+            out = g.complete()
+            for c in range(C):
+                gray = oracle_mod.bgr2gray(bgrs[c][t]) if c == 1 else grays[c][t]
+                boxes, extra, feats = per_cam[c]
+                if gridfast:
+                    feats, _ = oracle_mod.gridfast_detect(gray, _rois(boxes, W, H), seed=t)
+                objs, _, r_res = refs[c].run(gray, [ORC.Rect(*b) for b in boxes], feats, t,
+                                             [(ORC.Rect(*e[0]), e[1], e[2]) for e in extra])
+                what = f"frame {t} camera {c}"
+                g_out, g_res = out[c]
+                for d, f in zip(g_out, feats):
+                    np.testing.assert_array_equal(t2d.points(d.features, d.num_features), f, err_msg=what)
+                valid = [d for d in g_out if d.valid]
+                assert len(valid) == len(objs), what
+                for d, o in zip(valid, objs):
+                    assert [d.boxes[i].tuple() for i in range(d.num_boxes)] == [b.tuple() for b in o.boxes], what
+                    assert d.num_sets == len(o.sets), what
+                    for s in range(d.num_sets):
+                        np.testing.assert_array_equal(t2d.points(d.sets[s], d.set_count[s]), o.sets[s], err_msg=what)
+                _check_result(g_res, r_res, what)
+                g_trk = g.trackers(c)
+                assert [(x.id, x.duration, x.num_boxes) for x in g_trk] == \
+                       [(x.id, x.duration, len(x.boxes)) for x in refs[c].active], what
+                n_obj += len(g_res["objects"])
+                n_matched += sum(1 for x in refs[c].active if x.duration > 1)
+    assert n_obj > 20 and n_matched > 5  # the sequence creates and continues trackers
+
+
+def test_group_window_errors():
+    """A detection whose box-width window the LK cannot run (2 px: CV_Assert(winSize > 2))
+    fails the frame only when it has >= 4 features (:744)."""
+    W, H = 160, 120
+    img = synth.texture(W, H, 3)
+    with t2d.Group(W, H, [0]) as g:
+        g.push_frame(0, img)
+        g.run(0, [[t2d.make_detection((10, 10, 30, 60), np.float32([[20, 20], [25, 30], [30, 40], [22, 50]]))]])
+        g.push_frame(0, img)
+        bad = t2d.make_detection((10, 10, 2, 30), np.float32([[11, 12], [11, 20], [11.5, 25], [11, 30]]))
+        with pytest.raises(t2d.T2dError):
+            g.run(1, [[bad]])
+        g.push_frame(0, img)
+        few = t2d.make_detection((10, 10, 2, 30), np.float32([[11, 12], [11, 20]]))
+        (dets, res), = g.run(2, [[few]])
+        assert dets[0].valid == 0 and res["objects"] == []

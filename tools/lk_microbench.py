@@ -58,8 +58,7 @@ def main():
         xs = np.array([o["iters"] for o in out if o["texture"] == texture], float)
         ys = np.array([o["us"] for o in out if o["texture"] == texture], float)
         slope, icpt = np.polyfit(xs, ys, 1)
-        print(json.dumps({"texture": texture, "us_per_iteration": round(slope, 3), "us_fixed": round(icpt, 2),
-                          "threads": os.environ.get("PSN_LK_THREADS", "auto")}))
+        print(json.dumps({"texture": texture, "us_per_iteration": round(slope, 3), "us_fixed": round(icpt, 2)}))
 
 
 if __name__ == "__main__":

@@ -15,7 +15,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))  # hiprt: the tests' HIP runtime helper
 
 from mcmtt_opticalflow_amd import _lib, lk, synth  # noqa: E402
 import hiprt  # noqa: E402
