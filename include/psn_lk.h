@@ -194,6 +194,14 @@ int psn_lk_timing_stats(psn_lk_ctx *ctx, int *n_push, double *push_ms, int *n_tr
 #define PSN_LK_VARIANT_FUSED_HELPERS 6
 int psn_lk_debug_set_variant(psn_lk_ctx *ctx, int key, int value);
 
+/* Window-sample counter (SURVEY 8(d)'s compute figure): while on, every box-
+ * window LK launch (lk_kernel_bx) adds, per point, sum over levels of
+ * w * h * (1 + iterations) to a device counter. _count_samples(ctx, 1) zeroes
+ * and enables it (device-wide sync), 0 disables; _read_samples syncs the
+ * device and returns the count. Test / benchmark instrumentation. */
+int psn_lk_debug_count_samples(psn_lk_ctx *ctx, int on);
+int psn_lk_debug_read_samples(psn_lk_ctx *ctx, unsigned long long *out);
+
 /* Diagnostic builds only (libpsn_lk_stamps.so, -DPSN_LK_STAMPS): record
  * shader-clock stamps of every LK workgroup's phases into a device buffer of
  * 64 u64 per workgroup. Returns PSN_LK_ERR_UNSUPPORTED in product builds. */

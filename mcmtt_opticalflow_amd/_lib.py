@@ -125,6 +125,9 @@ def load():
     L.psn_lk_timing_stats.argtypes = [vp, ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double)]
     L.psn_lk_debug_set_stamps.argtypes = [vp, vp]
+    L.psn_lk_debug_count_samples.argtypes = [vp, ip]
+    L.psn_lk_debug_read_samples.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.psn_lk_enable_timing.argtypes = [vp, ip, ip]
     L.psn_lk_set_ingest_overlap.argtypes = [vp, ip]
     L.psn_gridfast_default_params.argtypes = [ctypes.POINTER(GridFastParams)]
     L.psn_gridfast_default_params.restype = None

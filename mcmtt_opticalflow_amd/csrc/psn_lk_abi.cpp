@@ -71,6 +71,8 @@ struct psn_lk_ctx {
     int tiled_lds = 76 * 1024;
     int num_cus = 256;  // compute units of the device (launch shaping)
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
+    unsigned long long *d_samples = nullptr;  // psn_lk_debug_count_samples
+    bool count_samples = false;
     // GridFAST scratch (per-cell keypoints of one launch) and host-call outputs
     uint32_t *d_gf_kp = nullptr;
     int *d_gf_cnt = nullptr;
@@ -239,7 +241,7 @@ void psn_lk_destroy(psn_lk_ctx *c) {
         for (auto &se : v) (void)hipEventDestroy(se.second);
     for (uint8_t *p : c->d_stage)
         if (p) (void)hipFree(p);
-    for (void *p : {(void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
+    for (void *p : {(void *)c->d_samples, (void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status, (void *)c->d_gf_kp, (void *)c->d_gf_cnt, (void *)c->d_gf_xy,
                     (void *)c->d_gf_oc, (void *)c->d_gf_ot})
         if (p) (void)hipFree(p);
@@ -592,6 +594,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         a.status = d_status;
         a.err = d_err;
         a.stamps = c->d_stamps;
+        a.samples = c->count_samples ? c->d_samples : nullptr;
         a.counts = d_counts;
         int wgs = 0, lds = 0, maxpx = 0, nqd = 0, rows_ow = 0, lds_ow = 0, upt_bx = 0, lds_bx = 0;
         bool all_single = true, all_box = true;
@@ -815,6 +818,28 @@ int psn_lk_debug_set_variant(psn_lk_ctx *c, int key, int value) {
     case PSN_LK_VARIANT_FUSED_HELPERS: c->fused_helpers = std::max(0, value); return PSN_LK_OK;
     default: return PSN_LK_ERR_ARG;
     }
+}
+
+int psn_lk_debug_count_samples(psn_lk_ctx *c, int on) {
+    if (!c) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (on) {
+        if (!c->d_samples) HIPCHK(c, hipMalloc(&c->d_samples, sizeof(unsigned long long)));
+        HIPCHK(c, hipDeviceSynchronize());
+        HIPCHK(c, hipMemset(c->d_samples, 0, sizeof(unsigned long long)));
+    }
+    c->count_samples = on != 0;
+    return PSN_LK_OK;
+}
+
+int psn_lk_debug_read_samples(psn_lk_ctx *c, unsigned long long *out) {
+    if (!c || !out) return PSN_LK_ERR_ARG;
+    *out = 0;
+    if (!c->d_samples) return PSN_LK_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());  // launches of every stream the context was driven on
+    HIPCHK(c, hipMemcpy(out, c->d_samples, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return PSN_LK_OK;
 }
 
 int psn_lk_debug_set_stamps(psn_lk_ctx *c, void *d_stamps) {

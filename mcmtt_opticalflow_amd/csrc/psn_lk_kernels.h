@@ -71,6 +71,7 @@ struct LkLaunchArgs {
     uint8_t *status;
     float *err;              // may be null
     unsigned long long *stamps;  // diagnostic build only (PSN_LK_STAMPS): [wg][64] s_memtime
+    unsigned long long *samples; // optional: += sum over levels of w*h*(1 + iterations) per point
     int nq;
     int pad_;
     // optional per-query point counts on the device (<= num_pts, the grid

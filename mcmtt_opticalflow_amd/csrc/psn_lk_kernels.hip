@@ -2542,6 +2542,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
 
     unsigned IP[UPT][2], XP[UPT][2], YP[UPT][2];  // I, Ix, Iy as packed 16-bit pairs (pixels 0,1 and 2,3)
     int gmax = 0;              // max |Ix|, |Iy| of the thread's pixels
+    unsigned nwin = 0;         // window passes (A phase + iterations) over the levels: the sample count / (w*h)
 
     for (int level = maxL; level >= 0; level--) {
         const LevelDev I = ring_level_u(A.ring, Q.prev_slot, level);
@@ -2590,6 +2591,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
         // ---- A phase: Scharr + bilinear window values of the thread's units from
         // the I patch bytes; the 15 A chains (sum x class) as runs ----
         float A11, A12, A22;
+        nwin++;
         {
             const int sh = (ipx - 1) & 3;
             int T11[5] = {0, 0, 0, 0, 0}, T22[5] = {0, 0, 0, 0, 0}, T12[5] = {0, 0, 0, 0, 0};
@@ -2854,6 +2856,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
             }
             BX_MARK(3);  // iteration head (restage)
             BX_COUNT(10);
+            nwin++;
             const unsigned W0 = pack_w(w00, w01), W1 = pack_w(w10, w11);
             const int ox = inx - jr_x0, oy = iny - jr_y0, sj = ox & 3;
             const unsigned s0 = bx_sel(sj, 0), s1 = bx_sel(sj, 1), s2 = bx_sel(sj, 2), s3 = bx_sel(sj, 3);
@@ -3157,6 +3160,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
         A.next[2 * pi + 1] = NPy;
         A.status[pi] = (uint8_t)status;
         if (A.err) A.err[pi] = errv;
+        if (A.samples) atomicAdd(A.samples, (unsigned long long)nwin * (unsigned)(w * h));
     }
 }
 

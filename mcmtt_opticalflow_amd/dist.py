@@ -70,3 +70,75 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class ResultExchange:
+    """Per-frame hand-off of every camera's packed stTrack2DResult slot
+    (psn_t2d_pack_result) into Associator3D: each rank contributes its C
+    cameras' slots (rank r holds cameras r*C .. r*C+C-1), every rank receives
+    all of them in camera order (index == camID, PSNWhere_Associator3D.cpp:
+    1105-1116) in host memory.
+
+    backend "psn_comm": the library's RCCL communicator (psn_comm_init /
+    psn_comm_allgather over xGMI; the unique id travels over the
+    torch.distributed control group), pinned host -> device -> all-gather ->
+    pinned host on one HIP stream. backend "torch": the same exchange with
+    torch.distributed on CPU tensors (gloo), for the CPU tests."""
+
+    def __init__(self, world: int, rank: int, bytes_per_rank: int, device: int = 0, backend: str = "psn_comm"):
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+
+        self.world, self.rank, self.nbytes, self.backend = world, rank, bytes_per_rank, backend
+        self._comm = None
+        if backend == "torch":
+            self._recv = [torch.empty(bytes_per_rank, dtype=torch.uint8) for _ in range(world)]
+            return
+        from . import _lib
+
+        self._L = _lib.load()
+        uid = (ctypes.c_uint8 * _lib.COMM_UNIQUE_ID_BYTES)()
+        if rank == 0 and self._L.psn_comm_get_unique_id(uid) != 0:
+            raise RuntimeError("psn_comm_get_unique_id failed")
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)
+        ctypes.memmove(uid, box[0], len(box[0]))
+        comm = ctypes.c_void_p()
+        rc = self._L.psn_comm_init(world, rank, device, uid, ctypes.byref(comm))
+        if rc != 0:
+            raise RuntimeError(f"psn_comm_init failed ({rc})")
+        self._comm = comm
+        dev = torch.device("cuda", device)
+        self._stream = torch.cuda.Stream(dev)
+        self._send = torch.empty(bytes_per_rank, dtype=torch.uint8, device=dev)
+        self._recv_d = torch.empty(world * bytes_per_rank, dtype=torch.uint8, device=dev)
+        self._recv_h = torch.empty(world * bytes_per_rank, dtype=torch.uint8).pin_memory()
+
+    def allgather(self, send):
+        """send: uint8 numpy array of bytes_per_rank bytes (pinned for an async
+        upload) -> uint8 numpy array [world * bytes_per_rank] in camera order."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+
+        src = torch.from_numpy(np.ascontiguousarray(send).reshape(-1))
+        if self.backend == "torch":
+            dist.all_gather(self._recv, src.clone())
+            return torch.cat(self._recv).numpy()
+        with torch.cuda.stream(self._stream):
+            self._send.copy_(src, non_blocking=True)
+            rc = self._L.psn_comm_allgather(self._comm, self._send.data_ptr(), self._recv_d.data_ptr(), self.nbytes,
+                                            self._stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(f"psn_comm_allgather failed ({rc})")
+            self._recv_h.copy_(self._recv_d, non_blocking=True)
+        self._stream.synchronize()
+        return self._recv_h.numpy()
+
+    def close(self):
+        if self._comm is not None:
+            self._stream.synchronize()
+            self._L.psn_comm_destroy(self._comm)
+            self._comm = None

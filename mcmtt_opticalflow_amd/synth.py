@@ -104,3 +104,11 @@ def make_scene(cam: int, width: int, height: int, npts: int, nboxes: int | None 
     inner = np.stack([prng.uniform(4, box_w - 4, npts), prng.uniform(4, box_h - 4, npts)], axis=1)
     pts0 = (boxes0[pt_box] + inner).astype(np.float32)
     return CameraScene(cam, width, height, box_w, box_h, boxes0, vel, pts0, pt_box, bg, box_params)
+
+
+def to_bgr(gray: np.ndarray) -> np.ndarray:
+    """A deterministic colour frame whose channels are affine in the gray
+    rendering (the reference ingests BGR frames from imread, main.cpp:144, and
+    converts them with cvtColor(BGR2GRAY), PSNWhere_Tracker2D.cpp:257)."""
+    g = gray.astype(np.int32)
+    return np.stack([g, np.clip(g * 7 // 8 + 16, 0, 255), 255 - g], axis=-1).astype(np.uint8)

@@ -138,3 +138,72 @@ def test_result_slots_allgather_gloo_world2():
                 np.testing.assert_array_equal(a["prev"], b["prev"])
                 np.testing.assert_array_equal(a["curr"], b["curr"])
             assert g["detection_rects"] == r["detection_rects"] and g["tracker_rects"] == r["tracker_rects"]
+
+
+def _tracker_rank_worker(rank, world, port, C, q):
+    """The bench's Tracker2D-mode hand-off on CPU: rank r runs cameras r*C..r*C+C-1
+    (the oracle Tracker2D restatement stands in for the GPU group), packs each
+    camera's stTrack2DResult into its slot, and ResultExchange all-gathers the
+    slots (gloo here; psn_comm/RCCL on the GPUs)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle  # noqa: F401  (tests use the oracle as the checker / stand-in)
+        import tracker2d_oracle as T2
+
+        from mcmtt_opticalflow_amd import dist as pdist
+        from mcmtt_opticalflow_amd import synth
+        from mcmtt_opticalflow_amd import tracker2d as t2d
+
+        W, H, F = 160, 120, 3
+        cams = [rank * C + k for k in range(C)]
+        trackers = {cam: T2.CameraTracker(cam) for cam in cams}
+        scenes = {cam: synth.make_scene(cam, W, H, 24, nboxes=2, box_w=16, box_h=40, max_speed=2.0) for cam in cams}
+        slot = t2d.result_slot_bytes(8, 1)
+        ex = pdist.ResultExchange(world, rank, C * slot, backend="torch")
+        sent, got = {}, {}
+        for t in range(F):
+            send = np.zeros((C, slot), np.uint8)
+            for k, cam in enumerate(cams):
+                sc = scenes[cam]
+                pts = sc.points_at(t)
+                boxes = [T2.Rect(float(int(x)), float(int(y)), 16.0, 40.0) for x, y in sc.box_at(t)]
+                feats = [pts[sc.pt_box == i] for i in range(2)]
+                _, _, res = trackers[cam].run(sc.frame(t), boxes, feats, t)
+                t2d.pack_result(res, send[k])
+                sent[(cam, t)] = res
+            rows = ex.allgather(send).reshape(world * C, slot)
+            for cam in range(world * C):
+                got[(cam, t)] = t2d.unpack_result(rows[cam], 8, 1)
+        ex.close()
+        q.put((rank, sent, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tracker_results_exchange_gloo_world2():
+    world, C = 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tracker_rank_worker, args=(r, world, port, C, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sent = {}
+    for _, s, _ in out:
+        sent.update(s)
+    assert len(sent) == world * C * 3
+    for _, _, got in out:
+        for (cam, t), g in got.items():
+            r = sent[(cam, t)]
+            assert g["cam_id"] == cam and g["frame_idx"] == t  # row index == camera index
+            assert len(g["objects"]) == len(r["objects"])
+            for a, b in zip(g["objects"], r["objects"]):
+                assert (a["id"], a["box"], a["head"], a["score"]) == (b["id"], b["box"], b["head"], b["score"])
+                np.testing.assert_array_equal(a["prev"], b["prev"])
+                np.testing.assert_array_equal(a["curr"], b["curr"])
