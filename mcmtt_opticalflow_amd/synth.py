@@ -107,8 +107,11 @@ def make_scene(cam: int, width: int, height: int, npts: int, nboxes: int | None 
 
 
 def to_bgr(gray: np.ndarray) -> np.ndarray:
-    """A deterministic colour frame whose channels are affine in the gray
-    rendering (the reference ingests BGR frames from imread, main.cpp:144, and
-    converts them with cvtColor(BGR2GRAY), PSNWhere_Tracker2D.cpp:257)."""
+    """A deterministic colour frame around the gray rendering (the reference
+    ingests BGR frames from imread, main.cpp:144, and converts them with
+    cvtColor(BGR2GRAY), PSNWhere_Tracker2D.cpp:257): G = gray, B = gray + 24,
+    R = gray - 9 (clipped), chroma chosen so that the BT.601 luma of the colour
+    frame is the gray frame (0.114 * 24 - 0.299 * 9 ~ 0): the tracked images
+    keep the full contrast of the rendering."""
     g = gray.astype(np.int32)
-    return np.stack([g, np.clip(g * 7 // 8 + 16, 0, 255), 255 - g], axis=-1).astype(np.uint8)
+    return np.stack([np.clip(g + 24, 0, 255), g, np.clip(g - 9, 0, 255)], axis=-1).astype(np.uint8)

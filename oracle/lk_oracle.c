@@ -146,6 +146,79 @@ static void bsum_classify(const long long *t1, const long long *t2, int w, int h
         g_bsum_log[9] += worst;
         g_bsum_log[10] += common;
     }
+    {   /* [11] passes of a parity-scan evaluation of the float chains (binade of every step
+         * guessed from the exact prefix, restarted at the first failed guess), summed over
+         * b-sums that need one; [12] such b-sums; [13] max passes of one b-sum; [14] steps
+         * whose exact sum reaches 2^27 or more */
+        const int n8 = sse ? (w / 8) * 8 : 0;
+        int npass_max = 0, need = 0;
+        for (int cc = 0; cc < 10; cc++) {
+            const int s2 = cc / 5, c = cc % 5;
+            long long tv[16384];
+            int n = 0;
+            for (int y = 0; y < h; y++)
+                for (int x = 0; x < w; x++) {
+                    const int cx = x < n8 ? (x & 3) : 4;
+                    if (cx != c) continue;
+                    tv[n++] = (long long)(float)(s2 ? t2[y * w + x] : t1[y * w + x]);
+                }
+            /* true chain */
+            long long st = 0;
+            int inexact = 0, passes = 0, pos = 0;
+            long long S = 0;
+            while (pos < n) {
+                passes++;
+                long long P = S, s = S;
+                int k = pos, fail = -1;
+                for (; k < n; k++) {
+                    const long long xg = P + tv[k];
+                    long long ax = llabs(xg);
+                    long long u = 1;
+                    while (ax >= (1LL << 24) * u * 2 || (ax >= (1LL << 24) && u == 1 && ax >= (1LL << 24))) {
+                        if (ax < (1LL << 24) * 2 * u && u > 1) break;
+                        if (ax >= (1LL << 25) * u) u *= 2; else { if (ax >= (1LL << 24)) u = u < 2 ? 2 : u; break; }
+                    }
+                    /* u_true of the model state */
+                    const long long xt = s + tv[k];
+                    long long axt = llabs(xt), ut = 1;
+                    while (axt >= (1LL << 24) * ut) ut *= 2;
+                    if (ut > 1) ut /= 1;
+                    /* ulp: 1 below 2^24, 2 in [2^24, 2^25), ... */
+                    long long ug = 1;
+                    { long long a2x = llabs(xg); while (a2x >= (1LL << 24) * ug) ug *= 2; }
+                    if (ug != ut || (s % ut) != 0) { fail = k; break; }
+                    if (ax >= (1LL << 27)) g_bsum_log[14]++;
+                    /* round xt to a multiple of ut, ties to even */
+                    long long r = ((xt % ut) + ut) % ut, base = xt - r;
+                    if (2 * r > ut || (2 * r == ut && ((base / ut) & 1))) base += ut;
+                    if (ut > 1) inexact = 1;
+                    s = base;
+                    P += tv[k];
+                }
+                if (fail < 0) break;
+                {   /* the true step at the failure */
+                    const long long xt = s + tv[fail];
+                    long long axt = llabs(xt), ut = 1;
+                    while (axt >= (1LL << 24) * ut) ut *= 2;
+                    long long r = ((xt % ut) + ut) % ut, base = xt - r;
+                    if (2 * r > ut || (2 * r == ut && ((base / ut) & 1))) base += ut;
+                    S = base;
+                    pos = fail + 1;
+                    inexact = 1;
+                }
+            }
+            (void)st;
+            if (inexact) {
+                need = 1;
+                if (passes > npass_max) npass_max = passes;
+            }
+        }
+        if (need) {
+            g_bsum_log[11] += npass_max;
+            g_bsum_log[12]++;
+            if (npass_max > g_bsum_log[13]) g_bsum_log[13] = npass_max;
+        }
+    }
     g_bsum_log[0]++;
     g_bsum_log[1] += (a1 + a2) <= E;
     g_bsum_log[2] += (a1 <= E && a2 <= E);

@@ -126,6 +126,34 @@ def build_pyramid(img: np.ndarray, nlevels: int) -> list[np.ndarray]:
     return out
 
 
+def build_pyramid_packed(img: np.ndarray, nlevels: int) -> np.ndarray:
+    """The packed pyramid buffer lk_track_pyr takes (levels back to back)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    buf = np.empty(lib().oracle_level_offset(w, h, nlevels), np.uint8)
+    lib().oracle_build_pyramid(_p(img, _u8p), w, h, w, nlevels, _p(buf, _u8p))
+    return buf
+
+
+def lk_track_pyr(prev_pyr, next_pyr, w, h, prev_pts, win_size, max_level, criteria=(3, 30, 0.01), flags=0,
+                 min_eig_threshold=1e-4, accum=ACCUM_SSE2, nthreads=0, want_err=True):
+    """LK over prebuilt packed pyramids (the shared-pyramid schedule); max_level
+    is truncated here as buildOpticalFlowPyramid would."""
+    pts = np.ascontiguousarray(prev_pts, dtype=np.float32).reshape(-1, 2)
+    n = pts.shape[0]
+    nxt = np.zeros_like(pts)
+    st = np.zeros(n, np.uint8)
+    er = np.zeros(n, np.float32) if want_err else None
+    ml = effective_max_level(w, h, win_size[0], win_size[1], max_level)
+    rc = lib().oracle_lk_track_pyr(_p(prev_pyr, _u8p), _p(next_pyr, _u8p), w, h, _p(pts, _f32p), _p(nxt, _f32p),
+                                   _p(st, _u8p), _p(er, _f32p) if er is not None else None, n, win_size[0],
+                                   win_size[1], ml, criteria[0], criteria[1], criteria[2], flags, min_eig_threshold,
+                                   accum, nthreads)
+    if rc != 0:
+        raise ValueError(f"oracle_lk_track_pyr failed rc={rc}")
+    return nxt, st, er
+
+
 def calc_optical_flow_pyr_lk(prev_img, next_img, prev_pts, win_size=(21, 21), max_level=3,
                              criteria=(3, 30, 0.01), flags=0, min_eig_threshold=1e-4,
                              next_pts=None, accum=ACCUM_SSE2, nthreads=0, want_err=True):

@@ -131,11 +131,37 @@ def box_matching_cost(b1: Rect, b2: Rect) -> float:
     return (nom * nom) / (den * den)
 
 
+# Schedule knobs (bench.py's cpu_baseline legs): OpenMP threads of every LK call
+# (0: OMP_NUM_THREADS), and the shared-pyramid schedule -- each frame's
+# pyramid built once and reused by every call, as the MI355X path does --
+# instead of the reference's two pyramid builds per calcOpticalFlowPyrLK.
+NTHREADS = 0
+SHARED_PYRAMIDS = False
+_pyramids = {}
+
+
+def _pyramid(img):
+    key = id(img)
+    hit = _pyramids.get(key)
+    if hit is None or hit[0] is not img:
+        if len(_pyramids) > 64:
+            _pyramids.clear()
+        hit = (img, lk_oracle.build_pyramid_packed(img, 4))
+        _pyramids[key] = hit
+    return hit[1]
+
+
 def _lk(prev_img, next_img, pts, win):
     pts = np.asarray(pts, np.float32).reshape(-1, 2)
     if len(pts) == 0:
         return np.zeros((0, 2), np.float32), np.zeros(0, np.uint8)
-    nxt, st, _ = lk_oracle.calc_optical_flow_pyr_lk(prev_img, next_img, pts, win, 3)  # err requested (:781)
+    if SHARED_PYRAMIDS:
+        h, w = prev_img.shape
+        nxt, st, _ = lk_oracle.lk_track_pyr(_pyramid(prev_img), _pyramid(next_img), w, h, pts, win, 3,
+                                            nthreads=NTHREADS)
+        return nxt, st
+    nxt, st, _ = lk_oracle.calc_optical_flow_pyr_lk(prev_img, next_img, pts, win, 3,
+                                                    nthreads=NTHREADS)  # err requested (:781)
     return nxt, st
 
 

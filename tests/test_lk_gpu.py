@@ -355,3 +355,34 @@ def test_lk_box_kernel_windows(oracle_mod, kernel, win, flags):
     ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
     gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags, variants={"box": int(kernel == "box")})
     assert_same(gpu, ref, f"{kernel} win {win} flags {flags}")
+
+
+@pytest.mark.parametrize("win", [(21, 21), (64, 64), (64, 160)])
+def test_configs2_four_cameras_one_context(oracle_mod, win):
+    """BASELINE.json configs[2] on one GPU: 4 cameras x 1920x1080 x 512 points in
+    ONE context (camera k owns ring slots [kR, kR+R)), every camera's query in one
+    launch, with the OpenCV default window and the Tracker2D box windows
+    (64x64 backward, 64x160 forward); each camera against the oracle."""
+    W, H, R, C, N = 1920, 1080, 4, 4, 512
+    scenes = [synth.make_scene(20 + k, W, H, N) for k in range(C)]
+    with glk.LKContext(W, H, ring_slots=R * C, max_level_cap=3) as ctx:
+        for k, sc in enumerate(scenes):
+            ctx.push_frame(k * R + 1, synth.to_bgr(sc.frame(1)))  # BGR ingest
+            ctx.push_frame(k * R + 2, sc.frame(2))
+        pts = np.concatenate([sc.points_at(1) for sc in scenes])
+        qs = [glk.make_query(k * R + 1, k * R + 2, k * N, N, glk.make_params(win, 3)) for k in range(C)]
+        gn, gs, ge = ctx.track(qs, pts)
+    for k, sc in enumerate(scenes):
+        sl = slice(k * N, (k + 1) * N)
+        ref = oracle_ref(oracle_mod, sc.frame(1), sc.frame(2), pts[sl], win, 3)
+        assert_same((gn[sl], gs[sl], ge[sl]), ref, f"camera {k} win {win}")
+
+
+@pytest.mark.parametrize("win", [(21, 21), (64, 64)])
+def test_configs3_2048_points(oracle_mod, win):
+    """configs[3]'s per-GPU slice: 1 camera x 1920x1080 x 2048 points."""
+    sc, f0, f1 = scene_pair(31, 1920, 1080, 2048)
+    pts = sc.points_at(0)
+    ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3)
+    assert_same(gpu, ref, f"2048 points win {win}")
