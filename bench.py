@@ -95,19 +95,38 @@ def cpu_threads():
 # Tracker2D mode (default): configs[2] on every rank
 # ---------------------------------------------------------------------------
 
+import numpy as np  # noqa: E402
+
+
 class CameraFeed:
     """One camera's synthetic video (mcmtt_opticalflow_amd/synth.py): BGR frames
     in pinned host memory and, per frame, the detections (box, head box, 3D
     estimate) with their feature points."""
 
-    def __init__(self, cam, W, H, npts, nboxes, period, t2d, pinned):
+    def __init__(self, cam, W, H, npts, nboxes, period, t2d, pinned, jpeg=False):
         from mcmtt_opticalflow_amd import synth
 
         self.scene = synth.make_scene(cam, W, H, npts, nboxes=nboxes)
         self.period = period
-        self.frames = [pinned((H, W, 3)) for _ in range(period)]
-        for t in range(period):
-            self.frames[t][...] = synth.to_bgr(self.scene.frame(t))
+        self.jpeg = None
+        if jpeg:  # the camera's frames as baseline JPEG files (PIL/libjpeg-turbo, q90, 4:2:0, a restart per MCU row)
+            import io
+
+            from PIL import Image
+
+            self.jpeg = []
+            for t in range(period):
+                b = io.BytesIO()
+                Image.fromarray(synth.to_bgr(self.scene.frame(t))[..., ::-1]).save(
+                    b, "JPEG", quality=90, subsampling=2, restart_marker_rows=1)
+                buf = pinned((len(b.getvalue()),))
+                buf[:] = np.frombuffer(b.getvalue(), np.uint8)
+                self.jpeg.append(buf)
+            self.frames = None
+        else:
+            self.frames = [pinned((H, W, 3)) for _ in range(period)]
+            for t in range(period):
+                self.frames[t][...] = synth.to_bgr(self.scene.frame(t))
         self.boxes, self.feats = [], []
         for t in range(period):
             bx = [(float(int(x)), float(int(y)), float(self.scene.box_w), float(self.scene.box_h))
@@ -129,6 +148,13 @@ class CameraFeed:
 
     def frame(self, t):
         return self.frames[ping_pong(t, self.period)]
+
+    def push(self, group, k, t):
+        """Camera k's frame t into the group (async upload of BGR, or JPEG bytes decoded on the device)."""
+        if self.jpeg is not None:
+            group.push_frame_jpeg(k, self.jpeg[ping_pong(t, self.period)])
+        else:
+            group.push_frame(k, self.frame(t))
 
 
 def pinned_allocator():
@@ -223,7 +249,8 @@ def tracker_main(args):
     cams = [rank * C + k for k in range(C)]
     L = _lib.load()
     pinned = pinned_allocator()
-    feeds = [CameraFeed(c, W, H, args.points, args.boxes, args.period, t2d, pinned) for c in cams]
+    feeds = [CameraFeed(c, W, H, args.points, args.boxes, args.period, t2d, pinned, jpeg=args.ingest == "jpeg")
+             for c in cams]
     max_obj = 2 * args.boxes
     group = t2d.Group(W, H, cams, device=local_rank, max_objects=max_obj)
     slot_bytes = t2d.result_slot_bytes(max_obj, 1)
@@ -234,7 +261,7 @@ def tracker_main(args):
     def step(t, dets):
         group.launch(t, dets)
         for k, fd in enumerate(feeds):  # frame t+1 uploads while frame t runs
-            group.push_frame(k, fd.frame(t + 1))
+            fd.push(group, k, t + 1)
         group.complete_raw()
         for k in range(C):  # the hand-off slots (psn_t2d_pack_result) in host memory
             rc = T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
@@ -246,7 +273,7 @@ def tracker_main(args):
         return [fd.detections(t) for fd in feeds]
 
     for k, fd in enumerate(feeds):
-        group.push_frame(k, fd.frame(0))
+        fd.push(group, k, 0)
     t = 0
     for _ in range(args.warmup):
         step(t, all_dets(t))
@@ -310,6 +337,8 @@ def tracker_main(args):
                 "cameras": world * C, "cameras_per_gpu": C, "width": W, "height": H, "points_per_camera": args.points,
                 "detections_per_camera": args.boxes, "box": [64, 160], "levels": 4,
                 "win_backward": [64, 64], "win_forward": [64, 160],
+                "ingest": ("baseline JPEG files in host memory (q90 4:2:0, restart per MCU row), decoded on the device"
+                           if args.ingest == "jpeg" else "BGR frames in pinned host memory"),
                 "parallelism": f"{C} cameras-per-GPU x{world} (camera-sharded, RCCL all-gather of result slots)"},
             "roofline": {
                 "kernel": "lk_kernel_bx (every LK launch of a frame-set: forward + 3 chain steps)",
@@ -546,6 +575,8 @@ def main():
     ap.add_argument("--cameras", type=int, default=4, help="tracker mode: cameras per GPU (configs[2]: 4)")
     ap.add_argument("--points", type=int, default=512, help="tracker mode: feature points per camera")
     ap.add_argument("--boxes", type=int, default=8, help="tracker mode: detections per camera")
+    ap.add_argument("--ingest", choices=["bgr", "jpeg"], default="bgr",
+                    help="tracker mode: frames arrive as BGR arrays (default) or as JPEG files (device decode)")
     ap.add_argument("--kcameras", type=int, default=1, help="kernel mode: cameras per GPU")
     ap.add_argument("--kpoints", type=int, default=512, help="kernel mode: points per camera")
     ap.add_argument("--period", type=int, default=10)

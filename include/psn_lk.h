@@ -117,6 +117,12 @@ int psn_lk_push_frame_device(psn_lk_ctx *ctx, int slot, const uint8_t *dev, int 
  * slot has completed. Used to overlap frame t+1's upload with frame t's LK. */
 int psn_lk_push_frame_async(psn_lk_ctx *ctx, int slot, const uint8_t *host, int stride, int channels);
 
+/* The same from a compressed frame: a baseline JPEG (include/psn_jpeg.h) of
+ * the context's size is decoded on the device (cv::imread, main.cpp:144) into
+ * the slot's staging buffer and its pyramid built from the BGR result, all on
+ * the ingest stream; `jpeg` is copied before the call returns. */
+int psn_lk_push_frame_jpeg(psn_lk_ctx *ctx, int slot, const uint8_t *jpeg, size_t len);
+
 /* Ingest overlap modes (default OFF: builds run on the context stream).
  * STREAM: psn_lk_push_frame* builds the pyramid on the context's internal
  *   ingest stream, ordered only against earlier LK launches that read the same

@@ -241,6 +241,8 @@ const char *psn_t2d_group_last_error(psn_t2d_group *g);
 void *psn_t2d_group_lk_context(psn_t2d_group *g);
 int psn_t2d_group_push_frame(psn_t2d_group *g, int cam, const uint8_t *frame, int stride, int channels);
 int psn_t2d_group_push_frame_device(psn_t2d_group *g, int cam, const uint8_t *dev_frame, int stride, int channels);
+/* the camera's frame as a baseline JPEG file (decoded on the device, psn_lk_push_frame_jpeg) */
+int psn_t2d_group_push_frame_jpeg(psn_t2d_group *g, int cam, const uint8_t *jpeg, size_t len);
 int psn_t2d_group_launch(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *const *dets, const int *ndet,
                          int feature_mode, uint32_t seed);
 int psn_t2d_group_complete(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("PSN_LK_LIB") or os.path.join(_HERE, "lib", "libpsn_lk
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psn_lk.h")
 # every header whose entry points libpsn_lk.so exports
 HEADER_PATHS = [HEADER_PATH] + [os.path.join(os.path.dirname(_HERE), "include", h)
-                                for h in ("psn_sgsmooth.h", "psn_t2d_device.h")]
+                                for h in ("psn_sgsmooth.h", "psn_t2d_device.h", "psn_jpeg.h")]
 
 PSN_LK_OK = 0
 ERRORS = {
@@ -114,6 +114,16 @@ def load():
     L.psn_lk_push_frame.argtypes = [vp, ip, u8p, ip, ip]
     L.psn_lk_push_frame_device.argtypes = [vp, ip, vp, ip, ip]
     L.psn_lk_push_frame_async.argtypes = [vp, ip, u8p, ip, ip]
+    L.psn_lk_push_frame_jpeg.argtypes = [vp, ip, vp, ctypes.c_size_t]
+    L.psn_jpeg_info.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(ip), ctypes.POINTER(ip), ctypes.POINTER(ip)]
+    L.psn_jpeg_create.argtypes = [ip, ctypes.POINTER(vp)]
+    L.psn_jpeg_destroy.argtypes = [vp]
+    L.psn_jpeg_destroy.restype = None
+    L.psn_jpeg_last_error.argtypes = [vp]
+    L.psn_jpeg_last_error.restype = ctypes.c_char_p
+    L.psn_jpeg_set_stream.argtypes = [vp, vp]
+    L.psn_jpeg_decode_device.argtypes = [vp, vp, ctypes.c_size_t, vp, ip]
+    L.psn_jpeg_decode.argtypes = [vp, vp, ctypes.c_size_t, vp, ip]
     L.psn_lk_debug_set_variant.argtypes = [vp, ip, ip]
     L.psn_lk_track.argtypes = [vp, ctypes.POINTER(LkQuery), ip, fp, fp, u8p, fp]
     L.psn_lk_track_device.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp]

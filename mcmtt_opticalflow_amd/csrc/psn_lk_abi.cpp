@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "psn_lk.h"
+#include "psn_jpeg.h"
 #include "psn_gridfast.h"
 #include "psn_lk_kernels.h"
 
@@ -50,6 +51,7 @@ struct psn_lk_ctx {
     std::vector<uint8_t *> d_stage;
     std::vector<size_t> stage_cap;
     std::vector<int> used_slots;  // scratch of track_device_impl
+    psn_jpeg_ctx *jpeg = nullptr;  // psn_lk_push_frame_jpeg's decoder (on the ingest stream)
     uint8_t *d_pyr = nullptr;
     LevelDev *d_slots = nullptr;
     std::vector<LevelDev> h_slots;  // [nslots][kMaxLevels]
@@ -241,6 +243,7 @@ void psn_lk_destroy(psn_lk_ctx *c) {
         for (auto &se : v) (void)hipEventDestroy(se.second);
     for (uint8_t *p : c->d_stage)
         if (p) (void)hipFree(p);
+    if (c->jpeg) psn_jpeg_destroy(c->jpeg);
     for (void *p : {(void *)c->d_samples, (void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status, (void *)c->d_gf_kp, (void *)c->d_gf_cnt, (void *)c->d_gf_xy,
                     (void *)c->d_gf_oc, (void *)c->d_gf_ot})
@@ -416,6 +419,40 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
     return launch_build(c, a, s, slot);
 }
 
+// The slot's staging buffer, grown to `need` bytes (the old one may still be read by the ingest stream).
+static int ensure_stage(psn_lk_ctx *c, int slot, size_t need) {
+    if (c->stage_cap[slot] >= need) return PSN_LK_OK;
+    HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
+    if (c->d_stage[slot]) (void)hipFree(c->d_stage[slot]);
+    c->d_stage[slot] = nullptr;
+    c->stage_cap[slot] = 0;
+    HIPCHK(c, hipMalloc(&c->d_stage[slot], need));
+    c->stage_cap[slot] = need;
+    return PSN_LK_OK;
+}
+
+int psn_lk_push_frame_jpeg(psn_lk_ctx *c, int slot, const uint8_t *jpeg, size_t len) {
+    if (!c || !jpeg) return PSN_LK_ERR_ARG;
+    if (slot < 0 || slot >= c->user_slots) return set_err(c, PSN_LK_ERR_SLOT, "slot %d out of range", slot);
+    int w = 0, h = 0;
+    int rc = psn_jpeg_info(jpeg, len, &w, &h, nullptr);
+    if (rc) return set_err(c, rc, "JPEG headers");
+    if (w != c->width || h != c->height) return set_err(c, PSN_LK_ERR_ARG, "JPEG %dx%d, context %dx%d", w, h, c->width, c->height);
+    HIPCHK(c, hipSetDevice(c->device));
+    if ((rc = flush_pending(c))) return rc;
+    if (!c->jpeg) {
+        if ((rc = psn_jpeg_create(c->device, &c->jpeg))) return set_err(c, rc, "psn_jpeg_create");
+        psn_jpeg_set_stream(c->jpeg, c->ingest_stream);
+    }
+    const size_t row = (size_t)c->width * 3;
+    if ((rc = ensure_stage(c, slot, row * c->height))) return rc;
+    if ((rc = wait_slot_free(c, slot, c->ingest_stream))) return rc;
+    rc = psn_jpeg_decode_device(c->jpeg, jpeg, len, c->d_stage[slot], (int)row);
+    if (rc) return set_err(c, rc, "JPEG decode: %s", psn_jpeg_last_error(c->jpeg));
+    c->filled[slot] = 1;
+    return launch_build(c, build_args(c, slot, c->d_stage[slot], (int)row, 3), c->ingest_stream, slot);
+}
+
 int psn_lk_push_frame_async(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, int channels) {
     if (!c || !host || (channels != 1 && channels != 3) || stride < c->width * channels) return PSN_LK_ERR_ARG;
     if (slot < 0 || slot >= c->user_slots) return set_err(c, PSN_LK_ERR_SLOT, "slot %d out of range", slot);
@@ -423,14 +460,7 @@ int psn_lk_push_frame_async(psn_lk_ctx *c, int slot, const uint8_t *host, int st
     int rc = flush_pending(c);
     if (rc) return rc;
     const size_t row = (size_t)c->width * channels, need = row * c->height;
-    if (c->stage_cap[slot] < need) {
-        HIPCHK(c, hipStreamSynchronize(c->ingest_stream));  // the old buffer may still be read
-        if (c->d_stage[slot]) (void)hipFree(c->d_stage[slot]);
-        c->d_stage[slot] = nullptr;
-        c->stage_cap[slot] = 0;
-        HIPCHK(c, hipMalloc(&c->d_stage[slot], need));
-        c->stage_cap[slot] = need;
-    }
+    if ((rc = ensure_stage(c, slot, need))) return rc;
     hipStream_t s = c->ingest_stream;
     // the staging buffer is read only by this slot's previous build, which
     // precedes every read of the slot that wait_slot_free orders against

@@ -468,6 +468,11 @@ int psn_t2d_group_push_frame_device(psn_t2d_group *g, int cam, const uint8_t *de
     return gset(g, g->flow.StageFrame((size_t)cam, dev_frame, stride, channels, true));
 }
 
+int psn_t2d_group_push_frame_jpeg(psn_t2d_group *g, int cam, const uint8_t *jpeg, size_t len) {
+    if (!g || cam < 0 || (size_t)cam >= g->io.size() || !jpeg) return PSN_LK_ERR_ARG;
+    return gset(g, g->flow.StageFrameJpeg((size_t)cam, jpeg, len));
+}
+
 int psn_t2d_group_launch(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *const *dets, const int *ndet,
                          int feature_mode, uint32_t seed) {
     if (!g || !ndet || !dets || (feature_mode != PSN_T2D_FEATURES_GIVEN && feature_mode != PSN_T2D_FEATURES_GRIDFAST) ||

@@ -534,6 +534,16 @@ int Tracker2DFlow::StageFrame(size_t cam, const uint8_t *frame, int stride, int 
     return PSN_LK_OK;
 }
 
+int Tracker2DFlow::StageFrameJpeg(size_t cam, const uint8_t *jpeg, size_t len) {
+    if (!lk_ || cam >= cams_.size() || !jpeg) return PSN_LK_ERR_ARG;
+    Cam &c = cams_[cam];
+    const int rc = psn_lk_push_frame_jpeg(lk_, c.spare, jpeg, len);
+    if (rc) return fail(rc, "stage JPEG frame");
+    filled_[(size_t)c.spare] = 1;
+    c.staged = true;
+    return PSN_LK_OK;
+}
+
 int Tracker2DFlow::DetectFeatures(const std::vector<Detection> &dets, uint32_t seed,
                                   std::vector<std::vector<Point2f>> &features) {
     if (!lk_) return PSN_LK_ERR_ARG;

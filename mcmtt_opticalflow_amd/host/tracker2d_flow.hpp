@@ -90,6 +90,7 @@ class Tracker2DFlow {
     // the camera's staging slot; the next RunLaunch adopts it as frame t. May be
     // called for frame t+1 between RunLaunch(t) and RunComplete(t).
     int StageFrame(size_t cam, const uint8_t *frame, int stride, int channels, bool on_device);
+    int StageFrameJpeg(size_t cam, const uint8_t *jpeg, size_t len);  // a baseline JPEG, decoded on the device
     struct CamFrame {  // one camera's inputs and outputs of Run
         std::vector<Detection> dets;                      // height-validated detections of frame t
         std::vector<std::vector<Point2f>> features;       // in (given mode) / out (GridFAST mode)

@@ -119,6 +119,11 @@ class LKContext:
         self._check(self._L.psn_lk_push_frame_async(self._h, slot, img.ctypes.data, img.shape[1] * ch, ch),
                     "push_frame_async")
 
+    def push_frame_jpeg(self, slot: int, data: bytes):
+        """A baseline JPEG of the context's size, decoded on the device (psn_lk_push_frame_jpeg)."""
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        self._check(self._L.psn_lk_push_frame_jpeg(self._h, slot, buf, len(data)), "push_frame_jpeg")
+
     def push_frame_device(self, slot: int, dev_ptr: int, stride: int, channels: int = 1):
         self._check(self._L.psn_lk_push_frame_device(self._h, slot, dev_ptr, stride, channels), "push_frame_device")
 
@@ -274,3 +279,43 @@ class SGSmoother:
         if rc != 0:
             raise PsnLkError(rc, "psn_sg_lengths")
         return n
+
+
+class JpegDecoder:
+    """psn_jpeg (include/psn_jpeg.h): baseline JPEG -> BGR on the device."""
+
+    def __init__(self, device: int = 0):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        rc = self._L.psn_jpeg_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise PsnLkError(rc, "psn_jpeg_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.psn_jpeg_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @staticmethod
+    def info(data: bytes):
+        w, h, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        rc = _lib.load().psn_jpeg_info(data, len(data), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+        if rc != 0:
+            raise PsnLkError(rc, "psn_jpeg_info")
+        return w.value, h.value, c.value
+
+    def decode(self, data: bytes) -> np.ndarray:
+        """(H, W, 3) u8 BGR, as cv::imread(..., IMREAD_COLOR) returns it."""
+        w, h, _ = self.info(data)
+        out = np.empty((h, w, 3), np.uint8)
+        rc = self._L.psn_jpeg_decode(self._h, data, len(data), out.ctypes.data, 3 * w)
+        if rc != 0:
+            raise PsnLkError(rc, f"psn_jpeg_decode: {self._L.psn_jpeg_last_error(self._h).decode()}")
+        return out

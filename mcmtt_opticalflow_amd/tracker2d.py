@@ -165,6 +165,7 @@ def load():
     L.psn_t2d_group_lk_context.restype = vp
     L.psn_t2d_group_push_frame.argtypes = [vp, ip, vp, ip, ip]
     L.psn_t2d_group_push_frame_device.argtypes = [vp, ip, vp, ip, ip]
+    L.psn_t2d_group_push_frame_jpeg.argtypes = [vp, ip, vp, ctypes.c_size_t]
     L.psn_t2d_group_launch.argtypes = [vp, ctypes.c_uint, vp, vp, ip, ctypes.c_uint32]
     L.psn_t2d_group_complete.argtypes = [vp, vp, vp, ctypes.POINTER(Track2DResult)]
     L.psn_t2d_group_run.argtypes = [vp, ctypes.c_uint, vp, vp, ip, ctypes.c_uint32, ctypes.POINTER(Track2DResult)]
@@ -403,6 +404,12 @@ class Group:
         ch = 1 if img.ndim == 2 else img.shape[2]
         self._check(self._L.psn_t2d_group_push_frame(self._h, cam, img.ctypes.data, img.shape[1] * ch, ch),
                     "push_frame")
+
+    def push_frame_jpeg(self, cam: int, data):
+        """Camera `cam`'s frame t as a baseline JPEG file (bytes or a uint8 array), decoded on the device."""
+        self._check(self._L.psn_t2d_group_push_frame_jpeg(self._h, cam, data if isinstance(data, bytes) else
+                                                          ctypes.c_void_p(data.ctypes.data), len(data)),
+                    "push_frame_jpeg")
 
     def push_frame_device(self, cam: int, dev_ptr: int, stride: int, channels: int = 1):
         self._check(self._L.psn_t2d_group_push_frame_device(self._h, cam, ctypes.c_void_p(dev_ptr), stride, channels),

@@ -17,6 +17,7 @@
 #ifndef PSN_LK_ORACLE_H
 #define PSN_LK_ORACLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -88,6 +89,10 @@ int oracle_gridfast(const uint8_t *img, int w, int h, int stride, int rx, int ry
                     int nonmax, int max_total, int grid_rows, int grid_cols, float *out_xy, int *out_resp, int cap);
 uint32_t oracle_gridfast_key(uint32_t seed, uint32_t roi, uint32_t k);
 int oracle_gridfast_select(const float *cand_xy, int n, uint32_t seed, int roi, int cap, float *out_xy);
+
+/* ---- JPEG decode (oracle/jpeg_oracle.c): cv::imread's libjpeg baseline path ---- */
+int oracle_jpeg_info(const uint8_t *data, size_t n, int *w, int *h, int *ncomp);
+int oracle_jpeg_decode_bgr(const uint8_t *data, size_t n, uint8_t *out_bgr, int out_stride);
 
 #ifdef __cplusplus
 }

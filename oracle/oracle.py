@@ -70,6 +70,8 @@ def lib():
         L.oracle_gridfast_key.restype = ctypes.c_uint32
         L.oracle_gridfast_select.argtypes = [_f32p, ip, ctypes.c_uint32, ip, ip, _f32p]
         L.oracle_gridfast_select.restype = ip
+        L.oracle_jpeg_info.argtypes = [ctypes.c_void_p, ctypes.c_size_t, _i32p, _i32p, _i32p]
+        L.oracle_jpeg_decode_bgr.argtypes = [ctypes.c_void_p, ctypes.c_size_t, _u8p, ip]
         _lib = L
     return _lib
 
@@ -223,3 +225,18 @@ def gridfast_detect(img, rois, seed=0, threshold=10, nonmax=True, max_total=1000
         pts.append(gridfast_select(xy, seed, i, cap))
         tots.append(len(xy))
     return pts, np.asarray(tots, np.int32)
+
+
+# ---- JPEG decode (oracle/jpeg_oracle.c) ----
+
+def jpeg_decode_bgr(data: bytes) -> np.ndarray:
+    """cv::imread(..., IMREAD_COLOR) of a baseline JPEG: (H, W, 3) u8 BGR."""
+    buf = np.frombuffer(data, np.uint8)
+    w, h, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    if lib().oracle_jpeg_info(buf.ctypes.data, buf.size, ctypes.byref(w), ctypes.byref(h), ctypes.byref(nc)) != 0:
+        raise ValueError("not a baseline JPEG")
+    out = np.zeros((h.value, w.value, 3), np.uint8)
+    rc = lib().oracle_jpeg_decode_bgr(buf.ctypes.data, buf.size, _p(out, _u8p), 3 * w.value)
+    if rc != 0:
+        raise ValueError(f"oracle_jpeg_decode_bgr failed rc={rc}")
+    return out

@@ -11,7 +11,8 @@ import os
 import numpy as np
 import pytest
 
-GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
+                if not os.path.basename(p).startswith("jpeg_"))  # LK fixtures (JPEG: tests/test_jpeg.py)
 
 
 def load(path):
