@@ -32,6 +32,81 @@ void oracle_set_iter_log(int *buf) { g_iter_log = buf; }
  * (SSE2 lane or tail) sum|t1|+|t2| <= 2^24. */
 static long long *g_bsum_log = 0;
 void oracle_set_bsum_log(long long *buf) { g_bsum_log = buf; }
+static long long *g_chain_log = 0;
+static int g_chain_upt = 0;
+void oracle_set_chain_log(long long *buf, int upt) {
+    g_chain_log = buf;
+    g_chain_upt = upt;
+}
+/* lk_kernel_bx's chains of one b-sum evaluation through the binade-run model.
+ * buf: [0] evaluations, [1] of them on the exact fast path (every prefix of every
+ * chain an exact integer), [2] model != sequential sum (must stay 0), [3] sum over
+ * fallback evaluations of the longest serial walk (records + HARD terms) of a
+ * chain, [4] its maximum, [5] records, [6] HARD segments, [7] HARD terms, [8] max
+ * records of one chain in one wave, [9] max HARD segments of one chain in one
+ * wave, [10] fallback evaluations. */
+static void chain_classify(const long long *t1, const long long *t2, int w, int h, int sse) {
+    const int QW = (w + 3) / 4, U = h * QW, nqB = sse ? (w / 8) * 2 : 0;
+    const int need = (U + 255) / 256;
+    const int upt = g_chain_upt > 0 ? g_chain_upt : need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : 12;
+    float *f = (float *)malloc(sizeof(float) * (size_t)w * h);
+    int off[257];
+    int exact = 1, walk_max = 0, st[5];
+    long long recs = 0, hard = 0, hterms = 0;
+    int mrec = 0, mhard = 0, mismatch = 0;
+    float res[10];
+    for (int cc = 0; cc < 10; cc++) {
+        const long long *tv = cc < 5 ? t1 : t2;
+        const int c = cc % 5;
+        int n = 0;
+        for (int t = 0; t < 256; t++) {
+            off[t] = n;
+            for (int k = 0; k < upt; k++) {
+                const int un = t * upt + k;
+                if (un >= U) break;
+                const int y = un / QW, q = un % QW;
+                if (q < nqB) {
+                    if (c < 4) f[n++] = (float)tv[y * w + 4 * q + c];
+                } else if (c == 4) {
+                    for (int i = 0; i < 4; i++)
+                        if (4 * q + i < w) f[n++] = (float)tv[y * w + 4 * q + i];
+                }
+            }
+        }
+        off[256] = n;
+        long long P = 0;
+        for (int i = 0; i < n; i++) {
+            P += (long long)f[i];
+            if (llabs((long long)f[i]) > (1LL << 24) || llabs(P) > (1LL << 24)) exact = 0;
+        }
+        const float ser = oracle_chain_serial(f, n);
+        const float mod = oracle_chain_binade(f, n, off, 256, 64, st);
+        if (memcmp(&ser, &mod, 4) != 0) mismatch = 1;
+        res[cc] = ser;
+        recs += st[0];
+        hard += st[1];
+        hterms += st[2];
+        if (st[0] + st[2] > walk_max) walk_max = st[0] + st[2];
+        if (st[3] > mrec) mrec = st[3];
+        if (st[4] > mhard) mhard = st[4];
+    }
+    (void)res;
+    free(f);
+    g_chain_log[0]++;
+    g_chain_log[2] += mismatch;
+    if (exact) {
+        g_chain_log[1]++;
+        return;
+    }
+    g_chain_log[10]++;
+    g_chain_log[3] += walk_max;
+    if (walk_max > g_chain_log[4]) g_chain_log[4] = walk_max;
+    g_chain_log[5] += recs;
+    g_chain_log[6] += hard;
+    g_chain_log[7] += hterms;
+    if (mrec > g_chain_log[8]) g_chain_log[8] = mrec;
+    if (mhard > g_chain_log[9]) g_chain_log[9] = mhard;
+}
 static void bsum_classify(const long long *t1, const long long *t2, int w, int h, int sse) {
     const long long E = 1LL << 24;
     long long a1 = 0, a2 = 0, ca[10] = {0}, p[10] = {0};
@@ -527,7 +602,7 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
 
         float b1 = 0, b2 = 0;
         float qb0[4] = {0, 0, 0, 0}, qb1[4] = {0, 0, 0, 0};
-        if (g_bsum_log) {
+        if (g_bsum_log || g_chain_log) {
             long long *t1 = (long long *)malloc(sizeof(long long) * 2 * win_w * win_h), *t2 = t1 + win_w * win_h;
             for (int y = 0; y < win_h; y++)
                 for (int x = 0; x < win_w; x++) {
@@ -536,7 +611,8 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
                     t1[y * win_w + x] = (long long)d * dIw[2 * (y * win_w + x)];
                     t2[y * win_w + x] = (long long)d * dIw[2 * (y * win_w + x) + 1];
                 }
-            bsum_classify(t1, t2, win_w, win_h, sse);
+            if (g_bsum_log) bsum_classify(t1, t2, win_w, win_h, sse);
+            if (g_chain_log) chain_classify(t1, t2, win_w, win_h, sse);
             free(t1);
         }
         for (int y = 0; y < win_h; y++) {

@@ -78,6 +78,15 @@ int oracle_calc_optical_flow_pyr_lk(const uint8_t *prev_img, const uint8_t *next
  * buf[i*8 + level] (caller zeroes it). Single-threaded use only. */
 void oracle_set_iter_log(int *buf);
 void oracle_set_bsum_log(long long *buf);
+/* Analysis hook: every b-sum evaluation is cut into lk_kernel_bx's chains
+ * (units of 4 px, `upt` units per thread, 256 threads) and evaluated with the
+ * binade-run model (chain_model.c); buf[0..15] collects statistics (see
+ * chain_classify in lk_oracle.c). upt = 0 picks the kernel's UPT. */
+void oracle_set_chain_log(long long *buf, int upt);
+
+/* ---- Binade-run model of an ordered float chain (oracle/chain_model.c) ---- */
+float oracle_chain_serial(const float *f, int n);
+float oracle_chain_binade(const float *f, int n, const int *seg_off, int nseg, int wave, int *stats);
 
 /* ---- GridFAST feature extraction (oracle/gridfast_oracle.c) ----
  * FeatureDetector::create("GridFAST")->detect(gray, kps, mask(rect) = 255)
