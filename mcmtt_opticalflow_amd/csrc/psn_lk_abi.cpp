@@ -35,6 +35,12 @@ struct psn_lk_ctx {
     // the reads (one event per reading stream, all waited for by the next build
     // into the slot)
     hipStream_t ingest_stream = nullptr;
+    // psn_lk_push_frame_async: host uploads on their own stream (copy engine), so
+    // the uploads of several frames run back to back while their builds wait on
+    // the ingest stream (created at the highest priority: a build gates later
+    // LK launches and must not wait behind them for compute-unit slots)
+    hipStream_t copy_stream = nullptr;
+    std::vector<hipEvent_t> copy_done;
     int overlap = PSN_LK_OVERLAP_OFF;
     // PSN_LK_OVERLAP_FUSED: the last pushed build is deferred and run inside
     // the next LK launch that does not read its slot (tail workgroups)
@@ -180,7 +186,14 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (hipMemset(c->d_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     c->stream = c->own_stream;
-    if (hipStreamCreateWithFlags(&c->ingest_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+        if (hipStreamCreateWithPriority(&c->ingest_stream, hipStreamNonBlocking, greatest) != hipSuccess)
+            return fail(PSN_LK_ERR_HIP);
+        (void)least;
+    }
+    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     // slot layout: levels back to back, rows padded to 256 B (one HBM burst / 4 x 64-B lines)
     size_t slot_bytes = 0;
     std::vector<size_t> lv_off(c->nlevels);
@@ -223,8 +236,11 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     c->ready_rec.assign(c->nslots, 0);
     c->d_stage.assign(c->nslots, nullptr);
     c->stage_cap.assign(c->nslots, 0);
-    for (int i = 0; i < c->nslots; i++)
+    c->copy_done.assign(c->nslots, nullptr);
+    for (int i = 0; i < c->nslots; i++) {
         if (hipEventCreateWithFlags(&c->slot_ready[i], kSlotEventFlags) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+        if (hipEventCreateWithFlags(&c->copy_done[i], kSlotEventFlags) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    }
     *out = c;
     return PSN_LK_OK;
 }
@@ -236,7 +252,8 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->ingest_stream) (void)hipStreamSynchronize(c->ingest_stream);
-    for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready})
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready, &c->copy_done})
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
     for (auto &v : c->slot_free)
@@ -250,6 +267,7 @@ void psn_lk_destroy(psn_lk_ctx *c) {
         if (p) (void)hipFree(p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->ingest_stream) (void)hipStreamDestroy(c->ingest_stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     delete c;
 }
 
@@ -422,6 +440,7 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
 // The slot's staging buffer, grown to `need` bytes (the old one may still be read by the ingest stream).
 static int ensure_stage(psn_lk_ctx *c, int slot, size_t need) {
     if (c->stage_cap[slot] >= need) return PSN_LK_OK;
+    HIPCHK(c, hipStreamSynchronize(c->copy_stream));
     HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
     if (c->d_stage[slot]) (void)hipFree(c->d_stage[slot]);
     c->d_stage[slot] = nullptr;
@@ -461,12 +480,15 @@ int psn_lk_push_frame_async(psn_lk_ctx *c, int slot, const uint8_t *host, int st
     if (rc) return rc;
     const size_t row = (size_t)c->width * channels, need = row * c->height;
     if ((rc = ensure_stage(c, slot, need))) return rc;
-    hipStream_t s = c->ingest_stream;
-    // the staging buffer is read only by this slot's previous build, which
-    // precedes every read of the slot that wait_slot_free orders against
+    hipStream_t s = c->ingest_stream, cs = c->copy_stream;
+    // the staging buffer is read only by this slot's previous build (its ready
+    // event); the build waits for the upload and for every read of the slot
+    if (c->ready_rec[slot]) HIPCHK(c, hipStreamWaitEvent(cs, c->slot_ready[slot], 0));
+    HIPCHK(c, hipMemcpy2DAsync(c->d_stage[slot], row, host, stride, row, c->height, hipMemcpyHostToDevice, cs));
+    HIPCHK(c, hipEventRecord(c->copy_done[slot], cs));
     rc = wait_slot_free(c, slot, s);
     if (rc) return rc;
-    HIPCHK(c, hipMemcpy2DAsync(c->d_stage[slot], row, host, stride, row, c->height, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipStreamWaitEvent(s, c->copy_done[slot], 0));
     c->filled[slot] = 1;
     return launch_build(c, build_args(c, slot, c->d_stage[slot], (int)row, channels), s, slot);
 }

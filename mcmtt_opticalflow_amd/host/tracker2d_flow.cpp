@@ -122,13 +122,24 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
         cams_[c].spare = (int)c * kSlotsPerCam + kT2dInterval;
     }
     filled_.assign((size_t)nslots, 0);
-    hipStream_t fs = nullptr;
-    if (hipStreamCreateWithFlags(&fs, hipStreamNonBlocking) != hipSuccess) {
+    // stream priorities: the backward chains (three dependent launches per frame)
+    // are the frame's critical path; the forward calls fill the compute units they
+    // leave free instead of taking half of them (the device dispatches waiting
+    // workgroups of higher-priority queues first)
+    int least = 0, greatest = 0;
+    hipStream_t fs = nullptr, cs = nullptr;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&fs, hipStreamNonBlocking, least) != hipSuccess) {
         err_ = "forward stream";
         return PSN_LK_ERR_HIP;
     }
     fwd_stream_ = fs;
-    return PSN_LK_OK;
+    if (hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, greatest) != hipSuccess) {
+        err_ = "chain stream";
+        return PSN_LK_ERR_HIP;
+    }
+    chain_stream_ = cs;
+    return psn_lk_set_stream(lk_, cs);
 }
 
 // Device and pinned-host buffers of a device pass (grown on demand).
@@ -181,6 +192,10 @@ void Tracker2DFlow::Finalize() {
     }
     if (lk_) psn_lk_destroy(lk_);
     lk_ = nullptr;
+    if (chain_stream_) {
+        (void)hipStreamDestroy((hipStream_t)chain_stream_);
+        chain_stream_ = nullptr;
+    }
     cams_.clear();
 }
 
@@ -240,17 +255,23 @@ static int window_error(int win) {
 
 // Enqueue one device pass over the cameras in pc (everything asynchronous, one
 // host sync in PassComplete):
-//   1. the forward calls of every camera's trackers (:871-877): one counted LK
-//      launch on the forward stream, beside the chains;
-//   2. each detection's features at t: given (host points) or GridFAST on the
+//   1. each detection's features at t: given (host points) or GridFAST on the
 //      device straight into the chain inputs (:734-757), detections below the
 //      feature minimum (:744) gated to count 0 on the device;
-//   3. the backward chains (:763-811): per step ONE counted LK launch over every
+//   2. the backward chains (:763-811): per step ONE counted LK launch over every
 //      detection of every camera (capacity PSN_T2D_CHAIN_CAP points each; a
 //      stopped chain's count is 0, its workgroups exit at once) and one
 //      LocalSearchKLT + inlier-compaction kernel writing the next step's points
 //      and counts. A camera whose ring holds fewer past frames ends its chains
 //      earlier (per-chain last step); its queries in later steps are empty.
+//      The chain stream has the highest priority: its launches are the frame's
+//      critical path;
+//   3. the forward calls of every camera's trackers (:871-877): one counted LK
+//      launch on the (lowest-priority) forward stream, enqueued after the chain
+//      so that the chain's first kernels are dispatched before it.
+// The device-to-host copies of the results are enqueued by PassComplete: a copy
+// waiting for the pass would hold up, on the copy engine, the uploads of the
+// next frames (StageFrame) that the caller enqueues in between.
 int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed) {
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
     size_t K = 0, J = 0, F = 0;
@@ -275,7 +296,112 @@ int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t 
             rc = PSN_LK_ERR_HIP;
         }
     };
-    // 1. forward calls (every LK launch waits for the builds of the slots it reads)
+    win_bad_.assign(K, 0);
+    if (K) {  // 1-2. features and the backward chains
+        int max_steps = 0;
+        for (PassCam &p : pc) {
+            const int steps = StepsAvailable(p.cam);
+            for (size_t i = 0; i < p.dets->size(); i++) {
+                const size_t k = p.k0 + i;
+                const Rect box = (*p.dets)[i].box.scale(kFlowScale);
+                b.h_boxes[4 * k] = box.x;
+                b.h_boxes[4 * k + 1] = box.y;
+                b.h_boxes[4 * k + 2] = box.w;
+                b.h_boxes[4 * k + 3] = box.h;
+                win_bad_[k] = window_error((int)(box.w * kWinSizeRatio)) != 0;
+                b.h_last[k] = win_bad_[k] ? 0 : steps;
+                if (!win_bad_[k]) max_steps = std::max(max_steps, steps);
+            }
+        }
+        if (gridfast) {
+            psn_gridfast_params gp;
+            psn_gridfast_default_params(&gp);
+            gp.cap = (int)cap;  // kT2dMaxFeatures
+            std::vector<int> rois;
+            for (PassCam &p : pc) {
+                const size_t n = p.dets->size();
+                if (!n) continue;
+                rois.assign(4 * n, 0);
+                for (size_t i = 0; i < n; i++) {
+                    // cv::Rect((int)x, (int)y, (int)w, (int)h) of the cropped, scaled box
+                    const Rect r = (*p.dets)[i].box.scale(kFlowScale).cropWithSize(width_, height_);
+                    rois[4 * i] = (int)r.x;
+                    rois[4 * i + 1] = (int)r.y;
+                    rois[4 * i + 2] = (int)r.w;
+                    rois[4 * i + 3] = (int)r.h;
+                }
+                rc = psn_gridfast_detect_device(lk_, cams_[p.cam].ring[kT2dInterval - 1], rois.data(), (int)n, &gp, seed,
+                                                b.d_in + 2 * cap * p.k0, b.d_cnt + p.k0, b.d_tot + p.k0);
+                if (rc) return fail(rc, "psn_gridfast_detect_device");
+            }
+            chk(hipMemcpyAsync(b.h_rawcnt, b.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
+            chk(hipMemcpyAsync(b.h_in, b.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
+        } else {
+            for (PassCam &p : pc)
+                for (size_t i = 0; i < p.dets->size(); i++) {
+                    const size_t k = p.k0 + i;
+                    const std::vector<Point2f> &f = (*p.features)[i];
+                    const size_t n = std::min(f.size(), kT2dMaxFeatures);  // :753-757
+                    if (f.size() >= kT2dMinFeatures && win_bad_[k]) {
+                        err_ = "detection " + std::to_string(i) + " window";
+                        return window_error((int)(b.h_boxes[4 * k + 2] * kWinSizeRatio));
+                    }
+                    for (size_t j = 0; j < n; j++) {
+                        b.h_in[2 * (k * cap + j)] = f[j].x;
+                        b.h_in[2 * (k * cap + j) + 1] = f[j].y;
+                    }
+                    b.h_cnt[k] = (int)n;
+                }
+            // whole rows: a chain row's unused tail is never read (counts)
+            chk(hipMemcpyAsync(b.d_in, b.h_in, K * cap * 8, hipMemcpyHostToDevice, st), "chain inputs");
+            chk(hipMemcpyAsync(b.d_cnt, b.h_cnt, K * 4, hipMemcpyHostToDevice, st), "chain counts");
+        }
+        chk(hipMemcpyAsync(b.d_last, b.h_last, K * 4, hipMemcpyHostToDevice, st), "chain last steps");
+        if (!rc) rc = psn_t2d_gate_counts_device(b.d_cnt, (int)K, (int)kT2dMinFeatures, b.d_last, st);
+        chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
+        chk(hipMemsetAsync(b.d_nsteps, 0, b.nchains * (1 + S) * 4, st), "chain steps and set counts");
+        if (rc) return rc;
+        psn_t2d_chain_dev cd{};
+        cd.ndet = (int)K;
+        cd.cap = (int)cap;
+        cd.boxes = b.d_boxes;
+        cd.cnt = b.d_cnt;
+        cd.out_boxes = b.d_obox;
+        cd.sets = b.d_sets;
+        cd.set_cnt = b.d_setcnt;
+        cd.nsteps = b.d_nsteps;
+        cd.last_step = b.d_last;
+        for (int step = 1; step <= max_steps; step++) {
+            queries_.clear();
+            for (PassCam &p : pc) {
+                const Cam &cam = cams_[p.cam];
+                for (size_t i = 0; i < p.dets->size(); i++) {
+                    const size_t k = p.k0 + i;
+                    psn_lk_query q;
+                    psn_lk_default_params(&q.params);
+                    q.first_pt = (int)(k * cap);
+                    q.num_pts = (int)cap;
+                    if (step <= b.h_last[k]) {  // frame t-s+1 -> t-s with the square box-width window (:776-782)
+                        q.prev_slot = cam.ring[kT2dInterval - step];
+                        q.next_slot = cam.ring[kT2dInterval - 1 - step];
+                        q.params.win_w = q.params.win_h = (int)(b.h_boxes[4 * k + 2] * kWinSizeRatio);
+                    } else {  // the chain has ended (count 0 on the device): an empty query
+                        q.prev_slot = q.next_slot = cam.ring[kT2dInterval - 1];
+                    }
+                    queries_.push_back(q);
+                }
+            }
+            const float *in = step == 1 ? b.d_in : b.d_buf[step & 1];
+            rc = psn_lk_track_device_counted(lk_, queries_.data(), (int)K, b.d_cnt, in, b.d_out, b.d_status, b.d_err);
+            if (rc) return fail(rc, "psn_lk_track_device_counted");
+            cd.cur = in;
+            cd.nxt = b.d_out;
+            cd.next_in = b.d_buf[(step + 1) & 1];
+            rc = psn_t2d_chain_step_device(&cd, step, st);
+            if (rc) return fail(rc, "psn_t2d_chain_step_device");
+        }
+    }
+    // 3. forward calls (every LK launch waits for the builds of the slots it reads)
     if (J) {
         size_t o = K * cap;
         fwd_queries_.clear();
@@ -308,117 +434,7 @@ int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t 
                                              b.d_err);
         const int rs = psn_lk_set_stream(lk_, st);
         if (rc || rs) return fail(rc ? rc : rs, "forward launch");
-        if (F) {
-            chk(hipMemcpyAsync(b.h_fwd_out, b.d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
-            chk(hipMemcpyAsync(b.h_fwd_st, b.d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
-        }
     }
-    if (!K) return rc;
-    // 2. chain inputs: boxes, last steps, windows, features
-    win_bad_.assign(K, 0);
-    int max_steps = 0;
-    for (PassCam &p : pc) {
-        const int steps = StepsAvailable(p.cam);
-        for (size_t i = 0; i < p.dets->size(); i++) {
-            const size_t k = p.k0 + i;
-            const Rect box = (*p.dets)[i].box.scale(kFlowScale);
-            b.h_boxes[4 * k] = box.x;
-            b.h_boxes[4 * k + 1] = box.y;
-            b.h_boxes[4 * k + 2] = box.w;
-            b.h_boxes[4 * k + 3] = box.h;
-            win_bad_[k] = window_error((int)(box.w * kWinSizeRatio)) != 0;
-            b.h_last[k] = win_bad_[k] ? 0 : steps;
-            if (!win_bad_[k]) max_steps = std::max(max_steps, steps);
-        }
-    }
-    if (gridfast) {
-        psn_gridfast_params gp;
-        psn_gridfast_default_params(&gp);
-        gp.cap = (int)cap;  // kT2dMaxFeatures
-        std::vector<int> rois;
-        for (PassCam &p : pc) {
-            const size_t n = p.dets->size();
-            if (!n) continue;
-            rois.assign(4 * n, 0);
-            for (size_t i = 0; i < n; i++) {
-                // cv::Rect((int)x, (int)y, (int)w, (int)h) of the cropped, scaled box
-                const Rect r = (*p.dets)[i].box.scale(kFlowScale).cropWithSize(width_, height_);
-                rois[4 * i] = (int)r.x;
-                rois[4 * i + 1] = (int)r.y;
-                rois[4 * i + 2] = (int)r.w;
-                rois[4 * i + 3] = (int)r.h;
-            }
-            rc = psn_gridfast_detect_device(lk_, cams_[p.cam].ring[kT2dInterval - 1], rois.data(), (int)n, &gp, seed,
-                                            b.d_in + 2 * cap * p.k0, b.d_cnt + p.k0, b.d_tot + p.k0);
-            if (rc) return fail(rc, "psn_gridfast_detect_device");
-        }
-        chk(hipMemcpyAsync(b.h_rawcnt, b.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
-        chk(hipMemcpyAsync(b.h_in, b.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
-    } else {
-        for (PassCam &p : pc)
-            for (size_t i = 0; i < p.dets->size(); i++) {
-                const size_t k = p.k0 + i;
-                const std::vector<Point2f> &f = (*p.features)[i];
-                const size_t n = std::min(f.size(), kT2dMaxFeatures);  // :753-757
-                if (f.size() >= kT2dMinFeatures && win_bad_[k]) {
-                    err_ = "detection " + std::to_string(i) + " window";
-                    return window_error((int)(b.h_boxes[4 * k + 2] * kWinSizeRatio));
-                }
-                for (size_t j = 0; j < n; j++) {
-                    b.h_in[2 * (k * cap + j)] = f[j].x;
-                    b.h_in[2 * (k * cap + j) + 1] = f[j].y;
-                }
-                b.h_cnt[k] = (int)n;
-            }
-        // whole rows: a chain row's unused tail is never read (counts)
-        chk(hipMemcpyAsync(b.d_in, b.h_in, K * cap * 8, hipMemcpyHostToDevice, st), "chain inputs");
-        chk(hipMemcpyAsync(b.d_cnt, b.h_cnt, K * 4, hipMemcpyHostToDevice, st), "chain counts");
-    }
-    chk(hipMemcpyAsync(b.d_last, b.h_last, K * 4, hipMemcpyHostToDevice, st), "chain last steps");
-    if (!rc) rc = psn_t2d_gate_counts_device(b.d_cnt, (int)K, (int)kT2dMinFeatures, b.d_last, st);
-    chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
-    chk(hipMemsetAsync(b.d_nsteps, 0, b.nchains * (1 + S) * 4, st), "chain steps and set counts");
-    if (rc) return rc;
-    psn_t2d_chain_dev cd{};
-    cd.ndet = (int)K;
-    cd.cap = (int)cap;
-    cd.boxes = b.d_boxes;
-    cd.cnt = b.d_cnt;
-    cd.out_boxes = b.d_obox;
-    cd.sets = b.d_sets;
-    cd.set_cnt = b.d_setcnt;
-    cd.nsteps = b.d_nsteps;
-    cd.last_step = b.d_last;
-    for (int step = 1; step <= max_steps; step++) {
-        queries_.clear();
-        for (PassCam &p : pc) {
-            const Cam &cam = cams_[p.cam];
-            for (size_t i = 0; i < p.dets->size(); i++) {
-                const size_t k = p.k0 + i;
-                psn_lk_query q;
-                psn_lk_default_params(&q.params);
-                q.first_pt = (int)(k * cap);
-                q.num_pts = (int)cap;
-                if (step <= b.h_last[k]) {  // frame t-s+1 -> t-s with the square box-width window (:776-782)
-                    q.prev_slot = cam.ring[kT2dInterval - step];
-                    q.next_slot = cam.ring[kT2dInterval - 1 - step];
-                    q.params.win_w = q.params.win_h = (int)(b.h_boxes[4 * k + 2] * kWinSizeRatio);
-                } else {  // the chain has ended (count 0 on the device): an empty query
-                    q.prev_slot = q.next_slot = cam.ring[kT2dInterval - 1];
-                }
-                queries_.push_back(q);
-            }
-        }
-        const float *in = step == 1 ? b.d_in : b.d_buf[step & 1];
-        rc = psn_lk_track_device_counted(lk_, queries_.data(), (int)K, b.d_cnt, in, b.d_out, b.d_status, b.d_err);
-        if (rc) return fail(rc, "psn_lk_track_device_counted");
-        cd.cur = in;
-        cd.nxt = b.d_out;
-        cd.next_in = b.d_buf[(step + 1) & 1];
-        rc = psn_t2d_chain_step_device(&cd, step, st);
-        if (rc) return fail(rc, "psn_t2d_chain_step_device");
-    }
-    chk(hipMemcpyAsync(b.h_res, b.d_res, b.res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st), "chain results");
     return rc;
 }
 
@@ -432,11 +448,25 @@ int Tracker2DFlow::PassComplete(std::vector<PassCam> &pc, bool gridfast) {
             rc = PSN_LK_ERR_HIP;
         }
     };
-    chk(hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_)), "chain sync");
-    chk(hipStreamSynchronize((hipStream_t)fwd_stream_), "forward sync");
-    if (rc) return rc;
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
     DeviceBuffers *bp = dev_;
+    size_t K = 0, F = 0;
+    for (PassCam &p : pc) {
+        K += p.dets->size();
+        if (p.fwd)
+            for (const Job &jb : *p.fwd) F += jb.in->size();
+    }
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    if (K && bp)
+        chk(hipMemcpyAsync(bp->h_res, bp->d_res, bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
+            "chain results");
+    if (F && bp) {
+        chk(hipMemcpyAsync(bp->h_fwd_out, bp->d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
+        chk(hipMemcpyAsync(bp->h_fwd_st, bp->d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
+    }
+    chk(hipStreamSynchronize(st), "chain sync");
+    chk(hipStreamSynchronize(fs), "forward sync");
+    if (rc) return rc;
     for (PassCam &p : pc) {
         const size_t n = p.dets->size();
         if (gridfast) {

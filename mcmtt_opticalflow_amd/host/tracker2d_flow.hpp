@@ -168,7 +168,8 @@ class Tracker2DFlow {
                    std::vector<DetectedObject> &out, std::vector<Job> *fwd, bool gridfast, uint32_t seed);
 
     psn_lk_ctx *lk_ = nullptr;
-    void *fwd_stream_ = nullptr;  // hipStream_t of the forward launch, beside the chain's launches
+    void *fwd_stream_ = nullptr;    // hipStream_t of the forward launch, beside the chain's launches (lowest priority)
+    void *chain_stream_ = nullptr;  // the LK context's stream: the backward chains, the critical path (highest priority)
     std::vector<psn_lk_query> fwd_queries_;
     std::vector<Cam> cams_;
     int width_ = 0, height_ = 0;

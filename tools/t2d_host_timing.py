@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Host-side phase times of bench.py's default Tracker2D step (diagnostic):
+how long group.launch, the frame pushes, complete_raw and the result packing
+take on the host, per frame-set. Usage: python tools/t2d_host_timing.py [steps]"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from mcmtt_opticalflow_amd import tracker2d as t2d  # noqa: E402
+
+
+def main():
+    import torch
+
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    torch.cuda.set_device(0)
+    W, H, C, P, B, period = 1920, 1080, 4, 512, 8, 10
+    pinned = bench.pinned_allocator()
+    feeds = [bench.CameraFeed(c, W, H, P, B, period, t2d, pinned) for c in range(C)]
+    group = t2d.Group(W, H, list(range(C)), device=0, max_objects=2 * B)
+    slot_bytes = t2d.result_slot_bytes(2 * B, 1)
+    send = pinned((C, slot_bytes))
+    T = t2d.load()
+    for k, fd in enumerate(feeds):
+        fd.push(group, k, 0)
+    rows = []
+    for t in range(steps + 5):
+        dets = [fd.detections(t) for fd in feeds]
+        a = time.perf_counter()
+        group.launch(t, dets)
+        b = time.perf_counter()
+        for k, fd in enumerate(feeds):
+            fd.push(group, k, t + 1)
+        c = time.perf_counter()
+        group.complete_raw()
+        d = time.perf_counter()
+        for k in range(C):
+            T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
+        e = time.perf_counter()
+        if t >= 5:
+            rows.append((b - a, c - b, d - c, e - d, e - a))
+    r = np.array(rows) * 1e3
+    names = ["launch", "push x4", "complete (sync + host update)", "pack", "total"]
+    for i, n in enumerate(names):
+        print(f"{n:32s} mean {r[:, i].mean():7.3f} ms  p50 {np.median(r[:, i]):7.3f}  max {r[:, i].max():7.3f}")
+    group.close()
+
+
+if __name__ == "__main__":
+    main()
