@@ -81,6 +81,33 @@ static void chain_classify(const long long *t1, const long long *t2, int w, int 
         }
         const float ser = oracle_chain_serial(f, n);
         const float mod = oracle_chain_binade(f, n, off, 256, 64, st);
+        {   /* [11] terms after the chain's first inexact step, [12] of them the steps whose
+             * accumulator stays below 2^24 - 2^16 in magnitude (exact integer additions),
+             * [13] the same in blocks of 16 terms whose every step qualifies */
+            float acc = 0.f;
+            int first = -1;
+            long long P = 0;
+            for (int i = 0; i < n; i++) {
+                P += (long long)f[i];
+                if (first < 0 && (llabs(P) > (1LL << 24) || llabs((long long)f[i]) > (1LL << 24))) first = i;
+            }
+            if (first >= 0) {
+                int blk_ok = 1, blk_n = 0;
+                for (int i = 0; i < n; i++) {
+                    acc = acc + f[i];
+                    if (i < first) continue;
+                    const int ok = fabsf(acc) < (float)((1 << 24) - (1 << 16));
+                    g_chain_log[11]++;
+                    g_chain_log[12] += ok;
+                    blk_ok &= ok;
+                    if (++blk_n == 16) {
+                        if (blk_ok) g_chain_log[13] += 16;
+                        blk_ok = 1;
+                        blk_n = 0;
+                    }
+                }
+            }
+        }
         if (memcmp(&ser, &mod, 4) != 0) mismatch = 1;
         res[cc] = ser;
         recs += st[0];

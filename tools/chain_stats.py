@@ -28,7 +28,8 @@ import tracker2d_oracle as T2  # noqa: E402
 from mcmtt_opticalflow_amd import synth  # noqa: E402
 
 KEYS = ["evals", "fast_path", "mismatch", "walk_sum", "walk_max", "records", "hard_segs", "hard_terms",
-        "max_wave_records", "max_wave_hard", "fallback_evals"]
+        "max_wave_records", "max_wave_hard", "fallback_evals",
+        "suffix_terms", "suffix_exact_steps", "suffix_exact_in_blocks16"]
 
 
 def main():
