@@ -2320,68 +2320,58 @@ __device__ __forceinline__ int wave_min_scan(int v) {
     return v;
 }
 
-// Publish this wave's part of NC chains (per-lane run total T, maximum prefix M
-// >= 0 and minimum prefix m <= 0, prefixes relative to the run start): per
-// half wave (lanes 0-31, then the whole wave) the chain total and the extreme
-// prefixes, relative to the wave's start. int32 is enough: a run holds <= 48
-// terms < 2^25, and any wrap happens only past a prefix that already fails the
-// 2^24 bound.
+// Exactness of NC chains in three steps around two barriers (per-lane run total
+// T, maximum prefix M >= 0 and minimum prefix m <= 0, prefixes relative to the
+// run start). bx_publish: one wave scan per chain turns T into the exclusive
+// prefix inside the wave, and lanes 31 / 63 record the half-wave / wave totals
+// (rec[8c + 4 + wave], rec[8c + wave]). bx_check (after the first barrier):
+// each lane adds the earlier waves' totals and tests its own extreme prefixes
+// against 2^24; the wave's first failing half wave goes to rec[120 + wave]
+// (8: none). bx_eval (after the second barrier): the verdict, chain c's total
+// and its exact prefix before the first failing half wave, on lane c. int32 is
+// enough: every value up to the first failing prefix is exact, and what a wrap
+// past it produces is never read (only the FIRST failure counts).
+constexpr int kBxHalfRec = 120;
 template <int NC>
-__device__ __forceinline__ void bx_publish(const int (&T)[NC], const int (&M)[NC], const int (&m)[NC], bool bad,
-                                           int *rec, bool no_tail) {
-    const int lane = threadIdx.x & 63;
-    int *xw = rec + (threadIdx.x >> 6) * kBxRecInts;
+__device__ __forceinline__ void bx_publish(int (&T)[NC], int *rec, bool no_tail) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
         if (no_tail && c % 5 == 4) {  // empty tail chain (uniform)
-            if (lane == 31 || lane == 63) *(int4 *)(xw + 8 * c + (lane == 63 ? 4 : 0)) = make_int4(0, 0, 0, 0);
+            if (lane == 31 || lane == 63) rec[8 * c + wv + (lane == 31 ? 4 : 0)] = 0;
             continue;
         }
         const int incl = wave_scan(T[c]);
-        const int ex = incl - T[c];
-        const int hs = wave_max_scan(ex + M[c]);
-        const int ls = wave_min_scan(ex + m[c]);
-        // lanes 31 and 63 hold the half-wave and wave values: they write them directly
-        if (lane == 31 || lane == 63) *(int4 *)(xw + 8 * c + (lane == 63 ? 4 : 0)) = make_int4(incl, hs, ls, 0);
+        if (lane == 31 || lane == 63) rec[8 * c + wv + (lane == 31 ? 4 : 0)] = incl;
+        T[c] = incl - T[c];
     }
-    const bool anybad = __ballot(bad) != 0ull;
-    if (lane == 0) xw[8 * 15] = anybad ? 1 : 0;
 }
-// After the barrier: lane c < NC checks chain c over the 8 half waves in chain
-// order. Returns the wave-uniform verdict "every prefix of every chain is an
-// exact integer"; total = chain c's sum; h0 = the first half wave (0-7) where
-// any chain's prefix leaves the exact range (8: none); base0 = chain c's exact
-// prefix before half wave h0.
+template <int NC>
+__device__ __forceinline__ void bx_check(const int (&E)[NC], const int (&M)[NC], const int (&m)[NC], bool bad, int *rec,
+                                         bool no_tail) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    bool fail = bad;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        if (no_tail && c % 5 == 4) continue;
+        const int4 t = *(const int4 *)(rec + 8 * c);
+        const int p = (wv > 0 ? t.x : 0) + (wv > 1 ? t.y : 0) + (wv > 2 ? t.z : 0) + E[c];
+        fail |= (p + M[c] > kExact) | (p + m[c] < -kExact);
+    }
+    const unsigned long long f = __ballot(fail);
+    if (lane == 0) rec[kBxHalfRec + wv] = f == 0ull ? 8 : 2 * wv + ((unsigned)f == 0u ? 1 : 0);
+}
 template <int NC>
 __device__ __forceinline__ bool bx_eval(const int *rec, int &total, int &h0, int &base0) {
     const int lane = threadIdx.x & 63;
     const int c = lane < NC ? lane : 0;
-    long long base = 0;
-    int fh = 8;
-    int t31[4], t63[4];
-#pragma unroll
-    for (int wv = 0; wv < 4; wv++) {
-        const int *xw = rec + wv * kBxRecInts + 8 * c;
-        const int4 a = *(const int4 *)xw, b = *(const int4 *)(xw + 4);
-        const bool bad = rec[wv * kBxRecInts + 8 * 15] != 0;
-        t31[wv] = a.x;
-        t63[wv] = b.x;
-        const bool ok0 = (base + a.y <= (long long)kExact) & (base + a.z >= -(long long)kExact) & !bad;
-        const bool ok1 = (base + b.y <= (long long)kExact) & (base + b.z >= -(long long)kExact) & !bad;
-        const int f = !ok0 ? 2 * wv : !ok1 ? 2 * wv + 1 : 8;
-        fh = min(fh, f);
-        base += b.x;
-    }
-    total = (int)base;
-    if (lane >= NC) fh = 8;
-    h0 = __builtin_amdgcn_readlane(wave_min_scan(fh), 63);
-    long long b0 = 0;
-#pragma unroll
-    for (int wv = 0; wv < 4; wv++) {
-        if (2 * wv + 1 < h0) b0 += t63[wv];
-        else if (2 * wv + 1 == h0) b0 += t31[wv];
-    }
-    base0 = (int)b0;
+    const int4 hh = *(const int4 *)(rec + kBxHalfRec);
+    h0 = min(min(hh.x, hh.y), min(hh.z, hh.w));
+    const int4 t = *(const int4 *)(rec + 8 * c), s = *(const int4 *)(rec + 8 * c + 4);
+    total = t.x + t.y + t.z + t.w;
+    const int hw = h0 >> 1;
+    base0 = (hw > 0 ? t.x : 0) + (hw > 1 ? t.y : 0) + (hw > 2 ? t.z : 0) + (hw > 3 ? t.w : 0);
+    if (h0 & 1) base0 += hw == 0 ? s.x : hw == 1 ? s.y : hw == 2 ? s.z : s.w;
     return h0 == 8;
 }
 __device__ __forceinline__ float rl_f(int v, int lane) { return (float)__builtin_amdgcn_readlane(v, lane); }
@@ -2706,7 +2696,9 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
             BX_MARK(1);  // A window values + runs
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
-            bx_publish<15>(T, M, m, false, rec, tA == 0);
+            bx_publish<15>(T, rec, tA == 0);
+            __syncthreads();
+            bx_check<15>(T, M, m, false, rec, tA == 0);
             __syncthreads();
             int tot, h0, base0;
             const bool exact = bx_eval<15>(rec, tot, h0, base0);
@@ -2916,7 +2908,10 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
             BX_MARK(4);  // b main pass
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
-            bx_publish<10>(T, M, m, bad, rec, tB == 0);
+            bx_publish<10>(T, rec, tB == 0);
+            BX_MARK(9);  // b publish (this wave's scans and records)
+            __syncthreads();
+            bx_check<10>(T, M, m, bad, rec, tB == 0);
             __syncthreads();
             int tot, h0, base0;
             float b1, b2;

@@ -44,7 +44,8 @@ def main():
         s = st.to_array((npts, 64), np.uint64).astype(np.int64)
     tot = s[:, 15]
     slow = int(np.argmax(tot))
-    ph = s[:, :9]
+    ph = s[:, :9].copy()
+    ph[:, 5] += s[:, 9]  # slot 9 splits b_publish_eval: publish (9) + barrier and eval (5)
     out = {"window": [w, h], "points": npts, "wg_cycles_mean": float(tot.mean()), "wg_cycles_max": int(tot.max()),
            "iterations_mean": float(s[:, 10].mean()), "iterations_max": int(s[:, 10].max()),
            "serial_b_fraction": round(float(s[:, 11].sum() / max(s[:, 10].sum(), 1)), 3),
@@ -57,6 +58,7 @@ def main():
                                                 "barrier_wait": round(float(s[:, 13].sum() / nt), 1)}
     it = max(s[:, 10].sum(), 1)
     out["per_iteration"] = {k: round(float(ph[:, i].sum() / it), 1) for i, k in enumerate(PHASES) if i >= 3}
+    out["per_iteration"]["b_publish_only"] = round(float(s[:, 9].sum() / it), 1)  # inside b_publish_eval
     print(json.dumps(out, indent=1))
 
 
