@@ -2941,31 +2941,68 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     nsse = (ub / QW) * nqB + min(ub % QW, nqB) - sa;
                     ntail = (ub / QW) * tB + min(max(4 * (ub % QW) - n8, 0), tB) - ta;
                 };
+                // one unit's b products into the tile's chain regions
+                auto tile_unit = [&](int yk, int qk, bool uv, const unsigned (&ip)[2], const unsigned (&xp)[2],
+                                     const unsigned (&yp)[2], float *buf, int S, int P, int sa, int ta) {
+                    if (!uv) return;
+                    int d[4];
+                    bx_diffs(JR32 + (oy + yk) * JRP4 + (ox >> 2) + qk, JRP4, W0, W1, s0, s1, s2, s3, ip, d);
+                    const bool su = qk < nqB;
+                    const int base = su ? yk * nqB + qk - sa : 4 * S + yk * tB + 4 * qk - n8 - ta;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        // pixels past the window width write a dummy slot past the buffers (branch-free)
+                        const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                        const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                        const bool on = 4 * qk + i < w;
+                        float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 4 * PC;
+                        d1[0] = (float)__mul24(d[i], gx);
+                        d1[on ? P : 1] = (float)__mul24(d[i], gy);
+                    }
+                };
+                // Half-wave tiles (HW = 1): the whole wave writes one tile, K1 = UPT/2
+                // unit slots per lane. v_permlane32_swap of unit registers k and K1 + k
+                // gives, as its first result, lower lane l's unit k on lane l and its
+                // unit K1 + k on lane l + 32 (a lower-half tile), as its second, upper
+                // lane l + 32's unit K1 + k there and its unit k on lane l (an upper-half
+                // tile): both halves run one instruction stream.
+                constexpr int K1 = UPT / 2;
+                const bool split = HW == 1 && (UPT & 1) == 0;
+                auto swp = [](unsigned a, unsigned b, bool first) {
+                    auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+                    return first ? r[0] : r[1];
+                };
                 auto write_tile = [&](int g, float *buf) {
-                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
                     int sa, ta, nsse, ntail;
+                    if (split) {
+                        if ((tid >> 6) != (g >> 1)) return;
+                        tile_geo(g, sa, ta, nsse, ntail);
+                        const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                        const bool lower = (g & 1) == 0, own = ((tid >> 5) & 1) == (g & 1);
+                        const int ub = (own ? tid : tid ^ 32) * UPT + (lower == own ? 0 : K1);
+                        int yk = ub / QW, qk = ub - yk * QW;
+                        asm volatile("" : "+v"(yk), "+v"(qk));
+#pragma unroll
+                        for (int k = 0; k < K1; k++) {
+                            const unsigned ip[2] = {swp(IP[k][0], IP[K1 + k][0], lower), swp(IP[k][1], IP[K1 + k][1], lower)};
+                            const unsigned xp[2] = {swp(XP[k][0], XP[K1 + k][0], lower), swp(XP[k][1], XP[K1 + k][1], lower)};
+                            const unsigned yp[2] = {swp(YP[k][0], YP[K1 + k][0], lower), swp(YP[k][1], YP[K1 + k][1], lower)};
+                            tile_unit(yk, qk, ub + k < U, ip, xp, yp, buf, S, P, sa, ta);
+                            if (++qk == QW) {
+                                qk = 0;
+                                yk++;
+                            }
+                        }
+                        return;
+                    }
+                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
                     tile_geo(g, sa, ta, nsse, ntail);
                     const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                     int yk = y0, qk = q0;
                     asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
                     for (int k = 0; k < UPT; k++) {
-                        if (u0 + k < U) {
-                            int d[4];
-                            bx_diffs(JR32 + (oy + yk) * JRP4 + (ox >> 2) + qk, JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
-                            const bool su = qk < nqB;
-                            const int base = su ? yk * nqB + qk - sa : 4 * S + yk * tB + 4 * qk - n8 - ta;
-#pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                // pixels past the window width write a dummy slot past the buffers (branch-free)
-                                const int gx = (i & 1) ? hi16(XP[k][i >> 1]) : lo16(XP[k][i >> 1]);
-                                const int gy = (i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]);
-                                const bool on = 4 * qk + i < w;
-                                float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 4 * PC;
-                                d1[0] = (float)__mul24(d[i], gx);
-                                d1[on ? P : 1] = (float)__mul24(d[i], gy);
-                            }
-                        }
+                        tile_unit(yk, qk, u0 + k < U, IP[k], XP[k], YP[k], buf, S, P, sa, ta);
                         if (++qk == QW) {
                             qk = 0;
                             yk++;
