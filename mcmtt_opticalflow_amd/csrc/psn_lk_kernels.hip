@@ -2731,33 +2731,62 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     nsse = (ub / QW) * nqA + min(ub % QW, nqA) - sa;
                     ntail = (ub / QW) * tA + min(max(4 * (ub % QW) - nA4, 0), tA) - ta;
                 };
+                auto unitA = [&](int yk, int qk, bool uv, unsigned x0, unsigned x1, unsigned y0_, unsigned y1_, float *buf,
+                                 int S, int P, int sa, int ta) {
+                    if (!uv) return;
+                    unsigned xp[2] = {x0, x1}, yp[2] = {y0_, y1_};
+                    asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
+                    const bool su = qk < nqA;
+                    const int base = su ? yk * nqA + qk - sa : 4 * S + yk * tA + 4 * qk - nA4 - ta;
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        // pixels past the window width write a dummy slot past the buffers
+                        const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                        const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                        const bool on = 4 * qk + i < w;
+                        float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 2 * PCA;
+                        const int pp = on ? P : 1;
+                        d1[0] = (float)__mul24(gx, gx);
+                        d1[pp] = (float)__mul24(gx, gy);
+                        d1[2 * pp] = (float)__mul24(gy, gy);
+                    }
+                };
+                // half-wave tiles: the whole wave writes one (as the b fallback's write_tile)
+                constexpr int K1 = UPT / 2;
+                const bool split = HW == 1 && (UPT & 1) == 0;
+                auto swp = [](unsigned a, unsigned b, bool first) {
+                    auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+                    return first ? r[0] : r[1];
+                };
                 auto writeA = [&](int g, float *buf) {
-                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
                     int sa, ta, nsse, ntail;
+                    if (split) {
+                        if ((tid >> 6) != (g >> 1)) return;
+                        geoA(g, sa, ta, nsse, ntail);
+                        const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                        const bool lower = (g & 1) == 0, own = ((tid >> 5) & 1) == (g & 1);
+                        const int ub = (own ? tid : tid ^ 32) * UPT + (lower == own ? 0 : K1);
+                        int yk = ub / QW, qk = ub - yk * QW;
+                        asm volatile("" : "+v"(yk), "+v"(qk));
+#pragma unroll
+                        for (int k = 0; k < K1; k++) {
+                            unitA(yk, qk, ub + k < U, swp(XP[k][0], XP[K1 + k][0], lower), swp(XP[k][1], XP[K1 + k][1], lower),
+                                  swp(YP[k][0], YP[K1 + k][0], lower), swp(YP[k][1], YP[K1 + k][1], lower), buf, S, P, sa, ta);
+                            if (++qk == QW) {
+                                qk = 0;
+                                yk++;
+                            }
+                        }
+                        return;
+                    }
+                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
                     geoA(g, sa, ta, nsse, ntail);
                     const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                     int yk = y0, qk = q0;
                     asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
                     for (int k = 0; k < UPT; k++) {
-                        if (u0 + k < U) {
-                            unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
-                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
-                            const bool su = qk < nqA;
-                            const int base = su ? yk * nqA + qk - sa : 4 * S + yk * tA + 4 * qk - nA4 - ta;
-#pragma unroll
-                            for (int i = 0; i < 4; i++) {
-                                // pixels past the window width write a dummy slot past the buffers
-                                const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
-                                const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
-                                const bool on = 4 * qk + i < w;
-                                float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 2 * PCA;
-                                const int pp = on ? P : 1;
-                                d1[0] = (float)__mul24(gx, gx);
-                                d1[pp] = (float)__mul24(gx, gy);
-                                d1[2 * pp] = (float)__mul24(gy, gy);
-                            }
-                        }
+                        unitA(yk, qk, u0 + k < U, XP[k][0], XP[k][1], YP[k][0], YP[k][1], buf, S, P, sa, ta);
                         if (++qk == QW) {
                             qk = 0;
                             yk++;
