@@ -2717,11 +2717,11 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 // exact integer: the chains start from base0): tiles of HW half waves
                 // (the units of threads 32g..), products chain-major into 3 planes,
                 // double-buffered: the threads of the next tile write its products
-                // while the chain lanes (lanes 0-14 of wave 3; lane c holds chain c's
+                // while the chain lanes (lanes 0-14 of wave 0; lane c holds chain c's
                 // base0) sum the current one
                 const int HW = Q.bx_hw, PCA = 3 * bx_pc(UPT) * HW;
-                const bool chl = tid >= 192 && tid < 207;
-                const int cl = chl ? tid - 192 : 0, cs = cl / 5, cc = cl - 5 * cs;
+                const bool chl = tid < 15;  // wave 0: its tiles are written first, so it rarely writes while it sums
+                const int cl = chl ? tid : 0, cs = cl / 5, cc = cl - 5 * cs;
                 float acc = (float)base0;  // |base0| <= 2^24: exact
                 const int g_last = (U - 1) / (32 * UPT);
                 auto geoA = [&](int g, int &sa, int &ta, int &nsse, int &ntail) {
@@ -2809,7 +2809,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 for (int g = h0, t = 0; g <= g_last; g += HW, t ^= 1) {
                     float *cur = PL + t * PCA, *nxt = PL + (t ^ 1) * PCA;
                     if (g + HW <= g_last) writeA(g + HW, nxt);
-                    if ((tid >> 6) == 3) {
+                    if ((tid >> 6) == 0) {
                         int sa, ta, nsse, ntail;
                         geoA(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
@@ -2820,7 +2820,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     }
                     __syncthreads();
                 }
-                if (tid >= 192) {  // wave 3 combines in the SSE2 build's order
+                if (tid < 64) {  // wave 0 combines in the SSE2 build's order
                     const int av = __float_as_int(acc);
 #pragma unroll
                     for (int s = 0; s < 3; s++) {
@@ -2832,7 +2832,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                             const float c3 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 3));
                             t = __fadd_rn(t, __fadd_rn(__fadd_rn(__fadd_rn(c0, c1), c2), c3));
                         }
-                        if (tid == 192) RS[s] = t;
+                        if (tid == 0) RS[s] = t;
                     }
                 }
                 __syncthreads();
@@ -2956,11 +2956,11 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
             } else {
                 // ordered float chains from half wave h0 on, tiles of 32 threads' units,
                 // double-buffered: the threads of tile g+1 write its products while the
-                // chain lanes (wave 3, lanes 0-9, starting from the exact prefixes
+                // chain lanes (wave 0, lanes 0-9, starting from the exact prefixes
                 // base0) sum tile g
                 const int HW = Q.bx_hw, PC = bx_pc(UPT) * HW;
-                const bool chl = tid >= 192 && tid < 202;
-                const int cl = chl ? tid - 192 : 0, cs = cl / 5, cc = cl - 5 * cs;
+                const bool chl = tid < 10;  // wave 0 (as in the A fallback)
+                const int cl = chl ? tid : 0, cs = cl / 5, cc = cl - 5 * cs;
                 float acc = (float)base0;
                 const int g_last = (U - 1) / (32 * UPT);
                 auto tile_geo = [&](int g, int &sa, int &ta, int &nsse, int &ntail) {
@@ -3058,7 +3058,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     unsigned long long tc0, tc1, tc2;
                     BX_CLK(tc0);
 #endif
-                    if ((tid >> 6) == 3) {
+                    if ((tid >> 6) == 0) {
                         int sa, ta, nsse, ntail;
                         tile_geo(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
@@ -3073,14 +3073,14 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     __syncthreads();
 #ifdef PSN_LK_STAMPS
                     BX_CLK(tc2);
-                    bx_acc[12] += tc1 - tc0;  // (thread 192's view) chain sums incl. its own tile writes
+                    bx_acc[12] += tc1 - tc0;  // (chain lane 0's view) chain sums incl. its own tile writes
                     bx_acc[13] += tc2 - tc1;  // barrier wait
                     bx_acc[14]++;
 #endif
                 }
                 BX_MARK(7);  // serial b: pipelined products + chains
                 BX_COUNT(11);
-                if (tid >= 192) {  // wave 3 combines in the SSE2 build's order
+                if (tid < 64) {  // wave 0 combines in the SSE2 build's order
                     const int a = __float_as_int(acc);
                     float r1 = __int_as_float(__builtin_amdgcn_readlane(a, 4));
                     float r2 = __int_as_float(__builtin_amdgcn_readlane(a, 9));
@@ -3096,7 +3096,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                         r1 = __fadd_rn(r1, __fadd_rn(bb0, bb2));
                         r2 = __fadd_rn(r2, __fadd_rn(bb1, bb3));
                     }
-                    if (tid == 192) {
+                    if (tid == 0) {
                         RS[4] = r1;
                         RS[5] = r2;
                     }
@@ -3209,11 +3209,8 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
         unsigned long long t_end;
         BX_CLK(t_end);
         bx_acc[15] = t_end - bx_t0;
-        if (tid == 0 && A.stamps)
-            for (int i = 0; i < 16; i++)
-                if (i < 12 || i > 14) A.stamps[(size_t)blockIdx.x * 64 + i] = bx_acc[i];
-        if (tid == 192 && A.stamps)
-            for (int i = 12; i < 15; i++) A.stamps[(size_t)blockIdx.x * 64 + i] = bx_acc[i];
+        if (tid == 0 && A.stamps)  // thread 0: also the chain lane of the tile stamps 12-14
+            for (int i = 0; i < 16; i++) A.stamps[(size_t)blockIdx.x * 64 + i] = bx_acc[i];
     }
 #endif
     if (tid == 0) {
