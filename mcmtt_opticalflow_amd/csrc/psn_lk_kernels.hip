@@ -2390,8 +2390,10 @@ __device__ __forceinline__ int hi16(unsigned v) { return (int)v >> 16; }
 // bilinear with the diff folded into the accumulator constant 256 - 512 I
 // (I = the unit's window values, packed pairs ip).
 __device__ __forceinline__ void bx_diffs(const uint32_t *jp, int JRP4, unsigned W0, unsigned W1, unsigned s0,
-                                         unsigned s1, unsigned s2, unsigned s3, const unsigned (&ip)[2], int (&d)[4]) {
+                                         unsigned s1, unsigned s2, unsigned s3, const unsigned (&ipr)[2], int (&d)[4],
+                                         unsigned z) {
     const uint32_t a0 = jp[0], a1 = jp[1], b0 = jp[JRP4], b1 = jp[JRP4 + 1];
+    const unsigned ip[2] = {ipr[0] ^ z, ipr[1] ^ z};  // z: an opaque zero of the caller's loop (no hoisting)
     const int cw[4] = {256 - 512 * lo16(ip[0]), 256 - 512 * hi16(ip[0]), 256 - 512 * lo16(ip[1]), 256 - 512 * hi16(ip[1])};
     d[0] = sdot2(__builtin_amdgcn_perm(b1, b0, s0), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s0), W0, cw[0])) >> 9;
     d[1] = sdot2(__builtin_amdgcn_perm(b1, b0, s1), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s1), W0, cw[1])) >> 9;
@@ -2405,9 +2407,9 @@ __device__ __forceinline__ unsigned bx_sel(int sj, int i) {
 
 // Ordered float sum of a zero-padded LDS chain (16-B aligned, ceil(len/16)
 // blocks of 16 floats; +0 pads leave an integer-valued sum unchanged) onto acc,
-// with two blocks in flight while one is summed: the LDS latency hides behind
-// the dependent adds. Blocks go to three register sets with fixed roles (the
-// loop is unrolled by 3, so no in-flight register is ever copied); the loads
+// with one block in flight while one is summed: the LDS latency (~100 cycles)
+// hides behind the 16 dependent adds. Blocks go to two register sets with fixed
+// roles (the loop is unrolled by 2, so no in-flight register is ever copied); the loads
 // and their lgkmcnt waits are inline asm, because as plain loads the compiler
 // folds the loop-carried registers back into one load at the top of each step
 // and waits there. nbmax = the wave's largest block count (uniform); lanes past
@@ -2419,7 +2421,7 @@ typedef float bxf4 __attribute__((ext_vector_type(4)));
                  : "=v"(v0), "=v"(v1), "=v"(v2), "=v"(v3)                                              \
                  : "v"(addr)                                                                           \
                  : "memory")
-#define BX_WAIT8(v0, v1, v2, v3) asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3))
+#define BX_WAIT4(v0, v1, v2, v3) asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3))
 __device__ __forceinline__ float add16m(float acc, const bxf4 &a, const bxf4 &b, const bxf4 &c, const bxf4 &d, bool on) {
     float t = acc;
     t = t + a.x; t = t + a.y; t = t + a.z; t = t + a.w;
@@ -2436,24 +2438,18 @@ __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax
     // the chain is a dependent add sequence sharing its SIMD with other
     // workgroups' waves: issue it first
     __builtin_amdgcn_s_setprio(3);
-    bxf4 a0, a1, a2, a3, c0, c1, c2, c3, e0, e1, e2, e3;
+    bxf4 a0, a1, a2, a3, c0, c1, c2, c3;
     BX_LD(a0, a1, a2, a3, ad, 0, 16, 32, 48);
-    BX_LD(c0, c1, c2, c3, ad, 64, 80, 96, 112);
-    for (int b = 0; b < nbmax; b += 3) {
-        BX_LD(e0, e1, e2, e3, ad, 128, 144, 160, 176);
-        BX_WAIT8(a0, a1, a2, a3);
+    for (int b = 0; b < nbmax; b += 2) {
+        BX_LD(c0, c1, c2, c3, ad, 64, 80, 96, 112);
+        BX_WAIT4(a0, a1, a2, a3);
         acc = add16m(acc, a0, a1, a2, a3, b < nb);
-        BX_LD(a0, a1, a2, a3, ad, 192, 208, 224, 240);
-        BX_WAIT8(c0, c1, c2, c3);
+        BX_LD(a0, a1, a2, a3, ad, 128, 144, 160, 176);
+        BX_WAIT4(c0, c1, c2, c3);
         acc = add16m(acc, c0, c1, c2, c3, b + 1 < nb);
-        BX_LD(c0, c1, c2, c3, ad, 256, 272, 288, 304);
-        BX_WAIT8(e0, e1, e2, e3);
-        acc = add16m(acc, e0, e1, e2, e3, b + 2 < nb);
-        ad += 192u;
+        ad += 128u;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3)
-                 :
-                 : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : : "memory");
     __builtin_amdgcn_s_setprio(0);
     return acc;
 }
@@ -2884,6 +2880,8 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
             int T1[5] = {0, 0, 0, 0, 0}, M1[5] = {0, 0, 0, 0, 0}, m1[5] = {0, 0, 0, 0, 0};
             int T2[5] = {0, 0, 0, 0, 0}, M2[5] = {0, 0, 0, 0, 0}, m2[5] = {0, 0, 0, 0, 0};
             int dmax = 0;
+            unsigned zm;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(zm));
             {
                 int y = y0, q = q0;
             asm volatile("" : "+v"(y), "+v"(q));  // opaque: no per-unit address hoisting (VGPRs)
@@ -2891,7 +2889,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 for (int k = 0; k < UPT; k++) {
                     const bool uv = u0 + k < U;
                     int d[4];
-                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, zm);
                     int t1[4], t2[4];
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
@@ -2972,10 +2970,10 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 };
                 // one unit's b products into the tile's chain regions
                 auto tile_unit = [&](int yk, int qk, bool uv, const unsigned (&ip)[2], const unsigned (&xp)[2],
-                                     const unsigned (&yp)[2], float *buf, int S, int P, int sa, int ta) {
+                                     const unsigned (&yp)[2], float *buf, int S, int P, int sa, int ta, unsigned zf) {
                     if (!uv) return;
                     int d[4];
-                    bx_diffs(JR32 + (oy + yk) * JRP4 + (ox >> 2) + qk, JRP4, W0, W1, s0, s1, s2, s3, ip, d);
+                    bx_diffs(JR32 + (oy + yk) * JRP4 + (ox >> 2) + qk, JRP4, W0, W1, s0, s1, s2, s3, ip, d, zf);
                     const bool su = qk < nqB;
                     const int base = su ? yk * nqB + qk - sa : 4 * S + yk * tB + 4 * qk - n8 - ta;
 #pragma unroll
@@ -3002,6 +3000,8 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     return first ? r[0] : r[1];
                 };
                 auto write_tile = [&](int g, float *buf) {
+                    unsigned zf;  // opaque zero per tile: no diff constants hoisted out of the tile loop
+                    asm volatile("v_mov_b32 %0, 0" : "=v"(zf));
                     int sa, ta, nsse, ntail;
                     if (split) {
                         if ((tid >> 6) != (g >> 1)) return;
@@ -3016,7 +3016,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                             const unsigned ip[2] = {swp(IP[k][0], IP[K1 + k][0], lower), swp(IP[k][1], IP[K1 + k][1], lower)};
                             const unsigned xp[2] = {swp(XP[k][0], XP[K1 + k][0], lower), swp(XP[k][1], XP[K1 + k][1], lower)};
                             const unsigned yp[2] = {swp(YP[k][0], YP[K1 + k][0], lower), swp(YP[k][1], YP[K1 + k][1], lower)};
-                            tile_unit(yk, qk, ub + k < U, ip, xp, yp, buf, S, P, sa, ta);
+                            tile_unit(yk, qk, ub + k < U, ip, xp, yp, buf, S, P, sa, ta, zf);
                             if (++qk == QW) {
                                 qk = 0;
                                 yk++;
@@ -3031,7 +3031,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
                     for (int k = 0; k < UPT; k++) {
-                        tile_unit(yk, qk, u0 + k < U, IP[k], XP[k], YP[k], buf, S, P, sa, ta);
+                        tile_unit(yk, qk, u0 + k < U, IP[k], XP[k], YP[k], buf, S, P, sa, ta, zf);
                         if (++qk == QW) {
                             qk = 0;
                             yk++;
@@ -3153,7 +3153,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                 for (int k = 0; k < UPT; k++) {
                     const bool uv = u0 + k < U;
                     int d[4];
-                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, 0u);
 #pragma unroll
                     for (int i = 0; i < 4; i++)
                         if (uv && 4 * q + i < w) e += (unsigned)abs(d[i]);
@@ -3183,7 +3183,7 @@ __global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
                     for (int k = 0; k < UPT; k++) {
                         if (u0 + k < U && yk >= r0 && yk < r0 + tr) {
                             int d[4];
-                            bx_diffs(JR32 + (oy + (yk)) * JRP4 + (ox >> 2) + (qk), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d);
+                            bx_diffs(JR32 + (oy + (yk)) * JRP4 + (ox >> 2) + (qk), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, 0u);
 #pragma unroll
                             for (int i = 0; i < 4; i++)
                                 if (4 * qk + i < w) PL[(yk - r0) * w + 4 * qk + i] = (float)abs(d[i]);
