@@ -16,7 +16,10 @@ One step = one frame of every camera through CPSNWhere_Tracker2D::Run
      between them, all cameras in one launch per step (:763-811);
   3. forward LK of every active tracker (64x160) + matching cost (:851-1025);
   4. assignment, tracker update, ResultWithTracker (:1038-1164, :1231-1257);
-  5. every camera's stTrack2DResult packed into its binary slot in host memory;
+  5. every camera's stTrack2DResult packed into its binary slot in host memory.
+     Frames are pipelined as psn_t2d_group_complete_next allows: frame t+1's
+     backward chains are enqueued as soon as frame t's device work is done, and
+     run while the host does frame t's step 4-5 (same results as launch/complete);
      N > 1: one RCCL all-gather of the slots over xGMI (psn_comm_allgather, the
      hand-off into Associator3D, PSNWhere.cpp:264-269), landing in host memory.
 The timed region therefore runs from host frames to host results.
@@ -258,11 +261,14 @@ def tracker_main(args):
     exch = pdist.ResultExchange(world, rank, C * slot_bytes, device=local_rank) if world > 1 else None
     T = t2d.load()
 
-    def step(t, dets):
-        group.launch(t, dets)
+    def step(t, dets, next_dets):
+        group.launch(t, dets)  # after complete_next(t-1): frame t's forward calls only
         for k, fd in enumerate(feeds):  # frame t+1 uploads while frame t runs
             fd.push(group, k, t + 1)
-        group.complete_raw()
+        if next_dets is None:
+            group.complete_raw()
+        else:  # frame t+1's chains go to the GPU before the host matches frame t
+            group.complete_next(t + 1, next_dets, raw=True)
         for k in range(C):  # the hand-off slots (psn_t2d_pack_result) in host memory
             rc = T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
             if rc:
@@ -275,10 +281,15 @@ def tracker_main(args):
     for k, fd in enumerate(feeds):
         fd.push(group, k, 0)
     t = 0
-    for _ in range(args.warmup):
-        step(t, all_dets(t))
+    dets_warm = [all_dets(t + i) for i in range(args.warmup)]
+    # records built outside the timed region; one more frame: the last timed step launches its chains
+    # ahead, as the warm-up's last step did for the first timed frame (the timed region holds exactly
+    # `steps` frames' backward chains and forward calls)
+    dets_timed = [all_dets(args.warmup + i) for i in range(args.steps + 1)]
+    seq = dets_warm + dets_timed
+    for i in range(args.warmup):
+        step(t, seq[i], seq[i + 1] if i + 1 < len(seq) else None)
         t += 1
-    dets_timed = [all_dets(t + i) for i in range(args.steps)]  # records built outside the timed region
     lkh = group.lk_handle()
     L.psn_lk_enable_timing(lkh, 16 * args.steps + 64, 1)  # every LK launch (forward + 3 chain steps)
     sampler = SampleCounter(L, lkh)
@@ -287,7 +298,8 @@ def tracker_main(args):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        gathered = step(t, dets_timed[i])
+        j = args.warmup + i
+        gathered = step(t, seq[j], seq[j + 1])
         t += 1
     torch.cuda.synchronize()
     if world > 1:

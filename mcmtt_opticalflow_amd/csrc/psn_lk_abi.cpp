@@ -722,11 +722,11 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         }
         if (!all_single && all_box && c->box && !c->force_generic && !forced) {
             lds_bx = 0;  // the launch's UPT sizes every query's fallback planes; tiles as large as
-                         // three workgroups per CU allow
+                         // the kernel's occupancy (bx_occupancy) allows
             for (int i = 0; i < nqd; i++) {
                 psn::LkQueryDev &d = a.q[i];
                 d.bx_hw = 1;
-                while (d.bx_hw < 8 && psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw + 1).total <= psn::kBxLdsTarget)
+                while (d.bx_hw < 8 && psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw + 1).total <= psn::bx_lds_target(upt_bx))
                     d.bx_hw++;
                 lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw).total);
             }

@@ -2479,7 +2479,7 @@ __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax
     } while (0)
 #endif
 template <int UPT>
-__global__ __launch_bounds__(kBxNT, 3) void lk_kernel_bx(LkLaunchArgs A) {
+__global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NT = kBxNT;
     const int tid = threadIdx.x, lane = tid & 63;

@@ -16,9 +16,16 @@ struct psn_t2d {
 
 struct psn_t2d_group {
     psn::Tracker2DFlow flow;
-    std::vector<psn::Tracker2DFlow::CamFrame> io;
+    // two frames' io: the current frame's, and the next frame's once its chains
+    // are launched ahead (psn_t2d_group_complete_next)
+    std::vector<psn::Tracker2DFlow::CamFrame> iob[2];
+    std::vector<psn::Tracker2DFlow::CamFrame> &io() { return iob[cur]; }
+    int cur = 0;
     int feature_mode = PSN_T2D_FEATURES_GIVEN;
     bool launched = false;
+    bool ahead = false;  // the next frame's chains are in flight
+    unsigned ahead_frame = 0;
+    int ahead_mode = PSN_T2D_FEATURES_GIVEN;
     std::string err;
 };
 
@@ -442,7 +449,8 @@ int psn_t2d_group_create(int device, int ncams, const unsigned *cam_ids, int wid
         delete g;
         return rc;
     }
-    g->io.resize((size_t)ncams);
+    g->iob[0].resize((size_t)ncams);
+    g->iob[1].resize((size_t)ncams);
     *out = g;
     return 0;
 }
@@ -459,17 +467,17 @@ static int gset(psn_t2d_group *g, int rc) {
 }
 
 int psn_t2d_group_push_frame(psn_t2d_group *g, int cam, const uint8_t *frame, int stride, int channels) {
-    if (!g || cam < 0 || (size_t)cam >= g->io.size() || !frame) return PSN_LK_ERR_ARG;
+    if (!g || cam < 0 || (size_t)cam >= g->io().size() || !frame) return PSN_LK_ERR_ARG;
     return gset(g, g->flow.StageFrame((size_t)cam, frame, stride, channels, false));
 }
 
 int psn_t2d_group_push_frame_device(psn_t2d_group *g, int cam, const uint8_t *dev_frame, int stride, int channels) {
-    if (!g || cam < 0 || (size_t)cam >= g->io.size() || !dev_frame) return PSN_LK_ERR_ARG;
+    if (!g || cam < 0 || (size_t)cam >= g->io().size() || !dev_frame) return PSN_LK_ERR_ARG;
     return gset(g, g->flow.StageFrame((size_t)cam, dev_frame, stride, channels, true));
 }
 
 int psn_t2d_group_push_frame_jpeg(psn_t2d_group *g, int cam, const uint8_t *jpeg, size_t len) {
-    if (!g || cam < 0 || (size_t)cam >= g->io.size() || !jpeg) return PSN_LK_ERR_ARG;
+    if (!g || cam < 0 || (size_t)cam >= g->io().size() || !jpeg) return PSN_LK_ERR_ARG;
     return gset(g, g->flow.StageFrameJpeg((size_t)cam, jpeg, len));
 }
 
@@ -478,28 +486,33 @@ int psn_t2d_group_launch(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection
     if (!g || !ndet || !dets || (feature_mode != PSN_T2D_FEATURES_GIVEN && feature_mode != PSN_T2D_FEATURES_GRIDFAST) ||
         g->launched)
         return PSN_LK_ERR_ARG;
-    for (size_t c = 0; c < g->io.size(); c++) {
-        if (ndet[c] < 0 || (ndet[c] > 0 && !dets[c])) return PSN_LK_ERR_ARG;
-        psn::Tracker2DFlow::CamFrame &f = g->io[c];
-        const int rc = detections_in(dets[c], ndet[c], f.dets, f.features, feature_mode == PSN_T2D_FEATURES_GIVEN);
-        if (rc) return rc;
+    if (g->ahead) {  // the frame announced by complete_next: its detections are in io() already
+        if (frame_idx != g->ahead_frame || feature_mode != g->ahead_mode) return PSN_LK_ERR_ARG;
+        for (size_t c = 0; c < g->io().size(); c++)
+            if (ndet[c] < 0 || (size_t)ndet[c] != g->io()[c].dets.size()) return PSN_LK_ERR_ARG;
+    } else {
+        for (size_t c = 0; c < g->io().size(); c++) {
+            if (ndet[c] < 0 || (ndet[c] > 0 && !dets[c])) return PSN_LK_ERR_ARG;
+            psn::Tracker2DFlow::CamFrame &f = g->io()[c];
+            const int rc = detections_in(dets[c], ndet[c], f.dets, f.features, feature_mode == PSN_T2D_FEATURES_GIVEN);
+            if (rc) return rc;
+        }
     }
     g->feature_mode = feature_mode;
-    const int rc = g->flow.RunLaunch(frame_idx, g->io, feature_mode == PSN_T2D_FEATURES_GRIDFAST, seed);
+    const int rc = g->flow.RunLaunch(frame_idx, g->io(), feature_mode == PSN_T2D_FEATURES_GRIDFAST, seed);
+    g->ahead = false;
     if (rc) return gset(g, rc);
     g->launched = true;
     return 0;
 }
 
-int psn_t2d_group_complete(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,
-                           psn_track2d_result *results) {
-    if (!g || !ndet || !dets || !results || !g->launched) return PSN_LK_ERR_ARG;
-    g->launched = false;
-    int rc = g->flow.RunComplete(g->io);
-    if (rc) return gset(g, rc);
-    for (size_t c = 0; c < g->io.size(); c++) {
-        psn::Tracker2DFlow::CamFrame &f = g->io[c];
+// results of the current frame (after RunComplete) into the caller's records
+static int group_outputs(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,
+                         psn_track2d_result *results) {
+    for (size_t c = 0; c < g->io().size(); c++) {
+        psn::Tracker2DFlow::CamFrame &f = g->io()[c];
         if ((size_t)ndet[c] != f.dets.size()) return PSN_LK_ERR_ARG;
+        int rc = 0;
         if (g->feature_mode == PSN_T2D_FEATURES_GRIDFAST)
             for (int i = 0; i < ndet[c]; i++) {
                 rc = put_points(f.features[(size_t)i], dets[c][i].features, &dets[c][i].num_features);
@@ -512,6 +525,40 @@ int psn_t2d_group_complete(psn_t2d_group *g, psn_t2d_detection *const *dets, con
     return 0;
 }
 
+int psn_t2d_group_complete(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,
+                           psn_track2d_result *results) {
+    if (!g || !ndet || !dets || !results || !g->launched) return PSN_LK_ERR_ARG;
+    g->launched = false;
+    const int rc = g->flow.RunComplete(g->io());
+    if (rc) return gset(g, rc);
+    return group_outputs(g, dets, ndet, results);
+}
+
+int psn_t2d_group_complete_next(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,
+                                psn_track2d_result *results, unsigned next_frame_idx,
+                                psn_t2d_detection *const *next_dets, const int *next_ndet, int feature_mode,
+                                uint32_t seed) {
+    if (!g || !ndet || !dets || !results || !g->launched || !next_ndet || !next_dets ||
+        (feature_mode != PSN_T2D_FEATURES_GIVEN && feature_mode != PSN_T2D_FEATURES_GRIDFAST))
+        return PSN_LK_ERR_ARG;
+    std::vector<psn::Tracker2DFlow::CamFrame> &nx = g->iob[g->cur ^ 1];
+    for (size_t c = 0; c < nx.size(); c++) {
+        if (next_ndet[c] < 0 || (next_ndet[c] > 0 && !next_dets[c])) return PSN_LK_ERR_ARG;
+        const int rc = detections_in(next_dets[c], next_ndet[c], nx[c].dets, nx[c].features,
+                                     feature_mode == PSN_T2D_FEATURES_GIVEN);
+        if (rc) return rc;
+    }
+    g->launched = false;
+    const int rc = g->flow.RunComplete(g->io(), &nx, next_frame_idx, feature_mode == PSN_T2D_FEATURES_GRIDFAST, seed);
+    if (rc) return gset(g, rc);
+    const int orc = group_outputs(g, dets, ndet, results);
+    g->cur ^= 1;  // the next frame's io, launched ahead
+    g->ahead = true;
+    g->ahead_frame = next_frame_idx;
+    g->ahead_mode = feature_mode;
+    return orc;
+}
+
 int psn_t2d_group_run(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *const *dets, const int *ndet,
                       int feature_mode, uint32_t seed, psn_track2d_result *results) {
     const int rc = psn_t2d_group_launch(g, frame_idx, dets, ndet, feature_mode, seed);
@@ -519,7 +566,7 @@ int psn_t2d_group_run(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *c
 }
 
 int psn_t2d_group_trackers(psn_t2d_group *g, int cam, psn_t2d_tracker *out, int cap, int *n) {
-    if (!g || cam < 0 || (size_t)cam >= g->io.size() || !n || cap < 0 || (cap > 0 && !out)) return PSN_LK_ERR_ARG;
+    if (!g || cam < 0 || (size_t)cam >= g->io().size() || !n || cap < 0 || (cap > 0 && !out)) return PSN_LK_ERR_ARG;
     const std::deque<psn::Tracker2D *> &a = g->flow.ActiveTrackers((size_t)cam);
     *n = (int)a.size();
     if ((int)a.size() > cap) return PSN_T2D_ERR_CAPACITY;

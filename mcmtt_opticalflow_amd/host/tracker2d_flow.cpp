@@ -142,19 +142,28 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
     return psn_lk_set_stream(lk_, cs);
 }
 
-// Device and pinned-host buffers of a device pass (grown on demand).
+// Device and pinned-host buffers of a device pass (grown on demand). The
+// backward chains and the forward calls have separate arrays: a frame's chains
+// may run (launched ahead, RunComplete with a next frame) while its forward
+// inputs are staged and, if need be, its forward buffers regrown.
 struct Tracker2DFlow::DeviceBuffers {
     size_t nchains = 0, nfwd_pts = 0, nfwd_jobs = 0;
+    // chains: inputs, LK outputs, ping-pong point sets, err/status
     float *d_in = nullptr, *d_out = nullptr, *d_buf[2] = {nullptr, nullptr}, *d_err = nullptr;
     uint8_t *d_status = nullptr;
     double *d_boxes = nullptr, *d_obox = nullptr;
     float *d_sets = nullptr;
     int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr, *d_tot = nullptr, *d_last = nullptr;
+    // forward calls
+    float *d_fin = nullptr, *d_fout = nullptr, *d_ferr = nullptr;
+    uint8_t *d_fstatus = nullptr;
+    int *d_fcnt = nullptr;
     // pinned staging: inputs, then results
-    float *h_in = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
+    float *h_in = nullptr, *h_fin = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
     uint8_t *h_fwd_st = nullptr;
     double *h_boxes = nullptr, *h_obox = nullptr;
-    int *h_cnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr, *h_rawcnt = nullptr, *h_last = nullptr;
+    int *h_cnt = nullptr, *h_fcnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr, *h_rawcnt = nullptr,
+        *h_last = nullptr;
     // the chain's results live in one block per side, [nsteps | set counts | boxes | sets], so that
     // one memset clears the counters and one copy returns every used byte
     char *d_res = nullptr, *h_res = nullptr;
@@ -166,14 +175,39 @@ struct Tracker2DFlow::DeviceBuffers {
         sets = (float *)(base + res_sets_off);
     }
     static size_t res_box_off(size_t K, size_t S) { return (K * (1 + S) * 4 + 255) & ~(size_t)255; }
-    void release() {
-        for (void *p : {(void *)d_in, (void *)d_out, (void *)d_buf[0], (void *)d_buf[1], (void *)d_err, (void *)d_status,
-                        (void *)d_boxes, (void *)d_res, (void *)d_cnt, (void *)d_tot, (void *)d_last})
+    static void free_all(std::initializer_list<void *> dev, std::initializer_list<void *> host) {
+        for (void *p : dev)
             if (p) (void)hipFree(p);
-        for (void *p : {(void *)h_in, (void *)h_fwd_out, (void *)h_fwd_st, (void *)h_boxes, (void *)h_res,
-                        (void *)h_cnt, (void *)h_rawcnt, (void *)h_last})
+        for (void *p : host)
             if (p) (void)hipHostFree(p);
-        *this = DeviceBuffers();
+    }
+    void release_chains() {
+        free_all({d_in, d_out, d_buf[0], d_buf[1], d_err, d_status, d_boxes, d_res, d_cnt, d_tot, d_last},
+                 {h_in, h_boxes, h_res, h_cnt, h_rawcnt, h_last});
+        d_in = d_out = d_buf[0] = d_buf[1] = d_err = d_sets = nullptr;
+        d_status = nullptr;
+        d_boxes = d_obox = nullptr;
+        d_res = nullptr;
+        d_cnt = d_setcnt = d_nsteps = d_tot = d_last = nullptr;
+        h_in = h_sets = nullptr;
+        h_boxes = h_obox = nullptr;
+        h_res = nullptr;
+        h_cnt = h_setcnt = h_nsteps = h_rawcnt = h_last = nullptr;
+        nchains = 0;
+    }
+    void release_forward() {
+        free_all({d_fin, d_fout, d_ferr, d_fstatus, d_fcnt}, {h_fin, h_fwd_out, h_fwd_st, h_fcnt});
+        d_fin = d_fout = d_ferr = nullptr;
+        d_fstatus = nullptr;
+        d_fcnt = nullptr;
+        h_fin = h_fwd_out = nullptr;
+        h_fwd_st = nullptr;
+        h_fcnt = nullptr;
+        nfwd_pts = nfwd_jobs = 0;
+    }
+    void release() {
+        release_chains();
+        release_forward();
     }
 };
 
@@ -199,47 +233,75 @@ void Tracker2DFlow::Finalize() {
     cams_.clear();
 }
 
-int Tracker2DFlow::EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_jobs) {
+// Chain buffers for nchains detections: grown only between passes (no chain in
+// flight on the chain stream).
+int Tracker2DFlow::EnsureChains(size_t nchains) {
     if (!dev_) dev_ = new DeviceBuffers();
     DeviceBuffers &b = *dev_;
-    if (b.nchains >= nchains && b.nfwd_pts >= nfwd_pts && b.nfwd_jobs >= nfwd_jobs && b.d_in) return PSN_LK_OK;
+    if (b.nchains >= nchains && b.d_in) return PSN_LK_OK;
     if (lk_) psn_lk_sync(lk_);
-    if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
-    b.release();
-    const size_t K = std::max<size_t>(nchains, 16), F = std::max<size_t>(nfwd_pts, 1024), J = std::max<size_t>(nfwd_jobs, 16);
-    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, npt = K * cap + F;
+    b.release_chains();
+    const size_t K = std::max<size_t>(nchains, 16);
+    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, npt = K * cap;
     bool ok = true;
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
     auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
     dm((void **)&b.d_in, npt * 8);
     dm((void **)&b.d_out, npt * 8);
-    dm((void **)&b.d_buf[0], K * cap * 8);
-    dm((void **)&b.d_buf[1], K * cap * 8);
+    dm((void **)&b.d_buf[0], npt * 8);
+    dm((void **)&b.d_buf[1], npt * 8);
     dm((void **)&b.d_err, npt * 4);
     dm((void **)&b.d_status, npt);
     dm((void **)&b.d_boxes, K * 4 * 8);
     b.res_sets_off = DeviceBuffers::res_box_off(K, S) + K * S * 4 * 8;
     const size_t res_bytes = b.res_sets_off + K * S * cap * 8;
     dm((void **)&b.d_res, res_bytes);
-    dm((void **)&b.d_cnt, (K + J) * 4);
+    dm((void **)&b.d_cnt, K * 4);
     dm((void **)&b.d_tot, K * 4);
     dm((void **)&b.d_last, K * 4);
     hm((void **)&b.h_in, npt * 8);
-    hm((void **)&b.h_fwd_out, F * 8);
-    hm((void **)&b.h_fwd_st, F);
     hm((void **)&b.h_boxes, K * 4 * 8);
     hm((void **)&b.h_res, res_bytes);
-    hm((void **)&b.h_cnt, (K + J) * 4);
+    hm((void **)&b.h_cnt, K * 4);
     hm((void **)&b.h_rawcnt, K * 4);
     hm((void **)&b.h_last, K * 4);
     if (!ok) {
-        b.release();
-        err_ = "device-pass buffers: allocation failed";
+        b.release_chains();
+        err_ = "chain buffers: allocation failed";
         return PSN_LK_ERR_NOMEM;
     }
     b.carve(b.d_res, b.d_obox, b.d_sets, b.d_setcnt, b.d_nsteps, K, S);
     b.carve(b.h_res, b.h_obox, b.h_sets, b.h_setcnt, b.h_nsteps, K, S);
     b.nchains = K;
+    return PSN_LK_OK;
+}
+
+// Forward buffers for nfwd_pts points in nfwd_jobs calls: the forward stream is
+// the only device user, so growing them never waits for a chain in flight.
+int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
+    if (!dev_) dev_ = new DeviceBuffers();
+    DeviceBuffers &b = *dev_;
+    if (b.nfwd_pts >= nfwd_pts && b.nfwd_jobs >= nfwd_jobs && b.d_fin) return PSN_LK_OK;
+    if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+    b.release_forward();
+    const size_t F = std::max<size_t>(nfwd_pts, 1024), J = std::max<size_t>(nfwd_jobs, 16);
+    bool ok = true;
+    auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
+    auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
+    dm((void **)&b.d_fin, F * 8);
+    dm((void **)&b.d_fout, F * 8);
+    dm((void **)&b.d_ferr, F * 4);
+    dm((void **)&b.d_fstatus, F);
+    dm((void **)&b.d_fcnt, J * 4);
+    hm((void **)&b.h_fin, F * 8);
+    hm((void **)&b.h_fwd_out, F * 8);
+    hm((void **)&b.h_fwd_st, F);
+    hm((void **)&b.h_fcnt, J * 4);
+    if (!ok) {
+        b.release_forward();
+        err_ = "forward buffers: allocation failed";
+        return PSN_LK_ERR_NOMEM;
+    }
     b.nfwd_pts = F;
     b.nfwd_jobs = J;
     return PSN_LK_OK;
@@ -273,31 +335,31 @@ static int window_error(int win) {
 // waiting for the pass would hold up, on the copy engine, the uploads of the
 // next frames (StageFrame) that the caller enqueues in between.
 int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed) {
+    const int rc = PassLaunchChains(pc, gridfast, seed);
+    return rc ? rc : PassLaunchForward(pc);
+}
+
+// 1-2 of the pass: features and the backward chains, on the chain stream.
+int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uint32_t seed) {
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
-    size_t K = 0, J = 0, F = 0;
+    size_t K = 0;
     for (PassCam &p : pc) {
         p.k0 = K;
-        p.j0 = J;
-        p.f0 = F;
         K += p.dets->size();
-        if (p.fwd) {
-            J += p.fwd->size();
-            for (const Job &jb : *p.fwd) F += jb.in->size();
-        }
     }
-    if (K == 0 && J == 0) return PSN_LK_OK;
-    int rc = EnsureDevice(K, F, J);
+    win_bad_.assign(K, 0);
+    if (K == 0) return PSN_LK_OK;
+    int rc = EnsureChains(K);
     if (rc) return rc;
     DeviceBuffers &b = *dev_;
-    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_);
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !rc) {
             err_ = std::string(what) + ": " + hipGetErrorString(e);
             rc = PSN_LK_ERR_HIP;
         }
     };
-    win_bad_.assign(K, 0);
-    if (K) {  // 1-2. features and the backward chains
+    {
         int max_steps = 0;
         for (PassCam &p : pc) {
             const int steps = StepsAvailable(p.cam);
@@ -401,9 +463,35 @@ int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t 
             if (rc) return fail(rc, "psn_t2d_chain_step_device");
         }
     }
-    // 3. forward calls (every LK launch waits for the builds of the slots it reads)
-    if (J) {
-        size_t o = K * cap;
+    return rc;
+}
+
+// 3 of the pass: the forward calls of every camera's trackers, on the forward
+// stream, in their own arrays (every LK launch waits for the builds of the
+// slots it reads).
+int Tracker2DFlow::PassLaunchForward(std::vector<PassCam> &pc) {
+    size_t J = 0, F = 0;
+    for (PassCam &p : pc) {
+        p.j0 = J;
+        p.f0 = F;
+        if (p.fwd) {
+            J += p.fwd->size();
+            for (const Job &jb : *p.fwd) F += jb.in->size();
+        }
+    }
+    if (J == 0) return PSN_LK_OK;
+    int rc = EnsureForward(F, J);
+    if (rc) return rc;
+    DeviceBuffers &b = *dev_;
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && !rc) {
+            err_ = std::string(what) + ": " + hipGetErrorString(e);
+            rc = PSN_LK_ERR_HIP;
+        }
+    };
+    {
+        size_t o = 0;
         fwd_queries_.clear();
         for (PassCam &p : pc) {
             if (!p.fwd) continue;
@@ -417,21 +505,21 @@ int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t 
                 psn_lk_default_params(&q.params);  // maxLevel 3, (COUNT|EPS, 30, 0.01), minEig 1e-4
                 q.params.win_w = jb.win_w;
                 q.params.win_h = jb.win_h;
-                b.h_cnt[K + fwd_queries_.size()] = (int)pts.size();
+                b.h_fcnt[fwd_queries_.size()] = (int)pts.size();
                 fwd_queries_.push_back(q);
                 for (size_t i = 0; i < pts.size(); i++, o++) {
-                    b.h_in[2 * o] = pts[i].x;
-                    b.h_in[2 * o + 1] = pts[i].y;
+                    b.h_fin[2 * o] = pts[i].x;
+                    b.h_fin[2 * o + 1] = pts[i].y;
                 }
             }
         }
-        if (F) chk(hipMemcpyAsync(b.d_in + 2 * K * cap, b.h_in + 2 * K * cap, F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
-        chk(hipMemcpyAsync(b.d_cnt + K, b.h_cnt + K, J * 4, hipMemcpyHostToDevice, fs), "forward counts");
+        if (F) chk(hipMemcpyAsync(b.d_fin, b.h_fin, F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
+        chk(hipMemcpyAsync(b.d_fcnt, b.h_fcnt, J * 4, hipMemcpyHostToDevice, fs), "forward counts");
         if (rc) return rc;
         rc = psn_lk_set_stream(lk_, fs);
         if (!rc)
-            rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_cnt + K, b.d_in, b.d_out, b.d_status,
-                                             b.d_err);
+            rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_fcnt, b.d_fin, b.d_fout, b.d_fstatus,
+                                             b.d_ferr);
         const int rs = psn_lk_set_stream(lk_, st);
         if (rc || rs) return fail(rc ? rc : rs, "forward launch");
     }
@@ -441,6 +529,14 @@ int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t 
 // Wait for the pass and unpack it: features (GridFAST mode), every valid
 // detection's chain (boxes, point sets), the forward outputs.
 int Tracker2DFlow::PassComplete(std::vector<PassCam> &pc, bool gridfast) {
+    int rc = PassWait(pc);
+    if (!rc) rc = PassFeatures(pc, gridfast);
+    if (!rc) PassUnpack(pc);
+    return rc;
+}
+
+// Enqueue the result copies and wait for the pass's device work.
+int Tracker2DFlow::PassWait(std::vector<PassCam> &pc) {
     int rc = PSN_LK_OK;
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !rc) {
@@ -461,29 +557,46 @@ int Tracker2DFlow::PassComplete(std::vector<PassCam> &pc, bool gridfast) {
         chk(hipMemcpyAsync(bp->h_res, bp->d_res, bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
             "chain results");
     if (F && bp) {
-        chk(hipMemcpyAsync(bp->h_fwd_out, bp->d_out + 2 * K * cap, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
-        chk(hipMemcpyAsync(bp->h_fwd_st, bp->d_status + K * cap, F, hipMemcpyDeviceToHost, fs), "forward status");
+        chk(hipMemcpyAsync(bp->h_fwd_out, bp->d_fout, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
+        chk(hipMemcpyAsync(bp->h_fwd_st, bp->d_fstatus, F, hipMemcpyDeviceToHost, fs), "forward status");
     }
     chk(hipStreamSynchronize(st), "chain sync");
     chk(hipStreamSynchronize(fs), "forward sync");
-    if (rc) return rc;
+    return rc;
+}
+
+// After PassWait: what the next pass's chain launch overwrites (the chain
+// input staging h_in / h_rawcnt, win_bad_): GridFAST features, window errors.
+int Tracker2DFlow::PassFeatures(std::vector<PassCam> &pc, bool gridfast) {
+    if (!gridfast) return PSN_LK_OK;
+    const size_t cap = PSN_T2D_CHAIN_CAP;
+    DeviceBuffers *bp = dev_;
     for (PassCam &p : pc) {
         const size_t n = p.dets->size();
-        if (gridfast) {
-            p.features->assign(n, {});
-            for (size_t i = 0; i < n; i++) {
-                const size_t k = p.k0 + i;
-                const int m = bp->h_rawcnt[k];
-                // a window the LK cannot run fails the frame only if the chain had to run it (:744)
-                if (win_bad_[k] && (size_t)m >= kT2dMinFeatures) {
-                    err_ = "detection " + std::to_string(i) + " window";
-                    return window_error((int)(bp->h_boxes[4 * k + 2] * kWinSizeRatio));
-                }
-                const float *xy = bp->h_in + 2 * cap * k;
-                (*p.features)[i].resize((size_t)m);
-                for (int j = 0; j < m; j++) (*p.features)[i][(size_t)j] = Point2f{xy[2 * j], xy[2 * j + 1]};
+        p.features->assign(n, {});
+        for (size_t i = 0; i < n; i++) {
+            const size_t k = p.k0 + i;
+            const int m = bp->h_rawcnt[k];
+            // a window the LK cannot run fails the frame only if the chain had to run it (:744)
+            if (win_bad_[k] && (size_t)m >= kT2dMinFeatures) {
+                err_ = "detection " + std::to_string(i) + " window";
+                return window_error((int)(bp->h_boxes[4 * k + 2] * kWinSizeRatio));
             }
+            const float *xy = bp->h_in + 2 * cap * k;
+            (*p.features)[i].resize((size_t)m);
+            for (int j = 0; j < m; j++) (*p.features)[i][(size_t)j] = Point2f{xy[2 * j], xy[2 * j + 1]};
         }
+    }
+    return PSN_LK_OK;
+}
+
+// After PassWait: the chains' boxes and point sets (h_res) and the forward
+// outputs, which a next pass's chain launch leaves alone (unless it regrows the
+// chain buffers: ChainsFit).
+void Tracker2DFlow::PassUnpack(std::vector<PassCam> &pc) {
+    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
+    DeviceBuffers *bp = dev_;
+    for (PassCam &p : pc) {
         std::vector<Chain> chains;
         BackwardBegin(*p.dets, *p.features, *p.out, chains);  // valid detections, in order
         for (DetectedObject &ob : *p.out) {
@@ -513,7 +626,12 @@ int Tracker2DFlow::PassComplete(std::vector<PassCam> &pc, bool gridfast) {
             }
         }
     }
-    return PSN_LK_OK;
+}
+
+bool Tracker2DFlow::ChainsFit(const std::vector<CamFrame> &io) const {
+    size_t K = 0;
+    for (const CamFrame &f : io) K += f.dets.size();
+    return K == 0 || (dev_ && dev_->d_in && dev_->nchains >= K);
 }
 
 // One camera (0), one pass, synchronous.
@@ -937,10 +1055,9 @@ int Tracker2DFlow::TrackFrame(const std::vector<Detection> &dets, const std::vec
 
 // Adopt every camera's staged frame as frame t (the ring advances: the oldest
 // slot becomes the next staging slot; Run's buffer circulation, :310-316) and
-// enqueue the frame's device work: one pass over all cameras (forward calls of
-// every active tracker, features, backward chains).
-int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool gridfast, uint32_t seed) {
-    if (!lk_ || io.size() != cams_.size()) return PSN_LK_ERR_ARG;
+// set up the pass over io (forward calls not yet attached).
+int Tracker2DFlow::AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::vector<PassCam> &pass) {
+    if (io.size() != cams_.size()) return PSN_LK_ERR_ARG;
     for (size_t c = 0; c < cams_.size(); c++) {
         if (!cams_[c].staged) {
             err_ = "camera " + std::to_string(c) + ": no frame staged";
@@ -948,9 +1065,7 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
         }
         if (!gridfast && io[c].features.size() != io[c].dets.size()) return PSN_LK_ERR_ARG;
     }
-    run_frame_ = frameIdx;
-    run_gridfast_ = gridfast;
-    run_pass_.assign(cams_.size(), PassCam());
+    pass.assign(cams_.size(), PassCam());
     for (size_t c = 0; c < cams_.size(); c++) {
         Cam &cam = cams_[c];
         const int oldest = cam.ring[0];
@@ -958,18 +1073,48 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
         cam.ring[kT2dInterval - 1] = cam.spare;
         cam.spare = oldest;
         cam.staged = false;
-        cam.trackers.assign(cam.active.begin(), cam.active.end());
-        cam.fwd.clear();
-        ForwardJobs(c, cam.trackers, cam.fstatus, cam.fwd);
-        PassCam &p = run_pass_[c];
+        PassCam &p = pass[c];
         p.cam = c;
         p.dets = &io[c].dets;
         p.features = &io[c].features;
         p.out = &io[c].objects;
-        p.fwd = &cam.fwd;
+        p.fwd = nullptr;
         io[c].objects.clear();
     }
-    const int rc = PassLaunch(run_pass_, gridfast, seed);
+    return PSN_LK_OK;
+}
+
+// Enqueue frame t's device work for every camera: one pass over all cameras
+// (features, backward chains, forward calls of every active tracker). When
+// RunComplete(t-1) has launched frame t's chains already, only the forward
+// calls are enqueued here.
+int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool gridfast, uint32_t seed) {
+    if (!lk_ || io.size() != cams_.size()) return PSN_LK_ERR_ARG;
+    const bool pre = prelaunched_;
+    if (pre) {
+        if (&io != pre_io_ || frameIdx != pre_frame_ || gridfast != pre_gridfast_) {
+            err_ = "RunLaunch: frame " + std::to_string(frameIdx) + " is not the frame launched ahead (" +
+                   std::to_string(pre_frame_) + ")";
+            return PSN_LK_ERR_ARG;
+        }
+        prelaunched_ = false;
+        pre_io_ = nullptr;
+        run_pass_ = std::move(pre_pass_);
+        pre_pass_.clear();
+    } else {
+        const int rc = AdoptFrames(io, gridfast, run_pass_);
+        if (rc) return rc;
+    }
+    run_frame_ = frameIdx;
+    run_gridfast_ = gridfast;
+    for (size_t c = 0; c < cams_.size(); c++) {
+        Cam &cam = cams_[c];
+        cam.trackers.assign(cam.active.begin(), cam.active.end());
+        cam.fwd.clear();
+        ForwardJobs(c, cam.trackers, cam.fstatus, cam.fwd);
+        run_pass_[c].fwd = &cam.fwd;
+    }
+    const int rc = pre ? PassLaunchForward(run_pass_) : PassLaunch(run_pass_, gridfast, seed);
     if (rc) {
         (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
@@ -981,11 +1126,43 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
 // Wait for the frame's device work, then per camera: overlap flags (:824-835),
 // matching costs + majority gate (:906-1022), assignment and tracker update
 // (:1038-1164), result packaging (:1099-1101, :1144-1146).
-int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io) {
-    if (!lk_ || io.size() != cams_.size() || run_pass_.size() != cams_.size()) return PSN_LK_ERR_ARG;
-    const int rc = PassComplete(run_pass_, run_gridfast_);
+int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io) { return RunComplete(io, nullptr, 0, false, 0); }
+
+// With next: frame t+1's features and backward chains (its frames staged) are
+// enqueued as soon as frame t's device work is done, before the host part of
+// frame t, so the GPU runs them while the host matches frame t. Frame t+1's
+// chains read only its detections and the ring, never frame t's trackers, so
+// the results are those of RunLaunch(t+1) after RunComplete(t).
+int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> *next, unsigned nextFrameIdx,
+                               bool nextGridfast, uint32_t nextSeed) {
+    if (!lk_ || io.size() != cams_.size() || run_pass_.size() != cams_.size() || prelaunched_ || &io == next)
+        return PSN_LK_ERR_ARG;
+    // wait; what the next frame's chain launch overwrites is read first, the rest
+    // after that launch (the GPU starts the next chains before the unpacking)
+    int rc = PassWait(run_pass_);
+    if (!rc) rc = PassFeatures(run_pass_, run_gridfast_);
+    if (rc) {
+        run_pass_.clear();
+        return rc;
+    }
+    const bool unpack_first = next && !ChainsFit(*next);  // a regrow frees the result buffers
+    if (!next || unpack_first) PassUnpack(run_pass_);
+    int prc = PSN_LK_OK;
+    if (next) {
+        prc = AdoptFrames(*next, nextGridfast, pre_pass_);
+        if (!prc) prc = PassLaunchChains(pre_pass_, nextGridfast, nextSeed);
+        if (prc) {
+            (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+            pre_pass_.clear();
+        } else {
+            prelaunched_ = true;
+            pre_io_ = next;
+            pre_frame_ = nextFrameIdx;
+            pre_gridfast_ = nextGridfast;
+        }
+        if (!unpack_first) PassUnpack(run_pass_);
+    }
     run_pass_.clear();
-    if (rc) return rc;
     for (size_t c = 0; c < cams_.size(); c++) {
         Cam &cam = cams_[c];
         CamFrame &f = io[c];
@@ -995,7 +1172,7 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io) {
         MatchingAndUpdating(f.objects, cam.active, cam.storage, match, run_frame_, cam.newTrackerID, f.result);
         f.result.camID = cam.camID;
     }
-    return PSN_LK_OK;
+    return prc;
 }
 
 }  // namespace psn

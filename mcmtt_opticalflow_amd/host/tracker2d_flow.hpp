@@ -103,6 +103,13 @@ class Tracker2DFlow {
     // part: matching, tracker update, result packaging.
     int RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool gridfast, uint32_t seed);
     int RunComplete(std::vector<CamFrame> &io);
+    // RunComplete of frame t that launches frame t+1's features and backward
+    // chains (next: its io, detections set; its frames staged) as soon as frame
+    // t's device work is done, before the host part of frame t. The
+    // RunLaunch(nextFrameIdx, *next, nextGridfast, .) that must follow enqueues
+    // only the forward calls. Same results as RunComplete(t) + RunLaunch(t+1).
+    int RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> *next, unsigned nextFrameIdx, bool nextGridfast,
+                    uint32_t nextSeed);
     const std::deque<Tracker2D *> &ActiveTrackers(size_t cam) const { return cams_[cam].active; }
 
     // backward chain steps on the device (default) or on the host (single-camera API)
@@ -146,8 +153,14 @@ class Tracker2DFlow {
         std::vector<Job> *fwd;
         size_t k0, j0, f0;  // first chain / forward job / forward point of this camera in the pass
     };
-    int PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);
-    int PassComplete(std::vector<PassCam> &pc, bool gridfast);
+    int PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);  // chains, then forward
+    int PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);
+    int PassLaunchForward(std::vector<PassCam> &pc);
+    int PassComplete(std::vector<PassCam> &pc, bool gridfast);  // PassWait + PassFeatures + PassUnpack
+    int PassWait(std::vector<PassCam> &pc);
+    int PassFeatures(std::vector<PassCam> &pc, bool gridfast);
+    void PassUnpack(std::vector<PassCam> &pc);
+    bool ChainsFit(const std::vector<CamFrame> &io) const;
 
     int RunJobs(std::vector<Job> &jobs);
     int fail(int rc, const char *what);
@@ -159,7 +172,8 @@ class Tracker2DFlow {
     void BackwardEnd(std::vector<DetectedObject> &out, const std::vector<std::vector<Point2f>> &features);
     int StepsAvailable(size_t cam) const;  // chain steps the camera's ring holds frames for (0..3)
     bool StepAvailable(int step) const { return step <= StepsAvailable(0); }
-    int EnsureDevice(size_t nchains, size_t nfwd_pts, size_t nfwd_jobs);
+    int EnsureChains(size_t nchains);
+    int EnsureForward(size_t nfwd_pts, size_t nfwd_jobs);
     void ForwardJobs(size_t cam, const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
                      std::vector<Job> &jobs);
     void ForwardDone(const std::vector<Tracker2D *> &trackers, std::vector<std::vector<uint8_t>> &status,
@@ -180,7 +194,12 @@ class Tracker2DFlow {
     std::vector<uint8_t> st_out_;
     std::vector<psn_lk_query> queries_;
     std::vector<char> win_bad_;  // per chain of a pass: window the LK cannot run (error only if the chain has points)
+    int AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::vector<PassCam> &pass);
     std::vector<PassCam> run_pass_;  // the pass between RunLaunch and RunComplete
+    std::vector<PassCam> pre_pass_;  // the next frame's pass, chains launched by RunComplete
+    std::vector<CamFrame> *pre_io_ = nullptr;
+    unsigned pre_frame_ = 0;
+    bool pre_gridfast_ = false, prelaunched_ = false;
     unsigned run_frame_ = 0;
     bool run_gridfast_ = false;
     bool device_chain_ = true;

@@ -169,6 +169,8 @@ def load():
     L.psn_t2d_group_launch.argtypes = [vp, ctypes.c_uint, vp, vp, ip, ctypes.c_uint32]
     L.psn_t2d_group_complete.argtypes = [vp, vp, vp, ctypes.POINTER(Track2DResult)]
     L.psn_t2d_group_run.argtypes = [vp, ctypes.c_uint, vp, vp, ip, ctypes.c_uint32, ctypes.POINTER(Track2DResult)]
+    L.psn_t2d_group_complete_next.argtypes = [vp, vp, vp, ctypes.POINTER(Track2DResult), ctypes.c_uint, vp, vp, ip,
+                                              ctypes.c_uint32]
     L.psn_t2d_group_trackers.argtypes = [vp, ip, ctypes.POINTER(Tracker), ip, ctypes.POINTER(ip)]
     _lib = L
     return L
@@ -415,14 +417,46 @@ class Group:
         self._check(self._L.psn_t2d_group_push_frame_device(self._h, cam, ctypes.c_void_p(dev_ptr), stride, channels),
                     "push_frame_device")
 
-    def launch(self, frame_idx: int, dets_per_cam, gridfast: bool = False, seed: int = 0):
-        """dets_per_cam[c]: list of Detection records of camera c (kept alive until complete())."""
+    def _records(self, dets_per_cam):
         arrs = [(Detection * max(len(d), 1))(*d) for d in dets_per_cam]
         ptrs = (ctypes.c_void_p * self.ncams)(*[ctypes.addressof(a) for a in arrs])
         nd = (ctypes.c_int * self.ncams)(*[len(d) for d in dets_per_cam])
-        self._keep = (arrs, ptrs, nd)
+        return arrs, ptrs, nd
+
+    def launch(self, frame_idx: int, dets_per_cam, gridfast: bool = False, seed: int = 0):
+        """dets_per_cam[c]: list of Detection records of camera c (kept alive until complete()).
+        After complete_next(frame_idx, dets_per_cam, ...) the records given there are used
+        (only the forward calls are enqueued here)."""
+        ahead = getattr(self, "_ahead", None)
+        if ahead is not None:
+            arrs, ptrs, nd = ahead
+            assert [nd[c] for c in range(self.ncams)] == [len(d) for d in dets_per_cam]
+        else:
+            arrs, ptrs, nd = self._records(dets_per_cam)
         self._check(self._L.psn_t2d_group_launch(self._h, frame_idx, ptrs, nd, int(bool(gridfast)),
                                                  ctypes.c_uint32(seed & 0xffffffff)), "launch")
+        self._ahead = None
+        self._keep = (arrs, ptrs, nd)
+
+    def complete_next(self, next_frame_idx: int, next_dets_per_cam, gridfast: bool = False, seed: int = 0,
+                      raw: bool = False):
+        """complete() of the current frame that launches frame next_frame_idx's chains ahead
+        (psn_t2d_group_complete_next; that frame's images must be pushed already). The next
+        call must be launch(next_frame_idx, next_dets_per_cam, gridfast, seed)."""
+        arrs, ptrs, nd = self._keep
+        nxt = self._records(next_dets_per_cam)
+        self._check(self._L.psn_t2d_group_complete_next(self._h, ptrs, nd, self._res, next_frame_idx, nxt[1], nxt[2],
+                                                        int(bool(gridfast)), ctypes.c_uint32(seed & 0xffffffff)),
+                    "complete_next")
+        self._keep = None
+        self._ahead = nxt
+        if raw:
+            return None
+        out = []
+        for c in range(self.ncams):
+            self.results[c].r = self._res[c]
+            out.append((list(arrs[c])[:nd[c]], self.results[c].to_dict()))
+        return out
 
     def complete(self):
         """-> (per camera: list of output Detection records, result dict)."""

@@ -68,29 +68,36 @@ def _check_result(g_res, r_res, what):
     assert g_res["detection_rects"] == [] and g_res["tracker_rects"] == []
 
 
+@pytest.mark.parametrize("ahead", [False, True])
 @pytest.mark.parametrize("gridfast", [False, True])
 @pytest.mark.parametrize("W,H,bw,bh", [(640, 480, 32, 80), (960, 540, 64, 160)])
-def test_group_run_matches_oracle(oracle_mod, gridfast, W, H, bw, bh):
+def test_group_run_matches_oracle(oracle_mod, gridfast, W, H, bw, bh, ahead):
+    """ahead: frame t+1's chains are launched by complete_next(t) before the host
+    matches frame t (the pipelined driver of the bench)."""
     C, T = 3, 7
     scenes = [synth.make_scene(40 + c, W, H, 120, nboxes=3, box_w=bw, box_h=bh, max_speed=3.0) for c in range(C)]
     refs = [ORC.CameraTracker(cam_id=10 + c) for c in range(C)]
     rngs = [np.random.default_rng(500 + c) for c in range(C)]
     grays = [[sc.frame(t) for t in range(T)] for sc in scenes]
     bgrs = [[_bgr(grays[c][t], 100 * c + t) for t in range(T)] for c in range(C)]
+    per_frame = [[_camera_dets(scenes[c], t, rngs[c], tiny=(c == 0)) for c in range(C)] for t in range(T)]
+    g_frames = [[[t2d.make_detection(b, np.zeros((0, 2), np.float32) if gridfast else f, head=e[0],
+                                     location=e[1], height=e[2]) for b, e, f in zip(*per_frame[t][c])]
+                 for c in range(C)] for t in range(T)]
     n_obj = n_matched = 0
     with t2d.Group(W, H, [10 + c for c in range(C)]) as g:
         for c in range(C):  # camera 1 ingests BGR, the others gray
             g.push_frame(c, bgrs[c][0] if c == 1 else grays[c][0])
         for t in range(T):
-            per_cam = [_camera_dets(scenes[c], t, rngs[c], tiny=(c == 0)) for c in range(C)]
-            g_dets = [[t2d.make_detection(b, np.zeros((0, 2), np.float32) if gridfast else f, head=e[0],
-                                          location=e[1], height=e[2]) for b, e, f in zip(*per_cam[c])]
-                      for c in range(C)]
-            g.launch(t, g_dets, gridfast=gridfast, seed=t)
+            per_cam = per_frame[t]
+            g.launch(t, g_frames[t], gridfast=gridfast, seed=t)
             if t + 1 < T:  # frame t+1 is uploaded while frame t runs
                 for c in range(C):
                     g.push_frame(c, bgrs[c][t + 1] if c == 1 else grays[c][t + 1])
-            out = g.complete()
+            if ahead and t + 1 < T:
+                out = g.complete_next(t + 1, g_frames[t + 1], gridfast=gridfast, seed=t + 1)
+            else:
+                out = g.complete()
             for c in range(C):
                 gray = oracle_mod.bgr2gray(bgrs[c][t]) if c == 1 else grays[c][t]
                 boxes, extra, feats = per_cam[c]
@@ -116,6 +123,22 @@ def test_group_run_matches_oracle(oracle_mod, gridfast, W, H, bw, bh):
                 n_obj += len(g_res["objects"])
                 n_matched += sum(1 for x in refs[c].active if x.duration > 1)
     assert n_obj > 20 and n_matched > 5  # the sequence creates and continues trackers
+
+
+def test_group_ahead_protocol():
+    """complete_next must be followed by the launch of the frame it announced."""
+    W, H = 160, 120
+    img = synth.texture(W, H, 3)
+    d = [[t2d.make_detection((10, 10, 30, 60), np.float32([[20, 20], [25, 30], [30, 40], [22, 50]]))]]
+    with t2d.Group(W, H, [0]) as g:
+        g.push_frame(0, img)
+        g.launch(0, d)
+        g.push_frame(0, img)
+        g.complete_next(1, d)
+        with pytest.raises(t2d.T2dError):
+            g.launch(2, d)  # not the announced frame
+        g.launch(1, d)
+        g.complete()
 
 
 def test_group_window_errors():
