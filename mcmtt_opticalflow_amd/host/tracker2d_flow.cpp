@@ -139,6 +139,14 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
         return PSN_LK_ERR_HIP;
     }
     chain_stream_ = cs;
+    hipEvent_t e1 = nullptr, e2 = nullptr;
+    if (hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e2, hipEventDisableTiming) != hipSuccess) {
+        err_ = "result events";
+        return PSN_LK_ERR_HIP;
+    }
+    ev_chain_ = e1;
+    ev_fwd_ = e2;
     return psn_lk_set_stream(lk_, cs);
 }
 
@@ -158,12 +166,19 @@ struct Tracker2DFlow::DeviceBuffers {
     float *d_fin = nullptr, *d_fout = nullptr, *d_ferr = nullptr;
     uint8_t *d_fstatus = nullptr;
     int *d_fcnt = nullptr;
-    // pinned staging: inputs, then results
-    float *h_in = nullptr, *h_fin = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
+    // pinned staging of the chain inputs (and GridFAST features), two sets: a
+    // pass's set is written by its launch and read back by its completion, and
+    // the next frame's chains may be launched in between (RunComplete with next)
+    struct Stage {
+        float *h_in = nullptr;
+        double *h_boxes = nullptr;
+        int *h_cnt = nullptr, *h_rawcnt = nullptr, *h_last = nullptr;
+    } stage[2];
+    // pinned staging: forward inputs, then results
+    float *h_fin = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
     uint8_t *h_fwd_st = nullptr;
-    double *h_boxes = nullptr, *h_obox = nullptr;
-    int *h_cnt = nullptr, *h_fcnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr, *h_rawcnt = nullptr,
-        *h_last = nullptr;
+    double *h_obox = nullptr;
+    int *h_fcnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr;
     // the chain's results live in one block per side, [nsteps | set counts | boxes | sets], so that
     // one memset clears the counters and one copy returns every used byte
     char *d_res = nullptr, *h_res = nullptr;
@@ -182,17 +197,20 @@ struct Tracker2DFlow::DeviceBuffers {
             if (p) (void)hipHostFree(p);
     }
     void release_chains() {
-        free_all({d_in, d_out, d_buf[0], d_buf[1], d_err, d_status, d_boxes, d_res, d_cnt, d_tot, d_last},
-                 {h_in, h_boxes, h_res, h_cnt, h_rawcnt, h_last});
+        free_all({d_in, d_out, d_buf[0], d_buf[1], d_err, d_status, d_boxes, d_res, d_cnt, d_tot, d_last}, {h_res});
+        for (Stage &g : stage) {
+            free_all({}, {g.h_in, g.h_boxes, g.h_cnt, g.h_rawcnt, g.h_last});
+            g = Stage();
+        }
         d_in = d_out = d_buf[0] = d_buf[1] = d_err = d_sets = nullptr;
         d_status = nullptr;
         d_boxes = d_obox = nullptr;
         d_res = nullptr;
         d_cnt = d_setcnt = d_nsteps = d_tot = d_last = nullptr;
-        h_in = h_sets = nullptr;
-        h_boxes = h_obox = nullptr;
+        h_sets = nullptr;
+        h_obox = nullptr;
         h_res = nullptr;
-        h_cnt = h_setcnt = h_nsteps = h_rawcnt = h_last = nullptr;
+        h_setcnt = h_nsteps = nullptr;
         nchains = 0;
     }
     void release_forward() {
@@ -230,6 +248,12 @@ void Tracker2DFlow::Finalize() {
         (void)hipStreamDestroy((hipStream_t)chain_stream_);
         chain_stream_ = nullptr;
     }
+    for (void **e : {&ev_chain_, &ev_fwd_})
+        if (*e) {
+            (void)hipEventDestroy((hipEvent_t)*e);
+            *e = nullptr;
+        }
+    wait_chain_ = wait_fwd_ = false;
     cams_.clear();
 }
 
@@ -259,12 +283,14 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
     dm((void **)&b.d_cnt, K * 4);
     dm((void **)&b.d_tot, K * 4);
     dm((void **)&b.d_last, K * 4);
-    hm((void **)&b.h_in, npt * 8);
-    hm((void **)&b.h_boxes, K * 4 * 8);
     hm((void **)&b.h_res, res_bytes);
-    hm((void **)&b.h_cnt, K * 4);
-    hm((void **)&b.h_rawcnt, K * 4);
-    hm((void **)&b.h_last, K * 4);
+    for (DeviceBuffers::Stage &g : b.stage) {
+        hm((void **)&g.h_in, npt * 8);
+        hm((void **)&g.h_boxes, K * 4 * 8);
+        hm((void **)&g.h_cnt, K * 4);
+        hm((void **)&g.h_rawcnt, K * 4);
+        hm((void **)&g.h_last, K * 4);
+    }
     if (!ok) {
         b.release_chains();
         err_ = "chain buffers: allocation failed";
@@ -347,11 +373,16 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
         p.k0 = K;
         K += p.dets->size();
     }
+    const int si = stage_;  // this pass's staging set
+    stage_ ^= 1;
+    for (PassCam &p : pc) p.set = si;
+    std::vector<char> &win_bad_ = win_bad_sets_[si];
     win_bad_.assign(K, 0);
     if (K == 0) return PSN_LK_OK;
     int rc = EnsureChains(K);
     if (rc) return rc;
-    DeviceBuffers &b = *dev_;
+    DeviceBuffers::Stage &b = dev_->stage[si];
+    DeviceBuffers &db = *dev_;
     hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_);
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !rc) {
@@ -393,11 +424,11 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
                     rois[4 * i + 3] = (int)r.h;
                 }
                 rc = psn_gridfast_detect_device(lk_, cams_[p.cam].ring[kT2dInterval - 1], rois.data(), (int)n, &gp, seed,
-                                                b.d_in + 2 * cap * p.k0, b.d_cnt + p.k0, b.d_tot + p.k0);
+                                                db.d_in + 2 * cap * p.k0, db.d_cnt + p.k0, db.d_tot + p.k0);
                 if (rc) return fail(rc, "psn_gridfast_detect_device");
             }
-            chk(hipMemcpyAsync(b.h_rawcnt, b.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
-            chk(hipMemcpyAsync(b.h_in, b.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
+            chk(hipMemcpyAsync(b.h_rawcnt, db.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
+            chk(hipMemcpyAsync(b.h_in, db.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
         } else {
             for (PassCam &p : pc)
                 for (size_t i = 0; i < p.dets->size(); i++) {
@@ -415,24 +446,24 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
                     b.h_cnt[k] = (int)n;
                 }
             // whole rows: a chain row's unused tail is never read (counts)
-            chk(hipMemcpyAsync(b.d_in, b.h_in, K * cap * 8, hipMemcpyHostToDevice, st), "chain inputs");
-            chk(hipMemcpyAsync(b.d_cnt, b.h_cnt, K * 4, hipMemcpyHostToDevice, st), "chain counts");
+            chk(hipMemcpyAsync(db.d_in, b.h_in, K * cap * 8, hipMemcpyHostToDevice, st), "chain inputs");
+            chk(hipMemcpyAsync(db.d_cnt, b.h_cnt, K * 4, hipMemcpyHostToDevice, st), "chain counts");
         }
-        chk(hipMemcpyAsync(b.d_last, b.h_last, K * 4, hipMemcpyHostToDevice, st), "chain last steps");
-        if (!rc) rc = psn_t2d_gate_counts_device(b.d_cnt, (int)K, (int)kT2dMinFeatures, b.d_last, st);
-        chk(hipMemcpyAsync(b.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
-        chk(hipMemsetAsync(b.d_nsteps, 0, b.nchains * (1 + S) * 4, st), "chain steps and set counts");
+        chk(hipMemcpyAsync(db.d_last, b.h_last, K * 4, hipMemcpyHostToDevice, st), "chain last steps");
+        if (!rc) rc = psn_t2d_gate_counts_device(db.d_cnt, (int)K, (int)kT2dMinFeatures, db.d_last, st);
+        chk(hipMemcpyAsync(db.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
+        chk(hipMemsetAsync(db.d_nsteps, 0, db.nchains * (1 + S) * 4, st), "chain steps and set counts");
         if (rc) return rc;
         psn_t2d_chain_dev cd{};
         cd.ndet = (int)K;
         cd.cap = (int)cap;
-        cd.boxes = b.d_boxes;
-        cd.cnt = b.d_cnt;
-        cd.out_boxes = b.d_obox;
-        cd.sets = b.d_sets;
-        cd.set_cnt = b.d_setcnt;
-        cd.nsteps = b.d_nsteps;
-        cd.last_step = b.d_last;
+        cd.boxes = db.d_boxes;
+        cd.cnt = db.d_cnt;
+        cd.out_boxes = db.d_obox;
+        cd.sets = db.d_sets;
+        cd.set_cnt = db.d_setcnt;
+        cd.nsteps = db.d_nsteps;
+        cd.last_step = db.d_last;
         for (int step = 1; step <= max_steps; step++) {
             queries_.clear();
             for (PassCam &p : pc) {
@@ -453,12 +484,12 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
                     queries_.push_back(q);
                 }
             }
-            const float *in = step == 1 ? b.d_in : b.d_buf[step & 1];
-            rc = psn_lk_track_device_counted(lk_, queries_.data(), (int)K, b.d_cnt, in, b.d_out, b.d_status, b.d_err);
+            const float *in = step == 1 ? db.d_in : db.d_buf[step & 1];
+            rc = psn_lk_track_device_counted(lk_, queries_.data(), (int)K, db.d_cnt, in, db.d_out, db.d_status, db.d_err);
             if (rc) return fail(rc, "psn_lk_track_device_counted");
             cd.cur = in;
-            cd.nxt = b.d_out;
-            cd.next_in = b.d_buf[(step + 1) & 1];
+            cd.nxt = db.d_out;
+            cd.next_in = db.d_buf[(step + 1) & 1];
             rc = psn_t2d_chain_step_device(&cd, step, st);
             if (rc) return fail(rc, "psn_t2d_chain_step_device");
         }
@@ -537,6 +568,11 @@ int Tracker2DFlow::PassComplete(std::vector<PassCam> &pc, bool gridfast) {
 
 // Enqueue the result copies and wait for the pass's device work.
 int Tracker2DFlow::PassWait(std::vector<PassCam> &pc) {
+    const int rc = PassCopy(pc);
+    return rc ? rc : PassSync();
+}
+
+int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
     int rc = PSN_LK_OK;
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !rc) {
@@ -560,17 +596,37 @@ int Tracker2DFlow::PassWait(std::vector<PassCam> &pc) {
         chk(hipMemcpyAsync(bp->h_fwd_out, bp->d_fout, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
         chk(hipMemcpyAsync(bp->h_fwd_st, bp->d_fstatus, F, hipMemcpyDeviceToHost, fs), "forward status");
     }
-    chk(hipStreamSynchronize(st), "chain sync");
-    chk(hipStreamSynchronize(fs), "forward sync");
+    // everything the pass enqueued on either stream precedes these records
+    chk(hipEventRecord((hipEvent_t)ev_chain_, st), "chain results event");
+    chk(hipEventRecord((hipEvent_t)ev_fwd_, fs), "forward results event");
+    wait_chain_ = wait_fwd_ = rc == PSN_LK_OK;
     return rc;
 }
 
-// After PassWait: what the next pass's chain launch overwrites (the chain
-// input staging h_in / h_rawcnt, win_bad_): GridFAST features, window errors.
+// Spin on the completion events (a blocking stream sync sleeps and wakes
+// ~0.1 ms late; the next frame's work is enqueued right after this returns).
+int Tracker2DFlow::PassSync() {
+    for (int i = 0; i < 2; i++) {
+        bool &w = i ? wait_fwd_ : wait_chain_;
+        if (!w) continue;
+        hipEvent_t e = (hipEvent_t)(i ? ev_fwd_ : ev_chain_);
+        hipError_t q;
+        while ((q = hipEventQuery(e)) == hipErrorNotReady) __builtin_ia32_pause();
+        w = false;
+        if (q != hipSuccess) {
+            err_ = std::string(i ? "forward" : "chain") + " sync: " + hipGetErrorString(q);
+            return PSN_LK_ERR_HIP;
+        }
+    }
+    return PSN_LK_OK;
+}
+
+// After PassWait: GridFAST features (the pass's staging set) and window errors.
 int Tracker2DFlow::PassFeatures(std::vector<PassCam> &pc, bool gridfast) {
-    if (!gridfast) return PSN_LK_OK;
+    if (!gridfast || pc.empty() || !dev_) return PSN_LK_OK;
     const size_t cap = PSN_T2D_CHAIN_CAP;
-    DeviceBuffers *bp = dev_;
+    const DeviceBuffers::Stage *bp = &dev_->stage[pc[0].set];
+    const std::vector<char> &win_bad_ = win_bad_sets_[pc[0].set];
     for (PassCam &p : pc) {
         const size_t n = p.dets->size();
         p.features->assign(n, {});
@@ -1137,18 +1193,15 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
                                bool nextGridfast, uint32_t nextSeed) {
     if (!lk_ || io.size() != cams_.size() || run_pass_.size() != cams_.size() || prelaunched_ || &io == next)
         return PSN_LK_ERR_ARG;
-    // wait; what the next frame's chain launch overwrites is read first, the rest
-    // after that launch (the GPU starts the next chains before the unpacking)
-    int rc = PassWait(run_pass_);
-    if (!rc) rc = PassFeatures(run_pass_, run_gridfast_);
-    if (rc) {
-        run_pass_.clear();
-        return rc;
-    }
-    const bool unpack_first = next && !ChainsFit(*next);  // a regrow frees the result buffers
-    if (!next || unpack_first) PassUnpack(run_pass_);
+    // The next frame's chains are enqueued right behind this frame's result copies
+    // (stream order keeps them from overwriting what is copied; their inputs go
+    // through the other staging set), then this frame is waited for and
+    // unpacked while they run. If they need larger chain buffers, the regrow
+    // waits, so this frame is unpacked first.
+    int rc = PassCopy(run_pass_);
+    const bool early = !rc && next && ChainsFit(*next);
     int prc = PSN_LK_OK;
-    if (next) {
+    auto prelaunch = [&]() {
         prc = AdoptFrames(*next, nextGridfast, pre_pass_);
         if (!prc) prc = PassLaunchChains(pre_pass_, nextGridfast, nextSeed);
         if (prc) {
@@ -1160,9 +1213,17 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
             pre_frame_ = nextFrameIdx;
             pre_gridfast_ = nextGridfast;
         }
-        if (!unpack_first) PassUnpack(run_pass_);
+    };
+    if (early) prelaunch();
+    if (!rc) rc = PassSync();
+    if (!rc) rc = PassFeatures(run_pass_, run_gridfast_);
+    if (rc) {
+        run_pass_.clear();
+        return rc;
     }
+    PassUnpack(run_pass_);
     run_pass_.clear();
+    if (next && !early) prelaunch();
     for (size_t c = 0; c < cams_.size(); c++) {
         Cam &cam = cams_[c];
         CamFrame &f = io[c];

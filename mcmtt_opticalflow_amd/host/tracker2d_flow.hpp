@@ -152,12 +152,15 @@ class Tracker2DFlow {
         std::vector<DetectedObject> *out;
         std::vector<Job> *fwd;
         size_t k0, j0, f0;  // first chain / forward job / forward point of this camera in the pass
+        int set;            // the pass's staging set of chain inputs
     };
     int PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);  // chains, then forward
     int PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);
     int PassLaunchForward(std::vector<PassCam> &pc);
     int PassComplete(std::vector<PassCam> &pc, bool gridfast);  // PassWait + PassFeatures + PassUnpack
-    int PassWait(std::vector<PassCam> &pc);
+    int PassWait(std::vector<PassCam> &pc);  // PassCopy + PassSync
+    int PassCopy(std::vector<PassCam> &pc);  // enqueue the result copies, record the completion events
+    int PassSync();                          // wait for them
     int PassFeatures(std::vector<PassCam> &pc, bool gridfast);
     void PassUnpack(std::vector<PassCam> &pc);
     bool ChainsFit(const std::vector<CamFrame> &io) const;
@@ -193,7 +196,11 @@ class Tracker2DFlow {
     std::vector<float> xy_in_, xy_out_, err_out_, gf_xy_;
     std::vector<uint8_t> st_out_;
     std::vector<psn_lk_query> queries_;
-    std::vector<char> win_bad_;  // per chain of a pass: window the LK cannot run (error only if the chain has points)
+    // per chain of a pass (per staging set): window the LK cannot run (error only if the chain has points)
+    std::vector<char> win_bad_sets_[2];
+    int stage_ = 0;  // staging set of the next chain launch
+    void *ev_chain_ = nullptr, *ev_fwd_ = nullptr;  // hipEvent_t: a pass's result copies done
+    bool wait_chain_ = false, wait_fwd_ = false;
     int AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::vector<PassCam> &pass);
     std::vector<PassCam> run_pass_;  // the pass between RunLaunch and RunComplete
     std::vector<PassCam> pre_pass_;  // the next frame's pass, chains launched by RunComplete
