@@ -262,7 +262,7 @@ def tracker_main(args):
     T = t2d.load()
 
     def step(t, dets, next_dets):
-        group.launch(t, dets)  # after complete_next(t-1): frame t's forward calls only
+        group.launch(t, dets)  # after complete_next(t-1): a confirmation (frame t is in flight)
         for k, fd in enumerate(feeds):  # frame t+1 uploads while frame t runs
             fd.push(group, k, t + 1)
         if next_dets is None:
@@ -286,7 +286,7 @@ def tracker_main(args):
     # ahead, as the warm-up's last step did for the first timed frame (the timed region holds exactly
     # `steps` frames' backward chains and forward calls)
     dets_timed = [all_dets(args.warmup + i) for i in range(args.steps + 1)]
-    seq = dets_warm + dets_timed
+    seq = [group.records(d) for d in dets_warm + dets_timed]  # ctypes records, built before timing
     for i in range(args.warmup):
         step(t, seq[i], seq[i + 1] if i + 1 < len(seq) else None)
         t += 1

@@ -249,20 +249,26 @@ int psn_t2d_group_complete(psn_t2d_group *g, psn_t2d_detection *const *dets, con
                            psn_track2d_result *results);
 int psn_t2d_group_run(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *const *dets, const int *ndet,
                       int feature_mode, uint32_t seed, psn_track2d_result *results);
-/* psn_t2d_group_complete of frame t that also launches frame t+1 ahead: as soon
- * as frame t's device work is done, frame t+1's features (next_dets, feature_mode,
+/* psn_t2d_group_complete of frame t that also launches frame t+1: as soon as
+ * frame t's device work is done, frame t+1's features (next_dets, feature_mode,
  * seed) and backward chains are enqueued, and the GPU runs them while the host
  * matches frame t (the chains read only frame t+1's detections and the image
- * ring, never frame t's trackers: results are those of complete(t) + launch(t+1)).
- * Frame t+1 of every camera must be staged (push_frame) before this call; the
- * next call must be psn_t2d_group_launch(g, next_frame_idx, next_dets, next_ndet,
- * feature_mode, .), which then enqueues only the forward calls, and next_dets
- * must stay valid until that frame's complete. A pipelined driver:
+ * ring, never frame t's trackers); frame t+1's forward calls follow frame t's
+ * tracker update. Results are those of complete(t) + launch(t+1). Frame t+1 of
+ * every camera must be staged (push_frame) before this call; the next call must
+ * be psn_t2d_group_launch(g, next_frame_idx, next_dets, next_ndet, feature_mode,
+ * .), which then only confirms the frame, and next_dets must stay valid until
+ * that frame's complete. A pipelined driver:
  *   launch(0); push(1); complete_next(0 -> 1); launch(1); push(2); complete_next(1 -> 2); ... */
 int psn_t2d_group_complete_next(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,
                                 psn_track2d_result *results, unsigned next_frame_idx,
                                 psn_t2d_detection *const *next_dets, const int *next_ndet, int feature_mode,
                                 uint32_t seed);
+/* diagnostic: host microseconds accumulated since the last call from the entry
+ * of each complete to its phases (result copies + next chains enqueued, device
+ * work done, unpacked, matched and updated, next forward calls enqueued), and
+ * out6[5] = the number of completes */
+int psn_t2d_group_debug_host_times(psn_t2d_group *g, double *out6);
 /* camera c's active trackers (m_queueActiveTracker2D) after the last complete */
 int psn_t2d_group_trackers(psn_t2d_group *g, int cam, psn_t2d_tracker *out, int cap, int *n);
 

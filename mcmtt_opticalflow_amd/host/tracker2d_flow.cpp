@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -1142,35 +1143,26 @@ int Tracker2DFlow::AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::ve
 
 // Enqueue frame t's device work for every camera: one pass over all cameras
 // (features, backward chains, forward calls of every active tracker). When
-// RunComplete(t-1) has launched frame t's chains already, only the forward
-// calls are enqueued here.
+// RunComplete(t-1, next = frame t) has launched frame t already, this only
+// confirms it.
 int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool gridfast, uint32_t seed) {
     if (!lk_ || io.size() != cams_.size()) return PSN_LK_ERR_ARG;
-    const bool pre = prelaunched_;
-    if (pre) {
-        if (&io != pre_io_ || frameIdx != pre_frame_ || gridfast != pre_gridfast_) {
+    if (launched_ahead_) {
+        if (&io != pre_io_ || frameIdx != run_frame_ || gridfast != run_gridfast_) {
             err_ = "RunLaunch: frame " + std::to_string(frameIdx) + " is not the frame launched ahead (" +
-                   std::to_string(pre_frame_) + ")";
+                   std::to_string(run_frame_) + ")";
             return PSN_LK_ERR_ARG;
         }
-        prelaunched_ = false;
+        launched_ahead_ = false;
         pre_io_ = nullptr;
-        run_pass_ = std::move(pre_pass_);
-        pre_pass_.clear();
-    } else {
-        const int rc = AdoptFrames(io, gridfast, run_pass_);
-        if (rc) return rc;
+        return PSN_LK_OK;
     }
+    int rc = AdoptFrames(io, gridfast, run_pass_);
+    if (rc) return rc;
     run_frame_ = frameIdx;
     run_gridfast_ = gridfast;
-    for (size_t c = 0; c < cams_.size(); c++) {
-        Cam &cam = cams_[c];
-        cam.trackers.assign(cam.active.begin(), cam.active.end());
-        cam.fwd.clear();
-        ForwardJobs(c, cam.trackers, cam.fstatus, cam.fwd);
-        run_pass_[c].fwd = &cam.fwd;
-    }
-    const int rc = pre ? PassLaunchForward(run_pass_) : PassLaunch(run_pass_, gridfast, seed);
+    AttachForward(run_pass_);
+    rc = PassLaunch(run_pass_, gridfast, seed);
     if (rc) {
         (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
@@ -1179,43 +1171,57 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
     return rc;
 }
 
+// the forward calls of every camera's active trackers (m_queueActiveTracker2D
+// after the previous frame's update) into the pass
+void Tracker2DFlow::AttachForward(std::vector<PassCam> &pass) {
+    for (size_t c = 0; c < cams_.size(); c++) {
+        Cam &cam = cams_[c];
+        cam.trackers.assign(cam.active.begin(), cam.active.end());
+        cam.fwd.clear();
+        ForwardJobs(c, cam.trackers, cam.fstatus, cam.fwd);
+        pass[c].fwd = &cam.fwd;
+    }
+}
+
 // Wait for the frame's device work, then per camera: overlap flags (:824-835),
 // matching costs + majority gate (:906-1022), assignment and tracker update
 // (:1038-1164), result packaging (:1099-1101, :1144-1146).
 int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io) { return RunComplete(io, nullptr, 0, false, 0); }
 
-// With next: frame t+1's features and backward chains (its frames staged) are
-// enqueued as soon as frame t's device work is done, before the host part of
-// frame t, so the GPU runs them while the host matches frame t. Frame t+1's
+// With next: frame t+1 is launched from here. Its features and backward chains
+// (its frames staged) are enqueued as soon as frame t's device work is done,
+// before the host part of frame t, so the GPU runs them while the host matches
+// frame t; its forward calls follow frame t's tracker update. Frame t+1's
 // chains read only its detections and the ring, never frame t's trackers, so
 // the results are those of RunLaunch(t+1) after RunComplete(t).
 int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> *next, unsigned nextFrameIdx,
                                bool nextGridfast, uint32_t nextSeed) {
-    if (!lk_ || io.size() != cams_.size() || run_pass_.size() != cams_.size() || prelaunched_ || &io == next)
+    if (!lk_ || io.size() != cams_.size() || run_pass_.size() != cams_.size() || launched_ahead_ || &io == next)
         return PSN_LK_ERR_ARG;
     // The next frame's chains are enqueued right behind this frame's result copies
     // (stream order keeps them from overwriting what is copied; their inputs go
     // through the other staging set), then this frame is waited for and
     // unpacked while they run. If they need larger chain buffers, the regrow
     // waits, so this frame is unpacked first.
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t0 = clk::now();
+    auto stamp = [&](int i) { host_us_[i] += std::chrono::duration<double, std::micro>(clk::now() - t0).count(); };
     int rc = PassCopy(run_pass_);
     const bool early = !rc && next && ChainsFit(*next);
     int prc = PSN_LK_OK;
+    std::vector<PassCam> pre;
     auto prelaunch = [&]() {
-        prc = AdoptFrames(*next, nextGridfast, pre_pass_);
-        if (!prc) prc = PassLaunchChains(pre_pass_, nextGridfast, nextSeed);
+        prc = AdoptFrames(*next, nextGridfast, pre);
+        if (!prc) prc = PassLaunchChains(pre, nextGridfast, nextSeed);
         if (prc) {
             (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
-            pre_pass_.clear();
-        } else {
-            prelaunched_ = true;
-            pre_io_ = next;
-            pre_frame_ = nextFrameIdx;
-            pre_gridfast_ = nextGridfast;
+            pre.clear();
         }
     };
     if (early) prelaunch();
+    stamp(0);  // copies + next chains enqueued
     if (!rc) rc = PassSync();
+    stamp(1);  // device work done
     if (!rc) rc = PassFeatures(run_pass_, run_gridfast_);
     if (rc) {
         run_pass_.clear();
@@ -1224,6 +1230,7 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     PassUnpack(run_pass_);
     run_pass_.clear();
     if (next && !early) prelaunch();
+    stamp(2);  // unpacked
     for (size_t c = 0; c < cams_.size(); c++) {
         Cam &cam = cams_[c];
         CamFrame &f = io[c];
@@ -1233,7 +1240,24 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
         MatchingAndUpdating(f.objects, cam.active, cam.storage, match, run_frame_, cam.newTrackerID, f.result);
         f.result.camID = cam.camID;
     }
-    return prc;
+    stamp(3);  // matched, trackers updated
+    host_calls_++;
+    if (!next || prc) return prc;
+    // frame t+1's forward calls: the trackers as frame t's update left them
+    AttachForward(pre);
+    prc = PassLaunchForward(pre);
+    stamp(4);  // next forward enqueued
+    if (prc) {
+        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        return prc;
+    }
+    run_pass_ = std::move(pre);
+    run_frame_ = nextFrameIdx;
+    run_gridfast_ = nextGridfast;
+    pre_io_ = next;
+    launched_ahead_ = true;
+    return PSN_LK_OK;
 }
 
 }  // namespace psn

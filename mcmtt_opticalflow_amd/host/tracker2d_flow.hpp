@@ -103,14 +103,23 @@ class Tracker2DFlow {
     // part: matching, tracker update, result packaging.
     int RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool gridfast, uint32_t seed);
     int RunComplete(std::vector<CamFrame> &io);
-    // RunComplete of frame t that launches frame t+1's features and backward
-    // chains (next: its io, detections set; its frames staged) as soon as frame
-    // t's device work is done, before the host part of frame t. The
-    // RunLaunch(nextFrameIdx, *next, nextGridfast, .) that must follow enqueues
-    // only the forward calls. Same results as RunComplete(t) + RunLaunch(t+1).
+    // RunComplete of frame t that launches frame t+1 (next: its io, detections
+    // set; its frames staged): its features and backward chains as soon as frame
+    // t's device work is done, before the host part of frame t, its forward
+    // calls after frame t's tracker update. The RunLaunch(nextFrameIdx, *next,
+    // nextGridfast, .) that must follow only confirms it. Same results as
+    // RunComplete(t) + RunLaunch(t+1).
     int RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> *next, unsigned nextFrameIdx, bool nextGridfast,
                     uint32_t nextSeed);
     const std::deque<Tracker2D *> &ActiveTrackers(size_t cam) const { return cams_[cam].active; }
+    // diagnostic: accumulated host microseconds from RunComplete's entry to its
+    // phases (copies + next chains enqueued, device done, unpacked, matched, next
+    // forward enqueued) and the number of RunComplete calls; reset on read
+    void HostTimes(double out[6]) {
+        for (int i = 0; i < 5; i++) out[i] = host_us_[i], host_us_[i] = 0;
+        out[5] = host_calls_;
+        host_calls_ = 0;
+    }
 
     // backward chain steps on the device (default) or on the host (single-camera API)
     void SetDeviceChain(bool on) { device_chain_ = on; }
@@ -203,10 +212,11 @@ class Tracker2DFlow {
     bool wait_chain_ = false, wait_fwd_ = false;
     int AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::vector<PassCam> &pass);
     std::vector<PassCam> run_pass_;  // the pass between RunLaunch and RunComplete
-    std::vector<PassCam> pre_pass_;  // the next frame's pass, chains launched by RunComplete
-    std::vector<CamFrame> *pre_io_ = nullptr;
-    unsigned pre_frame_ = 0;
-    bool pre_gridfast_ = false, prelaunched_ = false;
+    void AttachForward(std::vector<PassCam> &pass);
+    std::vector<CamFrame> *pre_io_ = nullptr;  // the io of a frame RunComplete launched ahead
+    bool launched_ahead_ = false;              // run_pass_ is that frame, awaiting its RunLaunch
+    double host_us_[5] = {0, 0, 0, 0, 0};
+    long host_calls_ = 0;
     unsigned run_frame_ = 0;
     bool run_gridfast_ = false;
     bool device_chain_ = true;

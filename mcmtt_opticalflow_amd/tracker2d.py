@@ -172,6 +172,7 @@ def load():
     L.psn_t2d_group_complete_next.argtypes = [vp, vp, vp, ctypes.POINTER(Track2DResult), ctypes.c_uint, vp, vp, ip,
                                               ctypes.c_uint32]
     L.psn_t2d_group_trackers.argtypes = [vp, ip, ctypes.POINTER(Tracker), ip, ctypes.POINTER(ip)]
+    L.psn_t2d_group_debug_host_times.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
     _lib = L
     return L
 
@@ -417,7 +418,11 @@ class Group:
         self._check(self._L.psn_t2d_group_push_frame_device(self._h, cam, ctypes.c_void_p(dev_ptr), stride, channels),
                     "push_frame_device")
 
-    def _records(self, dets_per_cam):
+    def records(self, dets_per_cam):
+        """The ctypes records of one frame's detections (launch / complete_next accept them
+        in place of the lists: a driver can build them outside its timed loop)."""
+        if isinstance(dets_per_cam, tuple):
+            return dets_per_cam
         arrs = [(Detection * max(len(d), 1))(*d) for d in dets_per_cam]
         ptrs = (ctypes.c_void_p * self.ncams)(*[ctypes.addressof(a) for a in arrs])
         nd = (ctypes.c_int * self.ncams)(*[len(d) for d in dets_per_cam])
@@ -430,9 +435,8 @@ class Group:
         ahead = getattr(self, "_ahead", None)
         if ahead is not None:
             arrs, ptrs, nd = ahead
-            assert [nd[c] for c in range(self.ncams)] == [len(d) for d in dets_per_cam]
         else:
-            arrs, ptrs, nd = self._records(dets_per_cam)
+            arrs, ptrs, nd = self.records(dets_per_cam)
         self._check(self._L.psn_t2d_group_launch(self._h, frame_idx, ptrs, nd, int(bool(gridfast)),
                                                  ctypes.c_uint32(seed & 0xffffffff)), "launch")
         self._ahead = None
@@ -440,11 +444,12 @@ class Group:
 
     def complete_next(self, next_frame_idx: int, next_dets_per_cam, gridfast: bool = False, seed: int = 0,
                       raw: bool = False):
-        """complete() of the current frame that launches frame next_frame_idx's chains ahead
+        """complete() of the current frame that launches frame next_frame_idx
         (psn_t2d_group_complete_next; that frame's images must be pushed already). The next
-        call must be launch(next_frame_idx, next_dets_per_cam, gridfast, seed)."""
+        call must be launch(next_frame_idx, next_dets_per_cam, gridfast, seed), which only
+        confirms it."""
         arrs, ptrs, nd = self._keep
-        nxt = self._records(next_dets_per_cam)
+        nxt = self.records(next_dets_per_cam)
         self._check(self._L.psn_t2d_group_complete_next(self._h, ptrs, nd, self._res, next_frame_idx, nxt[1], nxt[2],
                                                         int(bool(gridfast)), ctypes.c_uint32(seed & 0xffffffff)),
                     "complete_next")
@@ -481,6 +486,15 @@ class Group:
     def run(self, frame_idx: int, dets_per_cam, gridfast: bool = False, seed: int = 0):
         self.launch(frame_idx, dets_per_cam, gridfast, seed)
         return self.complete()
+
+    def debug_host_times(self):
+        """Mean host microseconds from the entry of complete to its phases since the last call
+        (psn_t2d_group_debug_host_times)."""
+        out = (ctypes.c_double * 6)()
+        self._check(self._L.psn_t2d_group_debug_host_times(self._h, out), "debug_host_times")
+        n = max(out[5], 1.0)
+        keys = ["next_chains_enqueued", "device_done", "unpacked", "matched", "next_forward_enqueued"]
+        return {k: round(out[i] / n, 1) for i, k in enumerate(keys)} | {"completes": int(out[5])}
 
     def trackers(self, cam: int, cap: int = 256) -> list[Tracker]:
         out = (Tracker * cap)()

@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
-"""Host-side phase times of bench.py's default Tracker2D step (diagnostic):
-how long group.launch, the frame pushes, complete_raw and the result packing
-take on the host, per frame-set. Usage: python tools/t2d_host_timing.py [steps]"""
+"""Host-side phase times of bench.py's default (pipelined) Tracker2D step
+(diagnostic): Python-side time of launch (a confirmation after complete_next),
+the frame pushes, complete_next and the result packing per frame-set, and the
+C++ phases inside complete_next (psn_t2d_group_debug_host_times).
+Usage: python tools/t2d_host_timing.py [steps]"""
 import ctypes
+import json
 import os
 import sys
 import time
@@ -28,18 +31,20 @@ def main():
     slot_bytes = t2d.result_slot_bytes(2 * B, 1)
     send = pinned((C, slot_bytes))
     T = t2d.load()
+    seq = [group.records([fd.detections(t) for fd in feeds]) for t in range(steps + 6)]
     for k, fd in enumerate(feeds):
         fd.push(group, k, 0)
     rows = []
     for t in range(steps + 5):
-        dets = [fd.detections(t) for fd in feeds]
+        if t == 5:
+            group.debug_host_times()  # reset after the warm-up
         a = time.perf_counter()
-        group.launch(t, dets)
+        group.launch(t, seq[t])
         b = time.perf_counter()
         for k, fd in enumerate(feeds):
             fd.push(group, k, t + 1)
         c = time.perf_counter()
-        group.complete_raw()
+        group.complete_next(t + 1, seq[t + 1], raw=True)
         d = time.perf_counter()
         for k in range(C):
             T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
@@ -47,9 +52,10 @@ def main():
         if t >= 5:
             rows.append((b - a, c - b, d - c, e - d, e - a))
     r = np.array(rows) * 1e3
-    names = ["launch", "push x4", "complete (sync + host update)", "pack", "total"]
+    names = ["launch (confirm)", "push x4", "complete_next", "pack", "total"]
     for i, n in enumerate(names):
         print(f"{n:32s} mean {r[:, i].mean():7.3f} ms  p50 {np.median(r[:, i]):7.3f}  max {r[:, i].max():7.3f}")
+    print("complete_next phases (us from entry):", json.dumps(group.debug_host_times()))
     group.close()
 
 
