@@ -650,6 +650,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         a.counts = d_counts;
         int wgs = 0, lds = 0, maxpx = 0, nqd = 0, rows_ow = 0, lds_ow = 0, upt_bx = 0, lds_bx = 0;
         bool all_single = true, all_box = true;
+        bool bx_notail = true;  // every query: SSE2 order with no scalar-tail pixels (width % 8 == 0)
         for (int i = 0; i < n; i++) {
             const psn_lk_query &qq = q[base + i];
             if (qq.num_pts == 0) {
@@ -662,6 +663,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch, orows, olds, bupt, blds);
             if (rc) return rc;
             all_box &= bupt > 0;
+            bx_notail &= (qq.params.flags & PSN_LK_ACCUM_SCALAR) == 0 && qq.params.win_w % 8 == 0;
             upt_bx = std::max(upt_bx, bupt);
             lds_bx = std::max(lds_bx, blds);
             a.q[nqd].qidx = base + i;
@@ -730,7 +732,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                     d.bx_hw++;
                 lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw).total);
             }
-            HIPCHK(c, psn::launch_lk_bx(a, wgs, upt_bx, lds_bx, c->stream));
+            HIPCHK(c, psn::launch_lk_bx(a, wgs, upt_bx, bx_notail, lds_bx, c->stream));
             continue;
         }
         if (!all_single) {  // the generic kernel runs every query of this launch: re-plan its LDS

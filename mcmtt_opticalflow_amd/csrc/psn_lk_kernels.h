@@ -259,7 +259,9 @@ void pyramid_grid(const PyrBuildArgs &a, int &tiles_x, int &tiles_y, int &lds_by
 // plus 1000 * E for the one-wave iteration mode (E window rows per lane).
 hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_bytes, bool single_tile, hipStream_t s);
 // Box-window kernel with UPT units per thread (4, 8, 10 or 12).
-hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, int lds_bytes, hipStream_t s);
+// notail: every query of the launch sums in the SSE2 order with width % 8 == 0
+// (no scalar-tail chain: a build without its per-pixel bookkeeping)
+hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, bool notail, int lds_bytes, hipStream_t s);
 hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
 
 }  // namespace psn

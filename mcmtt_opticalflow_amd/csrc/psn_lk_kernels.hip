@@ -2478,7 +2478,7 @@ __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax
     do {            \
     } while (0)
 #endif
-template <int UPT>
+template <int UPT, bool NOTAIL>
 __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NT = kBxNT;
@@ -2658,15 +2658,21 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             asm volatile("" : "+v"(q));
 #pragma unroll
             for (int k = 0; k < UPT; k++) {
-                const bool sA = q < nqA;
+                const bool sA = NOTAIL || q < nqA;
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const int gx = (i & 1) ? hi16(XP[k][i >> 1]) : lo16(XP[k][i >> 1]);
                     const int gy = (i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]);
+                    const int xx = __mul24(gx, gx), yy2 = __mul24(gy, gy), xy = __mul24(gx, gy);
+                    if (NOTAIL) {  // every unit is an SSE2 unit: pixel i feeds lane chain i
+                        T11[i] += xx;
+                        T22[i] += yy2;
+                        run_add(T12[i], M12[i], m12[i], xy);
+                        continue;
+                    }
                     // SSE2 unit: pixel i feeds lane chain i; else the tail chain, row-major
                     // (branch-free: the other chain gets a zero term)
                     const int ms = -(int)sA;
-                    const int xx = __mul24(gx, gx), yy2 = __mul24(gy, gy), xy = __mul24(gx, gy);
                     T11[i] += xx & ms;
                     T22[i] += yy2 & ms;
                     run_add(T12[i], M12[i], m12[i], xy & ms);
@@ -2692,9 +2698,9 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             BX_MARK(1);  // A window values + runs
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
-            bx_publish<15>(T, rec, tA == 0);
+            bx_publish<15>(T, rec, NOTAIL || tA == 0);
             __syncthreads();
-            bx_check<15>(T, M, m, false, rec, tA == 0);
+            bx_check<15>(T, M, m, false, rec, NOTAIL || tA == 0);
             __syncthreads();
             int tot, h0, base0;
             const bool exact = bx_eval<15>(rec, tot, h0, base0);
@@ -2732,7 +2738,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     if (!uv) return;
                     unsigned xp[2] = {x0, x1}, yp[2] = {y0_, y1_};
                     asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
-                    const bool su = qk < nqA;
+                    const bool su = NOTAIL || qk < nqA;
                     const int base = su ? yk * nqA + qk - sa : 4 * S + yk * tA + 4 * qk - nA4 - ta;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
@@ -2899,17 +2905,20 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         t2[i] = __mul24(d[i], gy);
                         dmax = max(dmax, abs(d[i]));
                     }
-                    // SSE2 unit -> lane chains 0-3, else the tail chain (branch-free)
-                    const int ms = -(int)(q < nqB);
+                    if (false) {  // (a no-tail form here costs registers: the products of later units are hoisted)
+                    } else {
+                        // SSE2 unit -> lane chains 0-3, else the tail chain (branch-free)
+                        const int ms = -(int)(q < nqB);
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        run_add(T1[i], M1[i], m1[i], t1[i] & ms);
-                        run_add(T2[i], M2[i], m2[i], t2[i] & ms);
-                    }
+                        for (int i = 0; i < 4; i++) {
+                            run_add(T1[i], M1[i], m1[i], t1[i] & ms);
+                            run_add(T2[i], M2[i], m2[i], t2[i] & ms);
+                        }
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        run_add(T1[4], M1[4], m1[4], t1[i] & ~ms);
-                        run_add(T2[4], M2[4], m2[4], t2[i] & ~ms);
+                        for (int i = 0; i < 4; i++) {
+                            run_add(T1[4], M1[4], m1[4], t1[i] & ~ms);
+                            run_add(T2[4], M2[4], m2[4], t2[i] & ~ms);
+                        }
                     }
                     if (++q == QW) {
                         q = 0;
@@ -2935,10 +2944,10 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             BX_MARK(4);  // b main pass
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
-            bx_publish<10>(T, rec, tB == 0);
+            bx_publish<10>(T, rec, NOTAIL || tB == 0);
             BX_MARK(9);  // b publish (this wave's scans and records)
             __syncthreads();
-            bx_check<10>(T, M, m, bad, rec, tB == 0);
+            bx_check<10>(T, M, m, bad, rec, NOTAIL || tB == 0);
             __syncthreads();
             int tot, h0, base0;
             float b1, b2;
@@ -2974,7 +2983,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     if (!uv) return;
                     int d[4];
                     bx_diffs(JR32 + (oy + yk) * JRP4 + (ox >> 2) + qk, JRP4, W0, W1, s0, s1, s2, s3, ip, d, zf);
-                    const bool su = qk < nqB;
+                    const bool su = NOTAIL || qk < nqB;
                     const int base = su ? yk * nqB + qk - sa : 4 * S + yk * tB + 4 * qk - n8 - ta;
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
@@ -3222,16 +3231,24 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
     }
 }
 
-hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, int lds_bytes, hipStream_t s) {
+hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, bool notail, int lds_bytes, hipStream_t s) {
     if (total_wgs <= 0) return hipSuccess;
     const dim3 grid(total_wgs), block(kBxNT);
+#define PSN_BX_CASE(U)                                                                              \
+    case U:                                                                                         \
+        if (notail)                                                                                 \
+            hipLaunchKernelGGL((lk_kernel_bx<U, true>), grid, block, lds_bytes, s, a);              \
+        else                                                                                        \
+            hipLaunchKernelGGL((lk_kernel_bx<U, false>), grid, block, lds_bytes, s, a);             \
+        break;
     switch (upt) {
-        case 4: hipLaunchKernelGGL(lk_kernel_bx<4>, grid, block, lds_bytes, s, a); break;
-        case 8: hipLaunchKernelGGL(lk_kernel_bx<8>, grid, block, lds_bytes, s, a); break;
-        case 10: hipLaunchKernelGGL(lk_kernel_bx<10>, grid, block, lds_bytes, s, a); break;
-        case 12: hipLaunchKernelGGL(lk_kernel_bx<12>, grid, block, lds_bytes, s, a); break;
+        PSN_BX_CASE(4)
+        PSN_BX_CASE(8)
+        PSN_BX_CASE(10)
+        PSN_BX_CASE(12)
         default: return hipErrorInvalidValue;
     }
+#undef PSN_BX_CASE
     return hipGetLastError();
 }
 
@@ -3290,8 +3307,10 @@ hipError_t lk_kernels_init() {
     for (const void *f : st)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = hipFuncSetAttribute((const void *)pyramid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
-    const void *bx[] = {(const void *)lk_kernel_bx<4>, (const void *)lk_kernel_bx<8>, (const void *)lk_kernel_bx<10>,
-                        (const void *)lk_kernel_bx<12>};
+    const void *bx[] = {(const void *)lk_kernel_bx<4, false>, (const void *)lk_kernel_bx<8, false>,
+                        (const void *)lk_kernel_bx<10, false>, (const void *)lk_kernel_bx<12, false>,
+                        (const void *)lk_kernel_bx<4, true>, (const void *)lk_kernel_bx<8, true>,
+                        (const void *)lk_kernel_bx<10, true>, (const void *)lk_kernel_bx<12, true>};
     for (const void *f : bx)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     return gridfast_kernels_init();
