@@ -2589,49 +2589,72 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             for (int k = 0; k < UPT; k++) {
                 const bool uv = u0 + k < U;
                 const int yy = uv ? y : 0, qq = uv ? q : 0;
-                int B[4][7];
+                // the unit's 4 x 7-byte patch window as packed 16-bit pairs: even pairs
+                // E[r][k] = (byte 2k, byte 2k+1), odd pairs O[r-1][k] = (2k+1, 2k+2) of rows 1, 2
+                s16x2 E[4][4], O[2][2];
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
                     const uint32_t *p = P32 + (yy + r) * PM + qq;
                     const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
                     const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                    B[r][0] = lo & 255;
-                    B[r][1] = (lo >> 8) & 255;
-                    B[r][2] = (lo >> 16) & 255;
-                    B[r][3] = lo >> 24;
-                    B[r][4] = hi & 255;
-                    B[r][5] = (hi >> 8) & 255;
-                    B[r][6] = (hi >> 16) & 255;
+                    E[r][0] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c010c00u));
+                    E[r][1] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
+                    E[r][2] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c050c04u));
+                    E[r][3] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c070c06u));
+                    if (r == 1 || r == 2) {
+                        O[r - 1][0] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c020c01u));
+                        O[r - 1][1] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
+                    }
                 }
-                int DX[2][5], DY[2][5];
+                // column masks of pixels 2k, 2k+1 (zero derivative outside the image)
+                unsigned cm[3];
+#pragma unroll
+                for (int kk = 0; kk < 3; kk++)
+                    cm[kk] = ((unsigned)(ipx + 4 * qq + 2 * kk) < (unsigned)cols ? 0xffffu : 0u) |
+                             ((unsigned)(ipx + 4 * qq + 2 * kk + 1) < (unsigned)cols ? 0xffff0000u : 0u);
+                // Scharr on packed pairs (|values| <= 4080: exact in 16 bits): DX/DY pairs
+                // (2k, 2k+1) of the two derivative rows o = 0, 1
+                unsigned DXp[2][3], DYp[2][3];
+                const s16x2 k3 = {3, 3}, k10 = {10, 10};
 #pragma unroll
                 for (int o = 0; o < 2; o++) {
-                    const bool rin = (unsigned)(ipy + yy + o) < (unsigned)rows;
-                    int sv[7], dv[7];
+                    const unsigned rm = (unsigned)(ipy + yy + o) < (unsigned)rows ? ~0u : 0u;
+                    s16x2 SV[4], DV[4];
 #pragma unroll
-                    for (int j = 0; j < 7; j++) {
-                        sv[j] = 3 * (B[o][j] + B[o + 2][j]) + 10 * B[o + 1][j];
-                        dv[j] = B[o + 2][j] - B[o][j];
+                    for (int kk = 0; kk < 4; kk++) {
+                        SV[kk] = (E[o][kk] + E[o + 2][kk]) * k3 + E[o + 1][kk] * k10;
+                        DV[kk] = E[o + 2][kk] - E[o][kk];
                     }
 #pragma unroll
-                    for (int j = 0; j < 5; j++) {
-                        // zero outside the image; branch-free (a select per value keeps the
-                        // unit one basic block)
-                        const int msk = -(int)(rin & ((unsigned)(ipx + 4 * qq + j) < (unsigned)cols));
-                        DX[o][j] = (sv[j + 2] - sv[j]) & msk;
-                        DY[o][j] = (3 * (dv[j] + dv[j + 2]) + 10 * dv[j + 1]) & msk;
+                    for (int kk = 0; kk < 3; kk++) {
+                        const s16x2 dvo = __builtin_bit_cast(
+                            s16x2, __builtin_amdgcn_alignbyte(__builtin_bit_cast(unsigned, DV[kk + 1]),
+                                                              __builtin_bit_cast(unsigned, DV[kk]), 2));
+                        const s16x2 dx = SV[kk + 1] - SV[kk];
+                        const s16x2 dy = (DV[kk] + DV[kk + 1]) * k3 + dvo * k10;
+                        DXp[o][kk] = __builtin_bit_cast(unsigned, dx) & cm[kk] & rm;
+                        DYp[o][kk] = __builtin_bit_cast(unsigned, dy) & cm[kk] & rm;
                     }
                 }
+                // bilinear window values by v_dot2 on (x, x+1) pairs, rounding folded in
+                const unsigned Wa = pack_w(iw00, iw01), Wb = pack_w(iw10, iw11);
+                const unsigned b1p[4] = {__builtin_bit_cast(unsigned, O[0][0]), __builtin_bit_cast(unsigned, E[1][1]),
+                                         __builtin_bit_cast(unsigned, O[0][1]), __builtin_bit_cast(unsigned, E[1][2])};
+                const unsigned b2p[4] = {__builtin_bit_cast(unsigned, O[1][0]), __builtin_bit_cast(unsigned, E[2][1]),
+                                         __builtin_bit_cast(unsigned, O[1][1]), __builtin_bit_cast(unsigned, E[2][2])};
                 int ix[4], iy[4], iv[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     const bool pv = uv && 4 * qq + i < w;
-                    iv[i] = PSN_DESCALE(__mul24(B[1][i + 1], iw00) + __mul24(B[1][i + 2], iw01) +
-                                                   __mul24(B[2][i + 1], iw10) + __mul24(B[2][i + 2], iw11), 9);
-                    const int gx = PSN_DESCALE(__mul24(DX[0][i], iw00) + __mul24(DX[0][i + 1], iw01) +
-                                                   __mul24(DX[1][i], iw10) + __mul24(DX[1][i + 1], iw11), 14);
-                    const int gy = PSN_DESCALE(__mul24(DY[0][i], iw00) + __mul24(DY[0][i + 1], iw01) +
-                                                   __mul24(DY[1][i], iw10) + __mul24(DY[1][i + 1], iw11), 14);
+                    const int h = i >> 1;
+                    // pairs (i, i+1): even i from the stored pairs, odd i shifted by 16 bits
+                    const unsigned x0 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[0][h + 1], DXp[0][h], 2) : DXp[0][h];
+                    const unsigned x1 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[1][h + 1], DXp[1][h], 2) : DXp[1][h];
+                    const unsigned y0_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[0][h + 1], DYp[0][h], 2) : DYp[0][h];
+                    const unsigned y1_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[1][h + 1], DYp[1][h], 2) : DYp[1][h];
+                    iv[i] = sdot2(b2p[i], Wb, sdot2(b1p[i], Wa, 1 << 8)) >> 9;
+                    const int gx = sdot2(x1, Wb, sdot2(x0, Wa, 1 << 13)) >> 14;
+                    const int gy = sdot2(y1_, Wb, sdot2(y0_, Wa, 1 << 13)) >> 14;
                     ix[i] = gx & -(int)pv;
                     iy[i] = gy & -(int)pv;
                     gmax = max(gmax, max(abs(ix[i]), abs(iy[i])));
