@@ -2912,13 +2912,15 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             unsigned zm;
             asm volatile("v_mov_b32 %0, 0" : "=v"(zm));
             {
-                int y = y0, q = q0;
-            asm volatile("" : "+v"(y), "+v"(q));  // opaque: no per-unit address hoisting (VGPRs)
+                // the unit's J row in dwords, stepped unit by unit (row-major units: +1, or
+                // to the next row's first quad); opaque start: no per-unit address hoisting
+                int q = q0, off = (oy + y0) * JRP4 + (ox >> 2) + q0;
+                asm volatile("" : "+v"(off), "+v"(q));
 #pragma unroll
                 for (int k = 0; k < UPT; k++) {
                     const bool uv = u0 + k < U;
                     int d[4];
-                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, zm);
+                    bx_diffs(JR32 + (uv ? off : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, zm);
                     int t1[4], t2[4];
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
@@ -2928,7 +2930,12 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         t2[i] = __mul24(d[i], gy);
                         dmax = max(dmax, abs(d[i]));
                     }
-                    if (false) {  // (a no-tail form here costs registers: the products of later units are hoisted)
+                    if (NOTAIL) {  // every unit feeds lane chains 0-3
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            run_add(T1[i], M1[i], m1[i], t1[i]);
+                            run_add(T2[i], M2[i], m2[i], t2[i]);
+                        }
                     } else {
                         // SSE2 unit -> lane chains 0-3, else the tail chain (branch-free)
                         const int ms = -(int)(q < nqB);
@@ -2943,9 +2950,10 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                             run_add(T2[4], M2[4], m2[4], t2[i] & ~ms);
                         }
                     }
-                    if (++q == QW) {
-                        q = 0;
-                        y++;
+                    {
+                        const bool wrap = q == QW - 1;
+                        off += wrap ? JRP4 - QW + 1 : 1;
+                        q = wrap ? 0 : q + 1;
                     }
                     // materialize the runs per unit (no sinking across units)
                     asm volatile("" : "+v"(T1[0]), "+v"(T1[1]), "+v"(T1[2]), "+v"(T1[3]), "+v"(T1[4]), "+v"(M1[0]),
