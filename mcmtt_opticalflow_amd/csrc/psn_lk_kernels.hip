@@ -2744,9 +2744,13 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 // double-buffered: the threads of the next tile write its products
                 // while the chain lanes (lanes 0-14 of wave 0; lane c holds chain c's
                 // base0) sum the current one
+                // the fallback's thread roles from an opaque copy of the thread id: computed
+                // here, not hoisted to the kernel start and spilled across the loops
+                int ftid = (int)threadIdx.x;
+                asm volatile("" : "+v"(ftid));
                 const int HW = Q.bx_hw, PCA = 3 * bx_pc(UPT) * HW;
-                const bool chl = tid < 15;  // wave 0: its tiles are written first, so it rarely writes while it sums
-                const int cl = chl ? tid : 0, cs = cl / 5, cc = cl - 5 * cs;
+                const bool chl = ftid < 15;  // wave 0: its tiles are written first, so it rarely writes while it sums
+                const int cl = chl ? ftid : 0, cs = cl / 5, cc = cl - 5 * cs;
                 float acc = (float)base0;  // |base0| <= 2^24: exact
                 const int g_last = (U - 1) / (32 * UPT);
                 auto geoA = [&](int g, int &sa, int &ta, int &nsse, int &ntail) {
@@ -2786,11 +2790,11 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 auto writeA = [&](int g, float *buf) {
                     int sa, ta, nsse, ntail;
                     if (split) {
-                        if ((tid >> 6) != (g >> 1)) return;
+                        if ((ftid >> 6) != (g >> 1)) return;
                         geoA(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
-                        const bool lower = (g & 1) == 0, own = ((tid >> 5) & 1) == (g & 1);
-                        const int ub = (own ? tid : tid ^ 32) * UPT + (lower == own ? 0 : K1);
+                        const bool lower = (g & 1) == 0, own = ((ftid >> 5) & 1) == (g & 1);
+                        const int ub = (own ? ftid : ftid ^ 32) * UPT + (lower == own ? 0 : K1);
                         int yk = ub / QW, qk = ub - yk * QW;
                         asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
@@ -2804,7 +2808,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         }
                         return;
                     }
-                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
+                    if ((ftid >> 5) < g || (ftid >> 5) >= g + HW) return;
                     geoA(g, sa, ta, nsse, ntail);
                     const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                     int yk = y0, qk = q0;
@@ -2834,7 +2838,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 for (int g = h0, t = 0; g <= g_last; g += HW, t ^= 1) {
                     float *cur = PL + t * PCA, *nxt = PL + (t ^ 1) * PCA;
                     if (g + HW <= g_last) writeA(g + HW, nxt);
-                    if ((tid >> 6) == 0) {
+                    if ((ftid >> 6) == 0) {
                         int sa, ta, nsse, ntail;
                         geoA(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
@@ -2845,7 +2849,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     }
                     __syncthreads();
                 }
-                if (tid < 64) {  // wave 0 combines in the SSE2 build's order
+                if (ftid < 64) {  // wave 0 combines in the SSE2 build's order
                     const int av = __float_as_int(acc);
 #pragma unroll
                     for (int s = 0; s < 3; s++) {
@@ -2857,7 +2861,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                             const float c3 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 3));
                             t = __fadd_rn(t, __fadd_rn(__fadd_rn(__fadd_rn(c0, c1), c2), c3));
                         }
-                        if (tid == 0) RS[s] = t;
+                        if (ftid == 0) RS[s] = t;
                     }
                 }
                 __syncthreads();
@@ -2996,9 +3000,12 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 // double-buffered: the threads of tile g+1 write its products while the
                 // chain lanes (wave 0, lanes 0-9, starting from the exact prefixes
                 // base0) sum tile g
+                // thread roles from an opaque copy of the thread id (see the A fallback)
+                int ftid = (int)threadIdx.x;
+                asm volatile("" : "+v"(ftid));
                 const int HW = Q.bx_hw, PC = bx_pc(UPT) * HW;
-                const bool chl = tid < 10;  // wave 0 (as in the A fallback)
-                const int cl = chl ? tid : 0, cs = cl / 5, cc = cl - 5 * cs;
+                const bool chl = ftid < 10;  // wave 0 (as in the A fallback)
+                const int cl = chl ? ftid : 0, cs = cl / 5, cc = cl - 5 * cs;
                 float acc = (float)base0;
                 const int g_last = (U - 1) / (32 * UPT);
                 auto tile_geo = [&](int g, int &sa, int &ta, int &nsse, int &ntail) {
@@ -3044,11 +3051,11 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     asm volatile("v_mov_b32 %0, 0" : "=v"(zf));
                     int sa, ta, nsse, ntail;
                     if (split) {
-                        if ((tid >> 6) != (g >> 1)) return;
+                        if ((ftid >> 6) != (g >> 1)) return;
                         tile_geo(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
-                        const bool lower = (g & 1) == 0, own = ((tid >> 5) & 1) == (g & 1);
-                        const int ub = (own ? tid : tid ^ 32) * UPT + (lower == own ? 0 : K1);
+                        const bool lower = (g & 1) == 0, own = ((ftid >> 5) & 1) == (g & 1);
+                        const int ub = (own ? ftid : ftid ^ 32) * UPT + (lower == own ? 0 : K1);
                         int yk = ub / QW, qk = ub - yk * QW;
                         asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
@@ -3064,7 +3071,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         }
                         return;
                     }
-                    if ((tid >> 5) < g || (tid >> 5) >= g + HW) return;
+                    if ((ftid >> 5) < g || (ftid >> 5) >= g + HW) return;
                     tile_geo(g, sa, ta, nsse, ntail);
                     const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                     int yk = y0, qk = q0;
@@ -3098,7 +3105,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     unsigned long long tc0, tc1, tc2;
                     BX_CLK(tc0);
 #endif
-                    if ((tid >> 6) == 0) {
+                    if ((ftid >> 6) == 0) {
                         int sa, ta, nsse, ntail;
                         tile_geo(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
@@ -3120,7 +3127,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 }
                 BX_MARK(7);  // serial b: pipelined products + chains
                 BX_COUNT(11);
-                if (tid < 64) {  // wave 0 combines in the SSE2 build's order
+                if (ftid < 64) {  // wave 0 combines in the SSE2 build's order
                     const int a = __float_as_int(acc);
                     float r1 = __int_as_float(__builtin_amdgcn_readlane(a, 4));
                     float r2 = __int_as_float(__builtin_amdgcn_readlane(a, 9));
@@ -3136,7 +3143,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         r1 = __fadd_rn(r1, __fadd_rn(bb0, bb2));
                         r2 = __fadd_rn(r2, __fadd_rn(bb1, bb3));
                     }
-                    if (tid == 0) {
+                    if (ftid == 0) {
                         RS[4] = r1;
                         RS[5] = r2;
                     }
