@@ -1070,7 +1070,8 @@ __device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int
 // aligned-down column gx0 & ~3) into LDS bytes: interior patches move as
 // aligned dwords by LDS-DMA (lane i of a chunk lands at dst + 4 * i, so the
 // chunk of dwords c0.. is contiguous in LDS); patches crossing the image border
-// gather their bytes through reflect-101 with plain loads and byte stores.
+// reflect their rows, move the dwords that lie inside the image the same way and
+// gather the others' bytes through reflect-101.
 template <int NT>
 __device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m,
                                           unsigned dv_m) {
@@ -1089,11 +1090,24 @@ __device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int g
             }
         }
     } else {
-        const int rb = 4 * m;
-        for (int q = threadIdx.x; q < PH * rb; q += NT) {
-            const int r = qdiv(q >> 2, dv_m), c = q - r * rb;
-            const int gy = refl101(gy0 + r, L.h), gx = refl101(ax + c, L.w);
-            dst[q] = L.p[(size_t)gy * L.pitch + gx];
+        // across the border: reflect-101 rows; dwords whose 4 columns are inside the
+        // image still move by LDS-DMA (lanes with such a dword: the DMA writes lane i's
+        // dword at dst + 4 * (c0 + i)), the others gather their 4 reflected bytes
+        for (int c0 = wid * 64; c0 < n; c0 += NT) {
+            const int q = c0 + lane;
+            if (q < n) {
+                const int r = qdiv(q, dv_m), j = q - r * m;
+                const uint8_t *row = L.p + (size_t)refl101(gy0 + r, L.h) * L.pitch;
+                const int x = ax + 4 * j;
+                if (x >= 0 && x + 4 <= L.w) {
+                    __builtin_amdgcn_global_load_lds((gptr_t)(row + x), (lptr_t)(dst + 4 * c0), 4, 0, 0);
+                } else {
+                    unsigned v = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) v |= (unsigned)row[refl101(x + b, L.w)] << (8 * b);
+                    *(unsigned *)(dst + 4 * q) = v;
+                }
+            }
         }
     }
 }
