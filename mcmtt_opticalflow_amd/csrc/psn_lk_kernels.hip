@@ -2349,16 +2349,18 @@ constexpr int kBxHalfRec = 120;
 template <int NC>
 __device__ __forceinline__ void bx_publish(int (&T)[NC], int *rec, bool no_tail) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // every chain's scan first (independent DPP chains interleave: no hazard
+    // waits between the steps of one scan), then the records in one exec region
+    int incl[NC];
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-        if (no_tail && c % 5 == 4) {  // empty tail chain (uniform)
-            if (lane == 31 || lane == 63) rec[8 * c + wv + (lane == 31 ? 4 : 0)] = 0;
-            continue;
-        }
-        const int incl = wave_scan(T[c]);
-        if (lane == 31 || lane == 63) rec[8 * c + wv + (lane == 31 ? 4 : 0)] = incl;
-        T[c] = incl - T[c];
+    for (int c = 0; c < NC; c++) incl[c] = (no_tail && c % 5 == 4) ? 0 : wave_scan(T[c]);
+    if (lane == 31 || lane == 63) {
+        int *r = rec + wv + (lane == 31 ? 4 : 0);
+#pragma unroll
+        for (int c = 0; c < NC; c++) r[8 * c] = incl[c];
     }
+#pragma unroll
+    for (int c = 0; c < NC; c++) T[c] = incl[c] - T[c];
 }
 template <int NC>
 __device__ __forceinline__ void bx_check(const int (&E)[NC], const int (&M)[NC], const int (&m)[NC], bool bad, int *rec,
