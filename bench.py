@@ -595,9 +595,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--tracker-pmc-summary", default=os.path.join(ROOT, "profiles", "r02j_tracker_pmc_summary.json"),
+    ap.add_argument("--tracker-pmc-summary", default=os.path.join(ROOT, "profiles", "r02k_tracker_pmc_summary.json"),
                     help="PMC FETCH/WRITE_SIZE summary of a default (tracker) run, for roofline.traffic")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02j_kernel_mode_pmc_summary.json"),
+    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02k_kernel_mode_pmc_summary.json"),
                     help="PMC summary of a kernel-mode run, for roofline.traffic")
     args = ap.parse_args()
     if args.mode == "kernel":
