@@ -2859,7 +2859,8 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         geoA(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                         const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
-                        const int nbmax = __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
+                        // (no-tail: every chain lane's length is nsse)
+                        const int nbmax = NOTAIL ? (nsse + 15) >> 4 : __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
                         if (chl) acc = chain_sum_pl(cur + cs * P + cc * S, len, nbmax, acc);
                         if (g + HW <= g_last) padA(g + HW, nxt);
                     }
@@ -3126,7 +3127,8 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         tile_geo(g, sa, ta, nsse, ntail);
                         const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
                         const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
-                        const int nbmax = __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
+                        // (no-tail: every chain lane's length is nsse)
+                        const int nbmax = NOTAIL ? (nsse + 15) >> 4 : __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
                         if (chl) acc = chain_sum_pl(cur + cs * P + cc * S, len, nbmax, acc);
                         if (g + HW <= g_last) pad_tile(g + HW, nxt);
                     }
