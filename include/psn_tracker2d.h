@@ -75,8 +75,8 @@ void psn_t2d_destroy(psn_t2d *t);
 const char *psn_t2d_last_error(psn_t2d *t);
 /* Where the backward chain's LocalSearchKLT steps run: 1 (default) on the
  * device -- every chain step's LK launch and LocalSearchKLT kernel enqueued
- * back to back, one host sync per frame -- or 0 on the host between launches
- * (env PSN_T2D_HOST_CHAIN=1 selects 0 at create). Results are identical. */
+ * back to back, one host sync per frame -- or 0 on the host between launches.
+ * Results are identical. */
 int psn_t2d_set_device_chain(psn_t2d *t, int on);
 /* ingest frame t into the ring's newest slot (cvtColor + resize, :256-263) */
 int psn_t2d_push_frame(psn_t2d *t, const uint8_t *frame, int stride, int channels);
@@ -182,11 +182,23 @@ int psn_t2d_track_frame_detect(psn_t2d *t, psn_t2d_detection *dets, int ndet, ui
 
 /* The assignment of Track2D_MatchingAndUpdating (:1040-1064 + CPSNWhere_Hungarian::Match):
  * cost = [rows x cols] row-major (the forward step's matchingCostArray);
- * non-finite entries become max(finite) + 100, a minimum-total-cost matching of
- * min(rows, cols) pairs is taken, and pairs at that substitute cost are dropped.
- * match[r] = the column matched to row r, or -1. Exact when the optimum is
- * unique (ties may be broken differently from the reference's Munkres). */
+ * non-finite entries become max(finite) + 100, the reference's Munkres
+ * (psn_t2d_hungarian_match) matches the matrix, and pairs at that substitute
+ * cost are dropped. match[r] = the column matched to row r, or -1. Ties break
+ * as the reference's row-major Munkres breaks them. */
 int psn_t2d_assign(const float *cost, int rows, int cols, int *match);
+
+/* CPSNWhere_Hungarian Initialize(float*, rows, cols) + Match()
+ * (helpers/PSNWhere_Hungarian.cpp:124-155, :212-359) on [rows x cols] float
+ * costs: non-finite entries become FLT_MAX - (sum of the finite ones), rows and
+ * columns without a finite entry are condensed out, the square is padded to its
+ * minimum line cover, Munkres steps 1-6 in float32 (row-major scans), and the
+ * starred pairs of finite original cost are returned in row-major order:
+ * out_rows/out_cols/out_costs (capacity min(rows, cols)), *n_out pairs
+ * (stMatchInfo rows / cols / matchCosts). A NaN cost or an empty matrix gives
+ * no pairs (the reference's Initialize leaves the matcher uninitialised). */
+int psn_t2d_hungarian_match(const float *cost, int rows, int cols, int *out_rows, int *out_cols, float *out_costs,
+                            int *n_out);
 
 /* ResultWithTracker (:1231-1257): id, last box and head, score 0,
  * featurePointsPrev = features, featurePointsCurr = tracked. */
@@ -259,7 +271,11 @@ int psn_t2d_group_run(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *c
  * be psn_t2d_group_launch(g, next_frame_idx, next_dets, next_ndet, feature_mode,
  * .), which then only confirms the frame, and next_dets must stay valid until
  * that frame's complete. A pipelined driver:
- *   launch(0); push(1); complete_next(0 -> 1); launch(1); push(2); complete_next(1 -> 2); ... */
+ *   launch(0); push(1); complete_next(0 -> 1); launch(1); push(2); complete_next(1 -> 2); ...
+ * If only the next frame cannot be launched (e.g. a detection whose window the
+ * LK cannot run), this frame's results are still written to dets / results and
+ * that error is returned; the next frame is not in flight, its images stay
+ * staged, and a plain psn_t2d_group_launch of it (fixed detections) follows. */
 int psn_t2d_group_complete_next(psn_t2d_group *g, psn_t2d_detection *const *dets, const int *ndet,
                                 psn_track2d_result *results, unsigned next_frame_idx,
                                 psn_t2d_detection *const *next_dets, const int *next_ndet, int feature_mode,

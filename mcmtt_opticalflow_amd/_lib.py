@@ -11,7 +11,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PSN_LK_LIB") or os.path.join(_HERE, "lib", "libpsn_lk.so")
+LIB_PATH = os.path.join(_HERE, "lib", "libpsn_lk.so")
+# the instrumented build of the same sources (tools/ only: per-phase s_memtime stamps)
+STAMPS_LIB_PATH = os.path.join(_HERE, "lib", "libpsn_lk_stamps.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psn_lk.h")
 # every header whose entry points libpsn_lk.so exports
 HEADER_PATHS = [HEADER_PATH] + [os.path.join(os.path.dirname(_HERE), "include", h)
@@ -90,13 +92,21 @@ def header_functions() -> list[str]:
 _lib = None
 
 
-def load():
-    global _lib
+_lib_path = None
+
+
+def load(path: str | None = None):
+    """The product library (mcmtt_opticalflow_amd/lib/libpsn_lk.so). Only the
+    profiling tools pass path (STAMPS_LIB_PATH), before anything else loads it."""
+    global _lib, _lib_path
+    path = path or LIB_PATH
     if _lib is not None:
+        if path != _lib_path:
+            raise RuntimeError(f"{_lib_path} is loaded already (asked for {path})")
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() (no CPU fallback exists)")
-    L = ctypes.CDLL(LIB_PATH)
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    L = ctypes.CDLL(path)
     vp, ip, u8p, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p
     L.psn_lk_abi_version.restype = ip
     L.psn_lk_default_params.argtypes = [ctypes.POINTER(LkParams)]
@@ -157,7 +167,7 @@ def load():
     L.psn_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
     L.psn_comm_destroy.argtypes = [vp]
     L.psn_comm_destroy.restype = None
-    _lib = L
+    _lib, _lib_path = L, path
     return L
 
 

@@ -293,7 +293,19 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(JpegArgs A) {
 
 int rd16(const uint8_t *p) { return (p[0] << 8) | p[1]; }
 
-void build_huff(const uint8_t *bits, const uint8_t *vals, int nvals, HuffDev &h) {
+// jdhuff.c jpeg_make_d_derived_tbl: false for a table libjpeg rejects with
+// JERR_BAD_HUFF_TABLE -- more codes of a length than fit after the shorter ones
+// (the canonical code would overflow its length; the all-ones code is not
+// allowed), or a DC symbol above 15. Checked before any table entry is written.
+bool build_huff(const uint8_t *bits, const uint8_t *vals, int nvals, bool dc, HuffDev &h) {
+    for (int l = 1, code = 0; l <= 16; l++) {
+        code += bits[l - 1];
+        if (code >= (1 << l)) return false;
+        code <<= 1;
+    }
+    if (dc)
+        for (int i = 0; i < nvals; i++)
+            if (vals[i] > 15) return false;
     memset(&h, 0, sizeof h);
     int code = 0, k = 0;
     for (int l = 1; l <= 16; l++) {
@@ -310,6 +322,7 @@ void build_huff(const uint8_t *bits, const uint8_t *vals, int nvals, HuffDev &h)
     }
     h.maxcode[17] = 0x7fffffff;
     for (int i = 0; i < 256; i++) h.vals[i] = i < nvals ? vals[i] : 0;
+    return true;
 }
 
 }  // namespace
@@ -390,7 +403,8 @@ int parse(const uint8_t *d, size_t n, Parsed &P, std::string &why) {
                 int cnt = 0;
                 for (int l = 0; l < 16; l++) cnt += s[o + 1 + l];
                 if (cnt > 256 || o + 17 + cnt > sl) return why = "bad DHT", PSN_LK_ERR_ARG;
-                psn::build_huff(s + o + 1, s + o + 17, cnt, tc ? P.tab.ac[th] : P.tab.dc[th]);
+                if (!psn::build_huff(s + o + 1, s + o + 17, cnt, tc == 0, tc ? P.tab.ac[th] : P.tab.dc[th]))
+                    return why = "bad DHT (code lengths or DC symbols)", PSN_LK_ERR_ARG;
                 o += 17 + cnt;
             }
         } else if (m == 0xC0 || m == 0xC1) {
@@ -433,8 +447,10 @@ int parse(const uint8_t *d, size_t n, Parsed &P, std::string &why) {
         a.hmax = std::max(a.hmax, a.c[c].h);
         a.vmax = std::max(a.vmax, a.c[c].v);
     }
+    // 4:4:4, 4:2:2 (h2v1) and 4:2:0 (h2v2) chroma; 4:4:0 (luma 1x2: a vertical-only
+    // upsample, h1v2) has no path in jpeg_color_kernel's chroma() and is refused
     if (a.nc == 3 && (a.c[0].h != a.hmax || a.c[0].v != a.vmax || a.c[1].h != 1 || a.c[1].v != 1 || a.c[2].h != 1 ||
-                      a.c[2].v != 1))
+                      a.c[2].v != 1 || (a.hmax == 1 && a.vmax == 2)))
         return why = "unsupported sampling", PSN_LK_ERR_UNSUPPORTED;
     const int mcux = (a.W + 8 * a.hmax - 1) / (8 * a.hmax), mcuy = (a.H + 8 * a.vmax - 1) / (8 * a.vmax);
     int blk = 0, plane = 0;

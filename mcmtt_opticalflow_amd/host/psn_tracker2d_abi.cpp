@@ -387,6 +387,25 @@ int psn_t2d_assign(const float *cost, int rows, int cols, int *match) {
     return 0;
 }
 
+int psn_t2d_hungarian_match(const float *cost, int rows, int cols, int *out_rows, int *out_cols, float *out_costs,
+                            int *n_out) {
+    if (rows < 0 || cols < 0 || !n_out || (rows > 0 && cols > 0 && (!cost || !out_rows || !out_cols || !out_costs)))
+        return PSN_LK_ERR_ARG;
+    *n_out = 0;
+    std::vector<float> c;
+    if (rows > 0 && cols > 0) c.assign(cost, cost + (size_t)rows * cols);
+    std::vector<int> r, k;
+    std::vector<float> v;
+    if (!psn::HungarianMatch(c, (size_t)rows, (size_t)cols, r, k, v)) return PSN_LK_ERR_ARG;
+    for (size_t i = 0; i < r.size(); i++) {
+        out_rows[i] = r[i];
+        out_cols[i] = k[i];
+        out_costs[i] = v[i];
+    }
+    *n_out = (int)r.size();
+    return 0;
+}
+
 int psn_t2d_result_with_tracker(const psn_t2d_tracker *trk, psn_object2d *out) {
     if (!trk || !out) return PSN_LK_ERR_ARG;
     psn::Tracker2D t;
@@ -417,8 +436,12 @@ int psn_t2d_matching_and_updating(const psn_t2d_detection *dets, int ndet, const
     }
     std::vector<int> m(objs.size(), -1);
     if (match) {
+        // an assignment: each tracker at most once (the Hungarian's output never
+        // repeats a column; a repeat would update and enqueue one tracker twice)
+        std::vector<char> taken((size_t)ntrk, 0);
         for (size_t d = 0; d < objs.size(); d++) {
             if (match[d] < -1 || match[d] >= ntrk) return PSN_LK_ERR_ARG;
+            if (match[d] >= 0 && taken[(size_t)match[d]]++) return PSN_LK_ERR_ARG;
             m[d] = match[d];
         }
     } else if (ntrk > 0 && !objs.empty()) {
@@ -550,6 +573,14 @@ int psn_t2d_group_complete_next(psn_t2d_group *g, psn_t2d_detection *const *dets
     }
     g->launched = false;
     const int rc = g->flow.RunComplete(g->io(), &nx, next_frame_idx, feature_mode == PSN_T2D_FEATURES_GRIDFAST, seed);
+    if (rc && g->flow.FrameCompleted()) {
+        // only the next frame failed to launch: this frame's results are still
+        // delivered, and that frame (staged again) is for a plain launch
+        const int orc = group_outputs(g, dets, ndet, results);
+        gset(g, rc);
+        g->err = "next frame " + std::to_string(next_frame_idx) + " not launched: " + g->err;
+        return orc ? orc : rc;
+    }
     if (rc) return gset(g, rc);
     const int orc = group_outputs(g, dets, ndet, results);
     g->cur ^= 1;  // the next frame's io, launched ahead

@@ -1141,6 +1141,16 @@ int Tracker2DFlow::AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::ve
     return PSN_LK_OK;
 }
 
+void Tracker2DFlow::UnadoptFrames() {
+    for (Cam &cam : cams_) {
+        const int newest = cam.ring[kT2dInterval - 1];
+        std::rotate(cam.ring, cam.ring + kT2dInterval - 1, cam.ring + kT2dInterval);
+        cam.ring[0] = cam.spare;
+        cam.spare = newest;
+        cam.staged = true;
+    }
+}
+
 // Enqueue frame t's device work for every camera: one pass over all cameras
 // (features, backward chains, forward calls of every active tracker). When
 // RunComplete(t-1, next = frame t) has launched frame t already, this only
@@ -1206,17 +1216,27 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     using clk = std::chrono::steady_clock;
     const clk::time_point t0 = clk::now();
     auto stamp = [&](int i) { host_us_[i] += std::chrono::duration<double, std::micro>(clk::now() - t0).count(); };
+    frame_completed_ = false;
     int rc = PassCopy(run_pass_);
     const bool early = !rc && next && ChainsFit(*next);
     int prc = PSN_LK_OK;
     std::vector<PassCam> pre;
+    // a next frame that cannot be launched leaves no trace: its chains drained,
+    // its frames staged again (the rings as before), frame t still completed
+    auto abandon_next = [&]() {
+        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        UnadoptFrames();
+        pre.clear();
+    };
     auto prelaunch = [&]() {
         prc = AdoptFrames(*next, nextGridfast, pre);
-        if (!prc) prc = PassLaunchChains(pre, nextGridfast, nextSeed);
         if (prc) {
-            (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
             pre.clear();
+            return;
         }
+        prc = PassLaunchChains(pre, nextGridfast, nextSeed);
+        if (prc) abandon_next();
     };
     if (early) prelaunch();
     stamp(0);  // copies + next chains enqueued
@@ -1225,6 +1245,7 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     if (!rc) rc = PassFeatures(run_pass_, run_gridfast_);
     if (rc) {
         run_pass_.clear();
+        if (next && early && !prc) abandon_next();  // frame t failed: nothing of t+1 stays in flight
         return rc;
     }
     PassUnpack(run_pass_);
@@ -1242,14 +1263,14 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     }
     stamp(3);  // matched, trackers updated
     host_calls_++;
+    frame_completed_ = true;
     if (!next || prc) return prc;
     // frame t+1's forward calls: the trackers as frame t's update left them
     AttachForward(pre);
     prc = PassLaunchForward(pre);
     stamp(4);  // next forward enqueued
     if (prc) {
-        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
-        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        abandon_next();
         return prc;
     }
     run_pass_ = std::move(pre);

@@ -38,6 +38,9 @@ void ResultWithTracker(const Tracker2D &tracker, Object2DInfo &out);
 // tracker2d_match.cpp: the assignment of Track2D_MatchingAndUpdating (inf
 // handling + minimum-cost matching, :1040-1064) and the update (:1066-1164)
 std::vector<int> AssignDetections(const std::vector<float> &cost, size_t rows, size_t cols);
+// CPSNWhere_Hungarian::Match (helpers/PSNWhere_Hungarian.cpp:212-359): matched pairs in row-major order
+bool HungarianMatch(const std::vector<float> &cost, size_t rows, size_t cols, std::vector<int> &outRows,
+                    std::vector<int> &outCols, std::vector<float> &outCosts);
 void MatchingAndUpdating(std::vector<DetectedObject> &dets, std::deque<Tracker2D *> &active,
                          std::list<Tracker2D> &storage, const std::vector<int> &match, unsigned frameIdx,
                          unsigned &newTrackerID, Track2DResult &result);
@@ -111,6 +114,11 @@ class Tracker2DFlow {
     // RunComplete(t) + RunLaunch(t+1).
     int RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> *next, unsigned nextFrameIdx, bool nextGridfast,
                     uint32_t nextSeed);
+    // After a failed RunComplete: true when frame t itself was completed (its
+    // results are in io) and only launching the next frame failed. The next
+    // frame's staged images and the rings are then as before the call, so a
+    // RunLaunch of that frame (e.g. with corrected detections) may follow.
+    bool FrameCompleted() const { return frame_completed_; }
     const std::deque<Tracker2D *> &ActiveTrackers(size_t cam) const { return cams_[cam].active; }
     // diagnostic: accumulated host microseconds from RunComplete's entry to its
     // phases (copies + next chains enqueued, device done, unpacked, matched, next
@@ -211,6 +219,8 @@ class Tracker2DFlow {
     void *ev_chain_ = nullptr, *ev_fwd_ = nullptr;  // hipEvent_t: a pass's result copies done
     bool wait_chain_ = false, wait_fwd_ = false;
     int AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::vector<PassCam> &pass);
+    void UnadoptFrames();  // AdoptFrames undone: frame t's slot back to staging, the oldest back in the ring
+    bool frame_completed_ = false;
     std::vector<PassCam> run_pass_;  // the pass between RunLaunch and RunComplete
     void AttachForward(std::vector<PassCam> &pass);
     std::vector<CamFrame> *pre_io_ = nullptr;  // the io of a frame RunComplete launched ahead

@@ -18,7 +18,7 @@ import numpy as np
 from ._lib import ERRORS
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("PSN_T2D_LIB") or os.path.join(_HERE, "lib", "libpsn_tracker2d.so")
+LIB_PATH = os.path.join(_HERE, "lib", "libpsn_tracker2d.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "psn_tracker2d.h")
 
 MAX_FEATURES = 100
@@ -152,6 +152,7 @@ def load():
     L.psn_t2d_track_frame.argtypes = [vp, ctypes.POINTER(Detection), ip, ctypes.POINTER(Tracker), ip, fp]
     L.psn_t2d_abi_version.restype = ip
     L.psn_t2d_assign.argtypes = [fp, ip, ip, vp]
+    L.psn_t2d_hungarian_match.argtypes = [fp, ip, ip, vp, vp, fp, ctypes.POINTER(ip)]
     L.psn_t2d_result_with_tracker.argtypes = [ctypes.POINTER(Tracker), ctypes.POINTER(Object2D)]
     L.psn_t2d_matching_and_updating.argtypes = [ctypes.POINTER(Detection), ip, ctypes.POINTER(Tracker), ip, fp, vp,
                                                 ctypes.c_uint, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(Tracker),
@@ -332,6 +333,20 @@ def assign(cost: np.ndarray) -> list[int]:
     return m[:rows].tolist()
 
 
+def hungarian_match(cost: np.ndarray):
+    """psn_t2d_hungarian_match (CPSNWhere_Hungarian::Match) -> (rows, cols, costs) of the matched pairs."""
+    c = np.ascontiguousarray(cost, np.float32)
+    rows, cols = c.shape
+    cap = max(min(rows, cols), 1)
+    r, k, v = np.zeros(cap, np.int32), np.zeros(cap, np.int32), np.zeros(cap, np.float32)
+    n = ctypes.c_int()
+    rc = load().psn_t2d_hungarian_match(c.ctypes.data, rows, cols, r.ctypes.data, k.ctypes.data, v.ctypes.data,
+                                        ctypes.byref(n))
+    if rc:
+        raise T2dError(rc, "psn_t2d_hungarian_match")
+    return r[:n.value].tolist(), k[:n.value].tolist(), v[:n.value].tolist()
+
+
 def result_with_tracker(trk: Tracker) -> dict:
     o = Object2D()
     rc = load().psn_t2d_result_with_tracker(ctypes.byref(trk), ctypes.byref(o))
@@ -450,13 +465,18 @@ class Group:
         confirms it."""
         arrs, ptrs, nd = self._keep
         nxt = self.records(next_dets_per_cam)
-        self._check(self._L.psn_t2d_group_complete_next(self._h, ptrs, nd, self._res, next_frame_idx, nxt[1], nxt[2],
-                                                        int(bool(gridfast)), ctypes.c_uint32(seed & 0xffffffff)),
-                    "complete_next")
+        rc = self._L.psn_t2d_group_complete_next(self._h, ptrs, nd, self._res, next_frame_idx, nxt[1], nxt[2],
+                                                 int(bool(gridfast)), ctypes.c_uint32(seed & 0xffffffff))
         self._keep = None
+        if rc:  # e.results: this frame's outputs when only the next frame's launch failed
+            err = T2dError(rc, f"complete_next: {self._L.psn_t2d_group_last_error(self._h).decode()}")
+            err.results = self._outputs(arrs, nd) if b"not launched" in self._L.psn_t2d_group_last_error(self._h) \
+                else None
+            raise err
         self._ahead = nxt
-        if raw:
-            return None
+        return None if raw else self._outputs(arrs, nd)
+
+    def _outputs(self, arrs, nd):
         out = []
         for c in range(self.ncams):
             self.results[c].r = self._res[c]

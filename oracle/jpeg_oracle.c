@@ -315,6 +315,15 @@ int oracle_jpeg_decode_bgr(const uint8_t *d, size_t n, uint8_t *out, int out_str
                     hh->bits[l] = s[o + l];
                     cnt += s[o + l];
                 }
+                if (cnt > 256) return -2;
+                /* jpeg_make_d_derived_tbl's JERR_BAD_HUFF_TABLE: code overflow, DC symbol > 15 */
+                for (int l = 1, code = 0; l <= 16; l++) {
+                    code += hh->bits[l];
+                    if (code >= (1 << l)) return -2;
+                    code <<= 1;
+                }
+                for (int i = 0; i < cnt; i++)
+                    if (tc == 0 && s[o + 17 + i] > 15) return -2;
                 for (int i = 0; i < cnt && i < 256; i++) hh->vals[i] = s[o + 17 + i];
                 hh->nvals = cnt;
                 hh->defined = 1;

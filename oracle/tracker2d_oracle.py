@@ -15,18 +15,17 @@ doubles (the reference's double math); cv::Point2f differences are float32.
 Only tests import this module.
 
 PARITY UNPINNED (the reference ships no tests or fixtures for this path). The
-assignment is the exhaustive minimum of the reference's cost (the reference's
-own CPSNWhere_Hungarian needs MSVC CRT functions, _isnanf / _finitef, and is
-not built here); where several assignments tie the reference's Munkres order
-is not reproduced.
+assignment restates the reference's own Munkres, CPSNWhere_Hungarian
+(oracle/munkres_oracle.py), so ties break in its order; that file is not
+compiled here (it needs the MSVC CRT's _isnanf / _finitef).
 """
 from __future__ import annotations
 
-import itertools
 import math
 
 import numpy as np
 
+import munkres_oracle
 import oracle as lk_oracle
 
 MIN_FEATURES = 4     # PSN_2D_FEATURE_MIN_NUM_TRACK (:12)
@@ -305,32 +304,9 @@ def forward_tracking(ring, trackers, dets):
 # ---------------------------------------------------------------------------
 
 def assign(cost: np.ndarray) -> list:
-    """:1040-1064: non-finite costs -> max(finite) + 100 (float32), a minimum
-    total-cost set of min(D, T) pairs (exhaustive), pairs at the substitute cost
-    dropped. Returns the tracker index per detection or -1."""
-    c = np.array(cost, np.float32, copy=True)
-    D, T = c.shape
-    if D == 0 or T == 0:
-        return [-1] * D
-    fin = c[np.isfinite(c)]
-    max_cost = np.float32(np.float32(fin.max() if fin.size and fin.max() > -1000.0 else -1000.0) + np.float32(100.0))
-    c[~np.isfinite(c)] = max_cost
-    best, best_pairs = None, None
-    if D <= T:
-        for perm in itertools.permutations(range(T), D):
-            tot = sum(float(c[d, perm[d]]) for d in range(D))
-            if best is None or tot < best:
-                best, best_pairs = tot, [(d, perm[d]) for d in range(D)]
-    else:
-        for perm in itertools.permutations(range(D), T):
-            tot = sum(float(c[perm[t], t]) for t in range(T))
-            if best is None or tot < best:
-                best, best_pairs = tot, [(perm[t], t) for t in range(T)]
-    match = [-1] * D
-    for d, t in best_pairs:
-        if c[d, t] != max_cost:
-            match[d] = t
-    return match
+    """:1040-1064 with the reference's Munkres (oracle/munkres_oracle.py): the
+    tracker index per detection or -1."""
+    return munkres_oracle.assign(cost)
 
 
 def result_with_tracker(tr: Tracker) -> dict:

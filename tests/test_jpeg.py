@@ -71,6 +71,57 @@ def test_jpeg_info_and_rejects():
         lk.JpegDecoder.info(prog)
 
 
+def _with_dht(data: bytes, tc_th: int, bits, vals) -> bytes:
+    """data with one more DHT segment right after SOI (parsed before the file's own)."""
+    body = bytes([tc_th]) + bytes(bits) + bytes(vals)
+    seg = b"\xff\xc4" + (len(body) + 2).to_bytes(2, "big") + body
+    return data[:2] + seg + data[2:]
+
+
+@pytest.mark.parametrize("case", ["two_1bit_codes", "overfull_1bit", "all_ones_3bit", "dc_symbol_200", "ac_overflow"])
+def test_jpeg_rejects_bad_huffman_tables(oracle_mod, case):
+    """jdhuff.c jpeg_make_d_derived_tbl's JERR_BAD_HUFF_TABLE cases: a canonical
+    code that overflows its length (would index past the 9-bit lookahead table),
+    and DC symbols above 15 (shifts of >= 16 bits in extend). Both the device
+    decoder's parser and the oracle refuse them (PSN_LK_ERR_ARG)."""
+    from mcmtt_opticalflow_amd import lk
+
+    _, data, _ = fixtures()[0]
+    z = [0] * 16
+    bad = {
+        "two_1bit_codes": (0x00, [2] + z[1:], [0, 1]),
+        "overfull_1bit": (0x00, [200] + z[1:], [0] * 200),  # the advisor's bits[0] = 200
+        "all_ones_3bit": (0x10, [0, 0, 8] + z[3:], list(range(8))),
+        "dc_symbol_200": (0x01, [0, 1] + z[2:], [200]),
+        "ac_overflow": (0x11, [0, 3, 3] + z[3:], [1, 2, 3, 4, 5, 6]),
+    }[case]
+    crafted = _with_dht(data, *bad)
+    with pytest.raises(lk.PsnLkError) as e:
+        lk.JpegDecoder.info(crafted)
+    assert e.value.code == -1  # PSN_LK_ERR_ARG
+    with pytest.raises(ValueError):
+        oracle_mod.jpeg_decode_bgr(crafted)
+    # a valid extra table (the JPEG standard's luminance DC table) is accepted
+    ok = _with_dht(data, 0x03, [0, 1, 5, 1, 1, 1, 1, 1, 1] + [0] * 7, list(range(12)))
+    assert lk.JpegDecoder.info(ok)[:2] == lk.JpegDecoder.info(data)[:2]
+
+
+def test_jpeg_rejects_440_sampling():
+    """4:4:0 (luma h1v2) has no upsampling path: refused as unsupported, never
+    decoded with the h2v2 rule."""
+    from mcmtt_opticalflow_amd import lk
+
+    pytest.importorskip("PIL")
+    data, _ = _pil_jpeg(np.zeros((32, 32, 3), np.uint8) + 90, quality=90, subsampling=0)
+    b = bytearray(data)
+    sof = b.find(b"\xff\xc0")
+    assert sof > 0 and b[sof + 11] == 0x11  # component 0's sampling byte (h=1, v=1)
+    b[sof + 11] = 0x12
+    with pytest.raises(lk.PsnLkError) as e:
+        lk.JpegDecoder.info(bytes(b))
+    assert e.value.code == -8  # PSN_LK_ERR_UNSUPPORTED
+
+
 # ------------------------------------------------------------------ GPU: device decoder
 
 @pytest.mark.gpu

@@ -257,11 +257,67 @@ def _rand_cost(rng, D, T):
     return c
 
 
+def _tie_cost(rng, D, T):
+    """Few distinct values (many tied optima), non-finite entries, whole rows /
+    columns without a finite entry."""
+    c = rng.integers(0, 3, (D, T)).astype(np.float32) * np.float32(0.5)
+    c[rng.random((D, T)) < 0.3] = np.inf
+    if D and rng.random() < 0.3:
+        c[int(rng.integers(0, D))] = np.inf
+    if T and rng.random() < 0.3:
+        c[:, int(rng.integers(0, T))] = -np.inf if rng.random() < 0.5 else np.inf
+    return c
+
+
+def test_hungarian_match_matches_oracle():
+    """psn_t2d_hungarian_match (C++) == oracle/munkres_oracle.py (Python), both
+    restating CPSNWhere_Hungarian::Match (helpers/PSNWhere_Hungarian.cpp:212-359):
+    same pairs in the same order, including the reference's tie order, its
+    FLT_MAX - sum infinity substitute, rows/columns without a finite entry
+    (condensed out) and the NaN early-out (:78-81)."""
+    import munkres_oracle as MO
+
+    rng = np.random.default_rng(5)
+    for trial in range(600):
+        D, T = int(rng.integers(0, 9)), int(rng.integers(0, 9))
+        c = _tie_cost(rng, D, T) if trial % 2 else _rand_cost(rng, D, T)
+        g = t2d.hungarian_match(c)
+        r = MO.hungarian_match(c)
+        assert (g[0], g[1]) == (r[0], r[1]), (trial, c, g, r)
+        assert np.array_equal(np.float32(g[2]), np.float32(r[2]))
+    nan = np.float32([[1, 2], [np.nan, 0]])
+    assert t2d.hungarian_match(nan) == ([], [], []) == MO.hungarian_match(nan)
+    assert t2d.hungarian_match(np.full((3, 2), np.inf, np.float32)) == ([], [], [])
+
+
+def test_hungarian_is_optimal_on_integer_costs():
+    """On finite integer-valued costs every float operation is exact, so the
+    Munkres restatements must reach the exhaustive minimum total cost."""
+    import itertools
+
+    import munkres_oracle as MO
+
+    rng = np.random.default_rng(9)
+    for trial in range(200):
+        D, T = int(rng.integers(1, 6)), int(rng.integers(1, 6))
+        c = rng.integers(0, 6, (D, T)).astype(np.float32)
+        rows, cols, costs = t2d.hungarian_match(c)
+        assert len(rows) == min(D, T) and len(set(rows)) == len(rows) and len(set(cols)) == len(cols)
+        best = min(sum(float(c[d, p[d]]) for d in range(D)) for p in itertools.permutations(range(T), D)) \
+            if D <= T else min(sum(float(c[p[t], t]) for t in range(T)) for p in itertools.permutations(range(D), T))
+        assert sum(costs) == best, (trial, c)
+        assert (rows, cols) == tuple(MO.hungarian_match(c)[:2])
+
+
 def test_assign_matches_oracle():
     rng = np.random.default_rng(31)
     for trial in range(400):
         D, T = int(rng.integers(0, 6)), int(rng.integers(0, 6))
         c = _rand_cost(rng, D, T)
+        assert t2d.assign(c) == ORC.assign(c), (trial, c)
+    for trial in range(300):  # tie-heavy, up to the headline's 8 x 8 (and beyond)
+        D, T = int(rng.integers(0, 13)), int(rng.integers(0, 13))
+        c = _tie_cost(rng, D, T)
         assert t2d.assign(c) == ORC.assign(c), (trial, c)
     # all infinite: every pair sits at the substitute cost, nothing matches
     assert t2d.assign(np.full((3, 2), np.inf, np.float32)) == [-1, -1, -1]
@@ -337,3 +393,21 @@ def test_matching_and_updating_matches_oracle():
             assert (go["id"], go["box"], go["head"], go["score"]) == (oo["id"], oo["box"], oo["head"], oo["score"])
             np.testing.assert_array_equal(go["prev"], oo["prev"])
             np.testing.assert_array_equal(go["curr"], oo["curr"])
+
+
+def test_matching_and_updating_rejects_repeated_tracker():
+    """A caller-supplied match must be an assignment: two detections on one
+    tracker would update and enqueue it twice (duplicate ids in the result)."""
+    rng = np.random.default_rng(3)
+    trk = [_rand_tracker(rng, 10 + i, 2)[0] for i in range(2)]
+    dets = []
+    for i in range(2):
+        d = t2d.make_detection((10.0 * i, 5.0, 40.0, 100.0), np.zeros((0, 2), np.float32))
+        f = np.float32([[1, 2], [3, 4], [5, 6], [7, 8]])
+        d.valid, d.num_boxes, d.num_sets, d.set_count[0] = 1, 1, 1, len(f)
+        ctypes.memmove(d.sets[0], f.ctypes.data, f.nbytes)
+        dets.append(d)
+    with pytest.raises(t2d.T2dError):
+        t2d.matching_and_updating(dets, trk, None, 3, 0, match=[1, 1])
+    t2d.matching_and_updating(dets, trk, None, 3, 0, match=[1, 0])
+    t2d.matching_and_updating(dets, trk, None, 3, 0, match=[-1, -1])

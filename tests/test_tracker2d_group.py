@@ -141,6 +141,43 @@ def test_group_ahead_protocol():
         g.complete()
 
 
+def test_group_next_frame_failure_keeps_frame():
+    """complete_next whose NEXT frame cannot launch (a 2-px-wide detection with 4
+    features: CV_Assert(winSize > 2)) still delivers this frame's results; the
+    next frame stays staged and a plain launch of it with valid detections gives
+    the results of an undisturbed run."""
+    W, H = 160, 120
+    imgs = [synth.texture(W, H, 3 + t) for t in range(3)]
+    good = [[[t2d.make_detection((10 + t, 10, 30, 60), np.float32([[20, 20], [25, 30], [30, 40], [22, 50]]))]]
+            for t in range(3)]
+    bad = [[t2d.make_detection((10, 10, 2, 30), np.float32([[11, 12], [11, 20], [11.5, 25], [11, 30]]))]]
+
+    def plain():
+        out = []
+        with t2d.Group(W, H, [0]) as g:
+            for t in range(3):
+                g.push_frame(0, imgs[t])
+                out.append(g.run(t, good[t])[0][1])
+        return out
+
+    ref = plain()
+    with t2d.Group(W, H, [0]) as g:
+        g.push_frame(0, imgs[0])
+        g.launch(0, good[0])
+        g.push_frame(0, imgs[1])
+        with pytest.raises(t2d.T2dError) as e:
+            g.complete_next(1, bad)
+        assert e.value.results is not None
+        r0 = e.value.results[0][1]
+        g.launch(1, good[1])  # frame 1 is still staged
+        r1 = g.complete()[0][1]
+        g.push_frame(0, imgs[2])
+        g.launch(2, good[2])
+        r2 = g.complete()[0][1]
+    for got, exp in zip([r0, r1, r2], ref):
+        _check_result(got, exp, "after a failed next-frame launch")
+
+
 def test_group_window_errors():
     """A detection whose box-width window the LK cannot run (2 px: CV_Assert(winSize > 2))
     fails the frame only when it has >= 4 features (:744)."""

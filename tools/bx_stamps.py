@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Phase clocks of the box-window LK kernel (lk_kernel_bx) from the diagnostic
 build (make -C mcmtt_opticalflow_amd/csrc stamps; run with
-PSN_LK_LIB=.../libpsn_lk_stamps.so). Tracker2D-like windows on the synthetic
+the stamps build, mcmtt_opticalflow_amd/lib/libpsn_lk_stamps.so). Tracker2D-like windows on the synthetic
 1080p scene, the reference's default criteria (30, 0.01), maxLevel 3.
 Prints per-workgroup mean / slowest cycles per phase (s_memtime ticks, thread
 0's view) and the serial-chain fraction of the iterations.
@@ -31,7 +31,7 @@ def main():
     sc = synth.make_scene(0, 1920, 1080, npts, nboxes=8)
     f0, f1 = sc.frame(0), sc.frame(1)
     pts = sc.points_at(1)
-    L = _lib.load()
+    L = _lib.load(_lib.STAMPS_LIB_PATH)
     st = hiprt.DeviceBuffer(npts * 64 * 8)
     with lk.LKContext(1920, 1080, ring_slots=2, max_level_cap=3) as ctx:
         ctx.push_frame(0, f0)

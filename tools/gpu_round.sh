@@ -8,7 +8,7 @@ O=gpurun_out/$R
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 && \
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && \
-PSN_LK_LIB=mcmtt_opticalflow_amd/lib/libpsn_lk_stamps.so WIN=64 WINH=64 NPTS=2048 timeout -k 10 120 python tools/bx_stamps.py > $O/st64.json 2>&1 && \
-PSN_LK_LIB=mcmtt_opticalflow_amd/lib/libpsn_lk_stamps.so WIN=64 WINH=160 NPTS=2048 timeout -k 10 120 python tools/bx_stamps.py > $O/st160.json 2>&1 && \
+WIN=64 WINH=64 NPTS=2048 timeout -k 10 120 python tools/bx_stamps.py > $O/st64.json 2>&1 && \
+WIN=64 WINH=160 NPTS=2048 timeout -k 10 120 python tools/bx_stamps.py > $O/st160.json 2>&1 && \
 (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $GRAFT_REPO_ROOT/$O/write -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-secondary > $GRAFT_REPO_ROOT/$O/write.log 2>&1)
 echo rc=$?

@@ -2,7 +2,7 @@
 """Phase breakdown of the LK kernel from in-kernel s_memtime stamps.
 
 Needs the diagnostic library (make -C mcmtt_opticalflow_amd/csrc stamps);
-run as PSN_LK_LIB=.../libpsn_lk_stamps.so python tools/lk_stamps.py.
+run as the stamps build, mcmtt_opticalflow_amd/lib/libpsn_lk_stamps.so python tools/lk_stamps.py.
 Stamps are shader-clock ticks; read the SHARES, not absolute time (stamping
 perturbs the kernel).
 """
@@ -30,7 +30,7 @@ def main():
     sc = synth.make_scene(0, 1920, 1080, npts)
     f0, f1 = sc.frame(0), sc.frame(1)
     pts = sc.points_at(0)
-    L = _lib.load()
+    L = _lib.load(_lib.STAMPS_LIB_PATH)
     st = hiprt.DeviceBuffer(npts * 64 * 8)
     with lk.LKContext(1920, 1080, ring_slots=2, max_level_cap=3) as ctx:
         ctx.push_frame(0, f0)
