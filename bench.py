@@ -1,40 +1,60 @@
 #!/usr/bin/env python3
 """Tracker2D benchmark (BASELINE.json metric) on MI355X.
 
-Default workload = BASELINE.json configs[2] on every GPU (north_star's target
+Default line = BASELINE.json configs[2] on every GPU (north_star's target
 shape, "4x1080p cameras with 512 tracked points/camera at 1 GPU"): C = 4
 cameras per rank, 1920x1080 BGR frames, 8 detections per camera (64x160 boxes,
 SURVEY 8(d)) with 64 feature points each (512 per camera; SURVEY 8(d) point
 recipe: uniform inside the boxes, seed 3000+cam), box-derived LK windows
-(64x64 backward, 64x160 forward), maxLevel 3.
+(64x64 backward, 64x160 forward), maxLevel 3. Per-GPU work is fixed as N grows
+(scaling "weak"), so SCALE's N=1 equals BENCH.
 
 One step = one frame of every camera through CPSNWhere_Tracker2D::Run
 (psn_where/PSNWhere_Tracker2D.cpp:251-373) as psn_t2d_group runs it:
   1. upload of frame t+1 of every camera from pinned host memory (copy engine)
      + BGR->gray + pyramid build, overlapping frame t's work (:256-263);
-  2. backward chains of every detection: 3 LK steps (64x64) with LocalSearchKLT
+  2. features of every detection: given (SURVEY 8(d) point recipe) or GridFAST
+     on the device (--features gridfast, :735-758);
+  3. backward chains of every detection: 3 LK steps (64x64) with LocalSearchKLT
      between them, all cameras in one launch per step (:763-811);
-  3. forward LK of every active tracker (64x160) + matching cost (:851-1025);
-  4. assignment, tracker update, ResultWithTracker (:1038-1164, :1231-1257);
-  5. every camera's stTrack2DResult packed into its binary slot in host memory.
-     Frames are pipelined as psn_t2d_group_complete_next allows: frame t+1's
-     backward chains are enqueued as soon as frame t's device work is done, and
-     run while the host does frame t's step 4-5 (same results as launch/complete);
+  4. forward LK of every active tracker (64x160) + matching cost (:851-1025);
+  5. the reference's Munkres assignment, tracker update, ResultWithTracker
+     (:1038-1164, :1231-1257);
+  6. every camera's stTrack2DResult packed into its binary slot in host memory;
      N > 1: one RCCL all-gather of the slots over xGMI (psn_comm_allgather, the
      hand-off into Associator3D, PSNWhere.cpp:264-269), landing in host memory.
-The timed region therefore runs from host frames to host results.
+Frames are pipelined as psn_t2d_group_complete_next allows (frame t+1's
+backward chains run while the host does frame t's steps 5-6; same results).
+The timed region runs from host frames to host results.
 
---mode kernel: the round-1 line, BASELINE.json configs[1] (1 camera, 512
-points, 21x21 window, frames resident in HBM), also reported as `secondary`.
+Modes and legs:
+  --total-cameras M   strong scaling, SURVEY 8(e): M cameras sharded over the
+                      ranks (configs[3]: --total-cameras 8 --points 2048
+                      --boxes 32; 8/4/2/1 cameras per GPU at N = 1/2/4/8).
+  --features gridfast the whole Run, GridFAST inside the timed region.
+  --verify            every frame's gathered result slots (warm-up and timed)
+                      checked against the oracle's CameraTracker replay of the
+                      same frames, after the timed region.
+  --mode kernel       BASELINE.json configs[1] (1 camera, 512 points, 21x21,
+                      frames resident in HBM); reported as `secondary`.
+  --mode config4      BASELINE.json configs[4]: 8 cameras sharded over the
+                      ranks, 3840x2160, 4096 points/camera, 21x21, 5 levels,
+                      SG(9, 1) post-filter of every point's trajectory.
+  At N = 1 the default line also carries `legs`: configs[3] on one GPU,
+  configs[4] on one GPU and the GridFAST Run (--no-legs skips them).
 
-Single GPU:  python bench.py --steps 100 --warmup 5
-Multi GPU:   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (one process per
+GPU, RANK/LOCAL_RANK/WORLD_SIZE set before anything touches a GPU); under
+torch.distributed.run the ranks come from the environment. --dry-run checks
+the launcher and the control plane without a GPU (gloo only).
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -44,7 +64,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Tracker2D frames/sec (all cameras) + achieved HBM GB/s fraction, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
-TIMING_EVERY = 8
+# VALU issue peak (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64 VALU
+# instruction per SIMD every 2 cycles (32 lanes per cycle) at 2.4 GHz
+N_SIMD, CLOCK_HZ = 256 * 4, 2.4e9
+VALU_PEAK_WAVE_INSTR = N_SIMD * CLOCK_HZ / 2.0
+OPS_PER_SAMPLE = 8  # ~8 integer ops per window sample per iteration
+DEFAULT_PROFILE = os.path.join(ROOT, "profiles", "r03_tracker_profile.json")
 
 
 def level_sizes(w, h, nlev):
@@ -86,39 +111,110 @@ def host_info():
     return info
 
 
-def cpu_threads():
-    """The host cores this run may use: the affinity set, capped by OMP_NUM_THREADS
-    when the box sets it (the GPU box allots 16 host cores per GPU)."""
+def cpu_share_threads():
+    """The host cores allotted to this GPU's job: the affinity set, capped by
+    OMP_NUM_THREADS when the box sets it (16 per GPU on the GPU box)."""
     n = len(os.sched_getaffinity(0))
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return min(n, omp) if omp > 0 else n
 
 
+def dist_env():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def file_sha16(path):
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 # ---------------------------------------------------------------------------
-# Tracker2D mode (default): configs[2] on every rank
+# Launcher: --gpus N without torch.distributed.run
 # ---------------------------------------------------------------------------
 
-import numpy as np  # noqa: E402
+def launch_ranks(args, argv):
+    """Start N rank processes of this script (one per GPU) before anything here
+    touches a GPU; rank 0's JSON line is the output. Non-zero if any rank fails."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # a failed rank: the others would wait for it forever
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return 1 if rc else 0
+
+
+def init_control_plane(world):
+    """Barriers, the RCCL id and max-over-ranks on gloo; the data plane is psn_comm (RCCL)."""
+    import torch.distributed as dist
+
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("gloo")
+
+
+def barrier(world):
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.barrier()
+
+
+# ---------------------------------------------------------------------------
+# Tracker2D workload (default line, configs[2] / configs[3], GridFAST, verify)
+# ---------------------------------------------------------------------------
+
+def cameras_of_rank(args, world, rank):
+    """Weak (cameras per GPU) or strong (--total-cameras sharded): the camera ids of this rank."""
+    if args.total_cameras:
+        if args.total_cameras % world:
+            raise SystemExit(f"--total-cameras {args.total_cameras} is not a multiple of {world} ranks")
+        c = args.total_cameras // world
+    else:
+        c = args.cameras
+    return [rank * c + k for k in range(c)]
 
 
 class CameraFeed:
     """One camera's synthetic video (mcmtt_opticalflow_amd/synth.py): BGR frames
-    in pinned host memory and, per frame, the detections (box, head box, 3D
-    estimate) with their feature points."""
+    (or JPEG files) in pinned host memory and, per frame, the detections (box,
+    head box, 3D estimate) with their feature points (given mode)."""
 
-    def __init__(self, cam, W, H, npts, nboxes, period, t2d, pinned, jpeg=False):
+    def __init__(self, cam, args, pinned):
         from mcmtt_opticalflow_amd import synth
 
-        self.scene = synth.make_scene(cam, W, H, npts, nboxes=nboxes)
-        self.period = period
+        W, H = args.width, args.height
+        self.scene = synth.make_scene(cam, W, H, args.points, nboxes=args.boxes)
+        self.period = args.period
+        self.gridfast = args.features == "gridfast"
         self.jpeg = None
-        if jpeg:  # the camera's frames as baseline JPEG files (PIL/libjpeg-turbo, q90, 4:2:0, a restart per MCU row)
+        if args.ingest == "jpeg":  # baseline JPEG files (PIL/libjpeg-turbo, q90, 4:2:0, a restart per MCU row)
             import io
 
             from PIL import Image
 
             self.jpeg = []
-            for t in range(period):
+            for t in range(self.period):
                 b = io.BytesIO()
                 Image.fromarray(synth.to_bgr(self.scene.frame(t))[..., ::-1]).save(
                     b, "JPEG", quality=90, subsampling=2, restart_marker_rows=1)
@@ -127,41 +223,46 @@ class CameraFeed:
                 self.jpeg.append(buf)
             self.frames = None
         else:
-            self.frames = [pinned((H, W, 3)) for _ in range(period)]
-            for t in range(period):
+            self.frames = [pinned((H, W, 3)) for _ in range(self.period)]
+            for t in range(self.period):
                 self.frames[t][...] = synth.to_bgr(self.scene.frame(t))
         self.boxes, self.feats = [], []
-        for t in range(period):
-            bx = [(float(int(x)), float(int(y)), float(self.scene.box_w), float(self.scene.box_h))
-                  for x, y in self.scene.box_at(t)]
+        for t in range(self.period):
+            self.boxes.append(detection_boxes(self.scene, t))
             pts = self.scene.points_at(t)
-            self.boxes.append(bx)
-            self.feats.append([pts[self.scene.pt_box == k] for k in range(nboxes)])
-        self.t2d = t2d
+            self.feats.append([pts[self.scene.pt_box == k] for k in range(args.boxes)])
 
-    def detections(self, t):
+    def detections(self, t2d, t):
         """Fresh records of frame t (the group writes its outputs into them)."""
         f = ping_pong(t, self.period)
         out = []
         for b, pts in zip(self.boxes[f], self.feats[f]):
-            head = (b[0] + b[2] / 4, b[1], b[2] / 2, b[3] / 8)
-            loc = ((b[0] + b[2] / 2) * 10.0, (b[1] + b[3]) * 10.0, 0.0)  # a ground-plane stand-in, mm
-            out.append(self.t2d.make_detection(b, pts, head=head, location=loc, height=1700.0))
+            head, loc, height = detection_extra(b)
+            out.append(t2d.make_detection(b, np.zeros((0, 2), np.float32) if self.gridfast else pts, head=head,
+                                          location=loc, height=height))
         return out
-
-    def frame(self, t):
-        return self.frames[ping_pong(t, self.period)]
 
     def push(self, group, k, t):
         """Camera k's frame t into the group (async upload of BGR, or JPEG bytes decoded on the device)."""
+        f = ping_pong(t, self.period)
         if self.jpeg is not None:
-            group.push_frame_jpeg(k, self.jpeg[ping_pong(t, self.period)])
+            group.push_frame_jpeg(k, self.jpeg[f])
         else:
-            group.push_frame(k, self.frame(t))
+            group.push_frame(k, self.frames[f])
+
+
+def detection_boxes(scene, f):
+    return [(float(int(x)), float(int(y)), float(scene.box_w), float(scene.box_h)) for x, y in scene.box_at(f)]
+
+
+def detection_extra(b):
+    """Head box (vecPartBoxes.front()), a ground-plane stand-in location (mm) and height."""
+    head = (b[0] + b[2] / 4, b[1], b[2] / 2, b[3] / 8)
+    loc = ((b[0] + b[2] / 2) * 10.0, (b[1] + b[3]) * 10.0, 0.0)
+    return head, loc, 1700.0
 
 
 def pinned_allocator():
-    import numpy as np
     import torch
 
     keep = []
@@ -172,218 +273,28 @@ def pinned_allocator():
         return t.numpy()
 
     alloc.keep = keep
-    _ = np
     return alloc
 
 
-def tracker_cpu_baseline(args, n_frames_cap=400):
-    """The oracle Tracker2D (oracle/tracker2d_oracle.py CameraTracker + oracle/lk_oracle.c)
-    on this host: the same synthetic cameras, detections and points, the
-    reference call schedule (every calcOpticalFlowPyrLK rebuilds both pyramids),
-    OpenMP over points as OpenCV's parallel_for_. Legs: the allotted host cores,
-    1 thread, and the shared-pyramid schedule at the allotted cores."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
+class LaunchTimes:
+    """Every LK launch of the timed region (HIP events on the stream each was
+    launched on), per kernel (psn_lk_timing_launches)."""
 
-    import oracle  # cpu_baseline leg only
-    import tracker2d_oracle as T2  # cpu_baseline leg only
-    from mcmtt_opticalflow_amd import synth
+    def __init__(self, L, lkh, cap):
+        self.L, self.h, self.cap = L, lkh, cap
+        L.psn_lk_enable_timing(lkh, cap, 1)
 
-    W, H, C = args.width, args.height, args.cameras
-    scenes = [synth.make_scene(c, W, H, args.points, nboxes=args.boxes) for c in range(C)]
-    grays = [[oracle.bgr2gray(synth.to_bgr(sc.frame(t))) for t in range(args.period)] for sc in scenes]
+    def read(self):
+        from mcmtt_opticalflow_amd import _lib
 
-    def leg(threads, shared, budget):
-        T2.NTHREADS, T2.SHARED_PYRAMIDS = threads, shared
-        cams = [T2.CameraTracker(c) for c in range(C)]
-        n, t0 = 0, None
-        for t in range(n_frames_cap + 2):
-            if t == 2:  # the ring holds frames: the steady state starts
-                t0 = time.perf_counter()
-            f = ping_pong(t, args.period)
-            for c, sc in enumerate(scenes):
-                bx = [T2.Rect(float(int(x)), float(int(y)), float(sc.box_w), float(sc.box_h)) for x, y in sc.box_at(f)]
-                pts = sc.points_at(f)
-                feats = [pts[sc.pt_box == k] for k in range(args.boxes)]
-                extra = [(T2.Rect(b.x + b.w / 4, b.y, b.w / 2, b.h / 8), ((b.x + b.w / 2) * 10.0, (b.y + b.h) * 10.0, 0.0),
-                          1700.0) for b in bx]
-                cams[c].run(grays[c][f], bx, feats, t, extra)
-                if t >= 2:
-                    n += 1
-            if t0 is not None and time.perf_counter() - t0 >= budget:
-                break
-        dt = time.perf_counter() - t0
-        T2.NTHREADS, T2.SHARED_PYRAMIDS = 0, False
-        return n / dt, n, dt
-
-    threads = cpu_threads()
-    v, n, dt = leg(threads, False, args.cpu_budget)
-    v1, n1, dt1 = leg(1, False, args.cpu_budget / 2)
-    vs, ns, dts = leg(threads, True, args.cpu_budget / 2)
-    hi = host_info()
-    return {"value": round(v, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} camera-frames ({C} cameras x {n // C} frames, {dt:.1f} s) of the same workload "
-                      "(1080p BGR->gray, 8 detections x 64 points, box windows, backward chains + forward + "
-                      "matching) through oracle/tracker2d_oracle.py + oracle/lk_oracle.c, OpenMP over points, "
-                      "reference call schedule (both pyramids rebuilt in every calcOpticalFlowPyrLK)",
-            "single_thread": round(v1, 4), "single_thread_sample": f"{n1} camera-frames, {dt1:.1f} s",
-            "shared_pyramid": round(vs, 4), "shared_pyramid_sample": f"{ns} camera-frames, {dts:.1f} s, {threads} threads",
-            "cores_note": "threads = the host cores this GPU's job is allotted (the box sets OMP_NUM_THREADS to its "
-                          "per-GPU CPU share; nproc counts the whole machine)",
-            **hi}
-
-
-def tracker_main(args):
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
-    from mcmtt_opticalflow_amd import _lib
-    from mcmtt_opticalflow_amd import dist as pdist
-    from mcmtt_opticalflow_amd import tracker2d as t2d
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:  # control plane (barriers, the RCCL id, max-over-ranks) on gloo; data plane on psn_comm (RCCL)
-        dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
-    W, H, C = args.width, args.height, args.cameras
-    cams = [rank * C + k for k in range(C)]
-    L = _lib.load()
-    pinned = pinned_allocator()
-    feeds = [CameraFeed(c, W, H, args.points, args.boxes, args.period, t2d, pinned, jpeg=args.ingest == "jpeg")
-             for c in cams]
-    max_obj = 2 * args.boxes
-    group = t2d.Group(W, H, cams, device=local_rank, max_objects=max_obj)
-    slot_bytes = t2d.result_slot_bytes(max_obj, 1)
-    send = pinned((C, slot_bytes))
-    exch = pdist.ResultExchange(world, rank, C * slot_bytes, device=local_rank) if world > 1 else None
-    T = t2d.load()
-
-    def step(t, dets, next_dets):
-        group.launch(t, dets)  # after complete_next(t-1): a confirmation (frame t is in flight)
-        for k, fd in enumerate(feeds):  # frame t+1 uploads while frame t runs
-            fd.push(group, k, t + 1)
-        if next_dets is None:
-            group.complete_raw()
-        else:  # frame t+1's chains go to the GPU before the host matches frame t
-            group.complete_next(t + 1, next_dets, raw=True)
-        for k in range(C):  # the hand-off slots (psn_t2d_pack_result) in host memory
-            rc = T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
-            if rc:
-                raise t2d.T2dError(rc, "psn_t2d_pack_result")
-        return exch.allgather(send) if exch else send
-
-    def all_dets(t):
-        return [fd.detections(t) for fd in feeds]
-
-    for k, fd in enumerate(feeds):
-        fd.push(group, k, 0)
-    t = 0
-    dets_warm = [all_dets(t + i) for i in range(args.warmup)]
-    # records built outside the timed region; one more frame: the last timed step launches its chains
-    # ahead, as the warm-up's last step did for the first timed frame (the timed region holds exactly
-    # `steps` frames' backward chains and forward calls)
-    dets_timed = [all_dets(args.warmup + i) for i in range(args.steps + 1)]
-    seq = [group.records(d) for d in dets_warm + dets_timed]  # ctypes records, built before timing
-    for i in range(args.warmup):
-        step(t, seq[i], seq[i + 1] if i + 1 < len(seq) else None)
-        t += 1
-    lkh = group.lk_handle()
-    L.psn_lk_enable_timing(lkh, 16 * args.steps + 64, 1)  # every LK launch (forward + 3 chain steps)
-    sampler = SampleCounter(L, lkh)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        j = args.warmup + i
-        gathered = step(t, seq[j], seq[j + 1])
-        t += 1
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = pdist.max_over_ranks(elapsed)
-    ts = {}
-    np_, nt, pm, tm = ctypes.c_int(), ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
-    L.psn_lk_timing_stats(lkh, ctypes.byref(np_), ctypes.byref(pm), ctypes.byref(nt), ctypes.byref(tm))
-    ts = {"n_track": nt.value, "track_ms": tm.value, "n_push": np_.value, "push_ms": pm.value}
-    samples = sampler.read()
-    # the gathered hand-off of the last frame: every camera's result, index == camID
-    objs_last = 0
-    if rank == 0:
-        rows = np.asarray(gathered).reshape(world * C, slot_bytes)
-        for cam in range(world * C):
-            r = t2d.unpack_result(rows[cam], max_obj, 1)
-            assert r["cam_id"] == cam and r["frame_idx"] == t - 1, (cam, r["cam_id"], r["frame_idx"])
-            objs_last += len(r["objects"])
-    group.close()
-    if exch:
-        exch.close()
-
-    fps_all = world * C * args.steps / elapsed
-    per_gpu_fps = C * args.steps / elapsed
-    pyr_b, lk_b = algorithmic_bytes(W, H, 4, args.points, c_in=3)
-    frame_b = pyr_b + lk_b
-    cam_frames_rank = C * args.steps
-    lk_ms_cf = ts["track_ms"] / cam_frames_rank  # LK kernel time per camera-frame (all launches, HIP events)
-    lk_gbps = lk_b / (lk_ms_cf * 1e-3) / 1e9 if lk_ms_cf > 0 else 0.0
-    out = None
-    if rank == 0:
-        pmc = tracker_traffic(args.tracker_pmc_summary, cam_frames_per_set=C)
-        out = {
-            "metric": METRIC, "value": round(fps_all, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
-            "config": {
-                "workload": (f"BASELINE.json configs[2] per GPU: {C} cameras x 1920x1080 BGR, {args.boxes} detections/camera "
-                             f"(64x160 boxes) x {args.points // args.boxes} points = {args.points} tracked points/camera, "
-                             "CPSNWhere_Tracker2D::Run: async H2D ingest from pinned host + BGR->gray + pyramid, "
-                             "3-step backward chains (64x64 windows, LocalSearchKLT on device), forward LK (64x160) "
-                             "+ matching cost, assignment + tracker update + ResultWithTracker, packed result slots "
-                             "in host memory" + (", RCCL all-gather of the slots (psn_comm)" if world > 1 else ""))
-                if (W, H, C, args.points, args.boxes) == (1920, 1080, 4, 512, 8) else
-                f"Tracker2D Run, {C} cameras/GPU, {W}x{H}, {args.boxes} detections x {args.points // args.boxes} points",
-                "cameras": world * C, "cameras_per_gpu": C, "width": W, "height": H, "points_per_camera": args.points,
-                "detections_per_camera": args.boxes, "box": [64, 160], "levels": 4,
-                "win_backward": [64, 64], "win_forward": [64, 160],
-                "ingest": ("baseline JPEG files in host memory (q90 4:2:0, restart per MCU row), decoded on the device"
-                           if args.ingest == "jpeg" else "BGR frames in pinned host memory"),
-                "parallelism": f"{C} cameras-per-GPU x{world} (camera-sharded, RCCL all-gather of result slots)"},
-            "roofline": {
-                "kernel": "lk_kernel_bx (every LK launch of a frame-set: forward + 3 chain steps)",
-                "bound": "hbm", "limiter": "latency / VALU (ordered float chains of the box-window sums)",
-                "achieved": round(lk_gbps, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(lk_gbps / HBM_PEAK_GBPS, 6),
-                "traffic": pmc, "traffic_unit": "HBM bytes per camera-frame over all LK launches (PMC)",
-                "traffic_source": os.path.relpath(args.tracker_pmc_summary, ROOT) if pmc else None,
-                "bytes_per_camera_frame": lk_b,
-                "bytes_note": "SURVEY 8(d) LK bytes 2*S_pyr + 21*N per camera-frame over the summed LK launch time",
-                "lk_ms_per_camera_frame": round(lk_ms_cf, 5), "lk_launches": ts["n_track"]},
-            "frame_level": {"algorithmic_bytes_per_camera_frame": frame_b,
-                            "bytes_formula": "SURVEY 8(d) c_in*S0 + 4*S_pyr - S_top + 21*N, c_in = 3 (BGR)",
-                            "achieved_GBps_per_gpu": round(frame_b * per_gpu_fps / 1e9, 3),
-                            "hbm_fraction": round(frame_b * per_gpu_fps / 1e9 / HBM_PEAK_GBPS, 6)},
-            "compute": {"window_samples_per_camera_frame": round(samples / cam_frames_rank) if samples else None,
-                        "gsamples_per_s_per_gpu": round(samples / cam_frames_rank * per_gpu_fps / 1e9, 3)
-                        if samples else None,
-                        "definition": "SURVEY 8(d): sum over points and levels of w*h*(1 + iterations), "
-                                      "counted on the device"},
-            "frames_per_set_per_s": round(args.steps / elapsed, 2),
-            "result_objects_last_frame": objs_last,
-            "cpu_baseline": None,
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = tracker_cpu_baseline(args)
-            out["speedup_vs_cpu"] = round(fps_all / out["cpu_baseline"]["value"], 1)
-            out["speedup_vs_cpu_shared_pyramid"] = round(fps_all / out["cpu_baseline"]["shared_pyramid"], 1)
-        if world == 1 and not args.no_secondary:
-            out["secondary"] = kernel_secondary(args)
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        per = {}
+        for ms, tag in _lib.timing_launches(self.L, self.h, self.cap):
+            k = _lib.kernel_of_tag(tag)
+            n, tot = per.get(k, (0, 0.0))
+            per[k] = (n + 1, tot + ms)
+        np_, nt, pm, tm = ctypes.c_int(), ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+        self.L.psn_lk_timing_stats(self.h, ctypes.byref(np_), ctypes.byref(pm), ctypes.byref(nt), ctypes.byref(tm))
+        return per, {"n_track": nt.value, "track_ms": tm.value}
 
 
 class SampleCounter:
@@ -402,30 +313,392 @@ class SampleCounter:
         return v.value if rc == 0 else None
 
 
-def tracker_traffic(path, cam_frames_per_set):
-    """PMC HBM bytes per camera-frame over every LK launch of a profiled default run
-    (tools/pmc_summary.py output; pyramid_kernel dispatches count camera-frames)."""
+def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
+    """The Tracker2D workload on this rank: warm-up, `steps` timed frames. Returns
+    the measurements (rank 0: with the gathered results of every frame when
+    args.verify)."""
+    import torch
+
+    from mcmtt_opticalflow_amd import _lib
+    from mcmtt_opticalflow_amd import dist as pdist
+    from mcmtt_opticalflow_amd import tracker2d as t2d
+
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    warmup = max(warmup, 1)  # the first step launches the frame the next one completes
+    torch.cuda.set_device(local_rank)
+    cams = cameras_of_rank(args, world, rank)
+    C = len(cams)
+    gridfast = args.features == "gridfast"
+    L = _lib.load()
+    pinned = pinned_allocator()
+    feeds = [CameraFeed(c, args, pinned) for c in cams]
+    max_obj = 2 * args.boxes
+    group = t2d.Group(args.width, args.height, cams, device=local_rank, max_objects=max_obj)
+    slot_bytes = t2d.result_slot_bytes(max_obj, 1)
+    send = pinned((C, slot_bytes))
+    exch = pdist.ResultExchange(world, rank, C * slot_bytes, device=local_rank) if world > 1 else None
+    T = t2d.load()
+    recorded = [] if args.verify else None
+
+    def step(t, dets, next_dets):
+        group.launch(t, dets, gridfast=gridfast, seed=t)  # after complete_next(t-1): a confirmation
+        for k, fd in enumerate(feeds):  # frame t+1 uploads while frame t runs
+            fd.push(group, k, t + 1)
+        group.complete_next(t + 1, next_dets, gridfast=gridfast, seed=t + 1, raw=True)
+        for k in range(C):  # the hand-off slots (psn_t2d_pack_result) in host memory
+            rc = T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
+            if rc:
+                raise t2d.T2dError(rc, "psn_t2d_pack_result")
+        g = exch.allgather(send) if exch else send
+        if recorded is not None:
+            recorded.append(np.array(g, copy=True).reshape(-1))
+        return g
+
+    def all_dets(t):
+        return [fd.detections(t2d, t) for fd in feeds]
+
+    for k, fd in enumerate(feeds):
+        fd.push(group, k, 0)
+    # ctypes records of every frame, built outside the timed region; one more
+    # frame than completed: the last step launches its successor ahead, as the
+    # warm-up's last step did for the first timed frame
+    seq = [group.records(all_dets(t)) for t in range(warmup + steps + 1)]
+    t = 0
+    for i in range(warmup):
+        step(t, seq[i], seq[i + 1])
+        t += 1
+    lkh = group.lk_handle()
+    launches = LaunchTimes(L, lkh, 8 * steps + 64)  # every LK launch (forward + 3 chain steps)
+    sampler = SampleCounter(L, lkh)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        j = warmup + i
+        gathered = step(t, seq[j], seq[j + 1])
+        t += 1
+    torch.cuda.synchronize()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    elapsed = pdist.max_over_ranks(elapsed)
+    per_kernel, ts = launches.read()
+    samples = sampler.read()
+    # feature points of the last completed frame (GridFAST mode: what GridFAST kept)
+    arrs, _, nd = seq[warmup + steps - 1]
+    pts_last = sum(int(arrs[c][i].num_features) for c in range(C) for i in range(nd[c])) / C
+    objs_last = 0
+    if rank == 0:  # the gathered hand-off of the last frame: every camera's result, index == camID
+        rows = np.asarray(gathered).reshape(-1, slot_bytes)
+        for cam in range(rows.shape[0]):
+            r = t2d.unpack_result(rows[cam], max_obj, 1)
+            assert r["cam_id"] == cam and r["frame_idx"] == t - 1, (cam, r["cam_id"], r["frame_idx"])
+            objs_last += len(r["objects"])
+    group.close()
+    if exch:
+        exch.close()
+    return {"elapsed": elapsed, "steps": steps, "warmup": warmup, "cams_per_rank": C, "world": world,
+            "per_kernel": per_kernel, "ts": ts, "samples": samples, "objs_last": objs_last,
+            "points_per_camera": pts_last, "recorded": recorded, "slot_bytes": slot_bytes, "max_obj": max_obj}
+
+
+def verify_tracker(args, r):
+    """Every recorded frame's gathered result slots against the oracle's
+    CameraTracker (oracle/tracker2d_oracle.py: the reference schedule, the
+    reference's Munkres) replayed over the same frames, detections and points
+    (GridFAST mode: the oracle's GridFAST with the same seeds). Outside the
+    timed region; checker only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # verify leg only: the checker
+    import tracker2d_oracle as T2  # verify leg only: the checker
+    from mcmtt_opticalflow_amd import synth
+    from mcmtt_opticalflow_amd import tracker2d as t2d
+
+    ncam = r["world"] * r["cams_per_rank"]
+    frames = len(r["recorded"])
+    T2.NTHREADS, T2.SHARED_PYRAMIDS = cpu_share_threads(), True
+    W, H = args.width, args.height
+    mism, checked, objects, first = 0, 0, 0, None
+    for cam in range(ncam):
+        sc = synth.make_scene(cam, W, H, args.points, nboxes=args.boxes)
+        ref = T2.CameraTracker(cam_id=cam)
+        jpeg = {}
+        for t in range(frames):
+            f = ping_pong(t, args.period)
+            bgr = synth.to_bgr(sc.frame(f))
+            if args.ingest == "jpeg":  # the bench's JPEG files, decoded by the oracle
+                if f not in jpeg:
+                    import io
+
+                    from PIL import Image
+
+                    b = io.BytesIO()
+                    Image.fromarray(bgr[..., ::-1]).save(b, "JPEG", quality=90, subsampling=2, restart_marker_rows=1)
+                    jpeg[f] = oracle.jpeg_decode_bgr(b.getvalue())
+                bgr = jpeg[f]
+            gray = oracle.bgr2gray(bgr)
+            boxes = detection_boxes(sc, f)
+            if args.features == "gridfast":
+                rois = []
+                for b in boxes:
+                    x, y = max(0.0, b[0]), max(0.0, b[1])
+                    rois.append((int(x), int(y), int(min(W - x - 1, b[2])), int(min(H - y - 1, b[3]))))
+                feats, _ = oracle.gridfast_detect(gray, rois, seed=t)
+            else:
+                pts = sc.points_at(f)
+                feats = [pts[sc.pt_box == k] for k in range(args.boxes)]
+            extra = [(T2.Rect(*h), loc, hh) for h, loc, hh in (detection_extra(b) for b in boxes)]
+            _, _, exp = ref.run(gray, [T2.Rect(*b) for b in boxes], feats, t, extra)
+            row = r["recorded"][t].reshape(-1, r["slot_bytes"])[cam]
+            got = t2d.unpack_result(row, r["max_obj"], 1)
+            ok = (got["cam_id"], got["frame_idx"], len(got["objects"])) == (exp["cam_id"], exp["frame_idx"],
+                                                                           len(exp["objects"]))
+            for go, eo in zip(got["objects"], exp["objects"]):
+                ok = ok and (go["id"], go["box"], go["head"], go["score"]) == (eo["id"], eo["box"], eo["head"],
+                                                                              eo["score"])
+                ok = ok and np.array_equal(go["prev"], eo["prev"]) and np.array_equal(go["curr"], eo["curr"])
+            checked += 1
+            objects += len(exp["objects"])
+            if not ok:
+                mism += 1
+                first = first or {"camera": cam, "frame": t}
+    T2.NTHREADS, T2.SHARED_PYRAMIDS = 0, False
+    return {"frames": frames, "cameras": ncam, "camera_frames_checked": checked, "objects_checked": objects,
+            "mismatches": mism, "first_mismatch": first,
+            "compared": "every frame's packed stTrack2DResult (ids, boxes, heads, scores, featurePointsPrev/Curr) "
+                        "bit for bit against oracle/tracker2d_oracle.py CameraTracker.run"}
+
+
+def tracker_cpu_baseline(args, n_frames_cap=400):
+    """The oracle Tracker2D (oracle/tracker2d_oracle.py CameraTracker + oracle/lk_oracle.c)
+    on this host: the same synthetic cameras, detections and points, the
+    reference call schedule (every calcOpticalFlowPyrLK rebuilds both pyramids),
+    OpenMP over points and over the rows of the full-frame passes. Legs: the
+    cores allotted to this GPU, 1 thread, all cores, and the shared-pyramid
+    schedule at the allotted cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # cpu_baseline leg only
+    import tracker2d_oracle as T2  # cpu_baseline leg only
+    from mcmtt_opticalflow_amd import synth
+
+    W, H, C = args.width, args.height, args.cameras
+    scenes = [synth.make_scene(c, W, H, args.points, nboxes=args.boxes) for c in range(C)]
+    grays = [[oracle.bgr2gray(synth.to_bgr(sc.frame(t))) for t in range(args.period)] for sc in scenes]
+
+    def leg(threads, shared, budget):
+        T2.NTHREADS, T2.SHARED_PYRAMIDS = threads, shared
+        cams = [T2.CameraTracker(c) for c in range(C)]
+        n, t0 = 0, None
+        for t in range(n_frames_cap + 2):
+            if t == 2:  # the ring holds frames: the steady state starts
+                t0 = time.perf_counter()
+            f = ping_pong(t, args.period)
+            for c, sc in enumerate(scenes):
+                boxes = detection_boxes(sc, f)
+                pts = sc.points_at(f)
+                feats = [pts[sc.pt_box == k] for k in range(args.boxes)]
+                extra = [(T2.Rect(*h), loc, hh) for h, loc, hh in (detection_extra(b) for b in boxes)]
+                cams[c].run(grays[c][f], [T2.Rect(*b) for b in boxes], feats, t, extra)
+                if t >= 2:
+                    n += 1
+            if t0 is not None and time.perf_counter() - t0 >= budget:
+                break
+        dt = time.perf_counter() - t0
+        T2.NTHREADS, T2.SHARED_PYRAMIDS = 0, False
+        return n / dt, n, dt
+
+    share, allc = cpu_share_threads(), len(os.sched_getaffinity(0))
+    v, n, dt = leg(share, False, args.cpu_budget)
+    v1, n1, dt1 = leg(1, False, args.cpu_budget / 2)
+    va, na, dta = leg(allc, False, args.cpu_budget / 2)
+    vs, ns, dts = leg(share, True, args.cpu_budget / 2)
+    return {"value": round(v, 4), "unit": "frames/s", "cores": share, "kind": "port",
+            "sample": f"{n} camera-frames ({C} cameras x {n // C} frames, {dt:.1f} s) of the same workload "
+                      "(1080p BGR->gray, 8 detections x 64 points, box windows, backward chains + forward + "
+                      "Munkres matching) through oracle/tracker2d_oracle.py + oracle/lk_oracle.c, OpenMP over "
+                      "points and over the rows of every pyramid/border/Scharr pass, reference call schedule "
+                      "(both pyramids rebuilt in every calcOpticalFlowPyrLK)",
+            "single_thread": round(v1, 4), "single_thread_sample": f"{n1} camera-frames, {dt1:.1f} s",
+            "all_cores": round(va, 4), "all_cores_threads": allc, "all_cores_sample": f"{na} camera-frames, {dta:.1f} s",
+            "shared_pyramid": round(vs, 4), "shared_pyramid_sample": f"{ns} camera-frames, {dts:.1f} s, {share} threads",
+            "cores_note": "cores = the host cores this GPU's job is allotted (the box sets OMP_NUM_THREADS to its "
+                          "per-GPU CPU share); all_cores = every core of the affinity set (the whole machine)",
+            **host_info()}
+
+
+def load_profile(path):
+    """A round profile summary (tools/profile_summary.py): per kernel the rocprofv3
+    kernel-trace mean duration, PMC HBM bytes (FETCH/WRITE, corrected per the
+    guide's HBM section) and SQ counters per launch, plus the sha of the profiled
+    libpsn_lk.so."""
     if not path or not os.path.exists(path):
         return None
-    ks = json.load(open(path)).get("kernels", {})
-    frames = ks.get("pyramid_kernel", {}).get("dispatches", 0)
-    lk = [v for k, v in ks.items() if k.startswith("lk_kernel")]
-    if not frames or not lk:
+    try:
+        return json.load(open(path))
+    except ValueError:
         return None
-    return int(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in lk) / frames)
+
+
+def tracker_roofline(args, r, C, profile):
+    """Roofline of the dominant LK kernel (largest share of the timed LK time),
+    per launch: SURVEY 8(d) LK bytes per camera-frame (2*S_pyr + 21*N) x the C
+    camera-frames one launch processes, over the launch's mean HIP-event duration;
+    VALU issue from the profile's SQ_INSTS_VALU per launch over the same duration."""
+    from mcmtt_opticalflow_amd import _lib
+
+    _, lk_b = algorithmic_bytes(args.width, args.height, 4, args.points)
+    per = r["per_kernel"]
+    if not per:
+        return None
+    name, (n, tot) = max(per.items(), key=lambda kv: kv[1][1])
+    avg_ms = tot / n
+    launch_b = C * lk_b
+    ach = launch_b / (avg_ms * 1e-3) / 1e9
+    out = {"kernel": name, "bound": "valu",
+           "achieved": round(ach, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 6),
+           "traffic": None, "bytes_per_launch": launch_b, "avg_launch_us": round(1e3 * avg_ms, 2),
+           "launches_timed": n,
+           "bytes_note": f"SURVEY 8(d) LK bytes 2*S_pyr + 21*N = {lk_b} per camera-frame x {C} camera-frames per "
+                         "launch; achieved/peak/frac are the HBM roofline of this kernel (contract fields)",
+           "per_kernel_us": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
+                                 "ms_per_step": round(v[1] / r["steps"], 4)} for k, v in sorted(per.items())}}
+    lib_sha = file_sha16(_lib.LIB_PATH)
+    if profile:
+        pk = profile.get("kernels", {}).get(name, {})
+        out["traffic"] = pk.get("hbm_bytes_per_launch")
+        out["profile"] = os.path.relpath(args.profile, ROOT)
+        out["profile_lib_sha16"] = profile.get("lib_sha16")
+        out["lib_sha16"] = lib_sha
+        out["profile_matches_binary"] = profile.get("lib_sha16") == lib_sha
+        out["profile_avg_launch_us"] = pk.get("avg_us")
+        vi = pk.get("SQ_INSTS_VALU")
+        if vi:
+            issue = vi / (avg_ms * 1e-3)
+            v = {"achieved": round(issue / 1e9, 2), "peak": round(VALU_PEAK_WAVE_INSTR / 1e9, 2),
+                 "unit": "G wave64-VALU-instructions/s", "frac": round(issue / VALU_PEAK_WAVE_INSTR, 4),
+                 "instructions_per_launch": int(vi),
+                 "peak_note": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
+            # useful lane work of every LK launch of a frame-set vs the lane slots they issued
+            lk_vi = sum(kv.get("SQ_INSTS_VALU", 0) * per.get(k, (0, 0))[0]
+                        for k, kv in profile.get("kernels", {}).items() if k.startswith("lk_kernel")) / r["steps"]
+            if r["samples"] and lk_vi:
+                useful = r["samples"] / r["steps"] * OPS_PER_SAMPLE
+                v["useful_lane_frac"] = round(useful / (lk_vi * 64), 4)
+                v["useful_note"] = (f"SURVEY 8(d) window samples x {OPS_PER_SAMPLE} ops per frame-set / "
+                                    "(SQ_INSTS_VALU of every LK launch per frame-set x 64 lanes)")
+            for key in ("SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+                if key in pk:
+                    v[key + "_per_launch"] = int(pk[key])
+            out["valu"] = v
+    return out
+
+
+def tracker_line(args, r, world, C, scaling, profile):
+    """The JSON line of a Tracker2D run (rank 0)."""
+    fps_all = world * C * r["steps"] / r["elapsed"]
+    per_gpu_fps = C * r["steps"] / r["elapsed"]
+    pyr_b, lk_b = algorithmic_bytes(args.width, args.height, 4, args.points, c_in=3)
+    frame_b = pyr_b + lk_b
+    cam_frames = C * r["steps"]
+    cfg3 = (args.total_cameras == 8 and args.points == 2048)
+    what = ("BASELINE.json configs[3]" if cfg3 else "BASELINE.json configs[2] per GPU"
+            if (args.width, args.height, args.cameras, args.points, args.boxes) == (1920, 1080, 4, 512, 8)
+            and not args.total_cameras else "Tracker2D Run")
+    out = {
+        "metric": METRIC, "value": round(fps_all, 2), "unit": "frames/s", "n_gpus": world, "steps": r["steps"],
+        "warmup": r["warmup"], "ms_per_step": round(1e3 * r["elapsed"] / r["steps"], 5), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
+        "config": {
+            "workload": (f"{what}: {world * C} cameras ({C} per GPU) x {args.width}x{args.height} "
+                         f"{'JPEG' if args.ingest == 'jpeg' else 'BGR'}, {args.boxes} detections/camera (64x160 "
+                         f"boxes) x " + ("GridFAST features (<= 100 each)" if args.features == "gridfast" else
+                                         f"{args.points // args.boxes} points = {args.points} tracked points/camera")
+                         + ", CPSNWhere_Tracker2D::Run: async H2D ingest + BGR->gray + pyramid, 3-step backward "
+                         "chains (64x64 windows, LocalSearchKLT on device), forward LK (64x160) + matching cost, "
+                         "Munkres + tracker update + ResultWithTracker, packed result slots in host memory"
+                         + (", RCCL all-gather of the slots (psn_comm)" if world > 1 else "")),
+            "cameras": world * C, "cameras_per_gpu": C, "width": args.width, "height": args.height,
+            "points_per_camera": args.points if args.features == "given" else round(r["points_per_camera"], 1),
+            "features": args.features, "detections_per_camera": args.boxes, "box": [64, 160], "levels": 4,
+            "win_backward": [64, 64], "win_forward": [64, 160],
+            "ingest": ("baseline JPEG files in host memory (q90 4:2:0, restart per MCU row), decoded on the device"
+                       if args.ingest == "jpeg" else "BGR frames in pinned host memory"),
+            "parallelism": f"camera-sharded x{world} ({C} cameras per GPU), RCCL all-gather of result slots"},
+        "roofline": tracker_roofline(args, r, C, profile),
+        "frame_level": {"algorithmic_bytes_per_camera_frame": frame_b,
+                        "bytes_formula": "SURVEY 8(d) c_in*S0 + 4*S_pyr - S_top + 21*N, c_in = 3 (BGR)",
+                        "achieved_GBps_per_gpu": round(frame_b * per_gpu_fps / 1e9, 3),
+                        "hbm_fraction": round(frame_b * per_gpu_fps / 1e9 / HBM_PEAK_GBPS, 6),
+                        "lk_ms_per_step": round(r["ts"]["track_ms"] / r["steps"], 4)},
+        "compute": {"window_samples_per_camera_frame": round(r["samples"] / cam_frames) if r["samples"] else None,
+                    "gsamples_per_s_per_gpu": round(r["samples"] / cam_frames * per_gpu_fps / 1e9, 3)
+                    if r["samples"] else None,
+                    "definition": "SURVEY 8(d): sum over points and levels of w*h*(1 + iterations), "
+                                  "counted on the device"},
+        "frames_per_set_per_s": round(r["steps"] / r["elapsed"], 2),
+        "result_objects_last_frame": r["objs_last"],
+        "cpu_baseline": None,
+    }
+    return out
+
+
+def tracker_main(args):
+    world, rank, local_rank = dist_env()
+    init_control_plane(world)
+    profile = load_profile(args.profile)
+    r = tracker_run(args, world, rank, local_rank)
+    C = r["cams_per_rank"]
+    out = None
+    if rank == 0:
+        out = tracker_line(args, r, world, C, "strong" if args.total_cameras else "weak", profile)
+        if args.verify:
+            out["verify"] = verify_tracker(args, r)
+            out["verify"]["note"] = "the timed loop copied each step's gathered slots (a few KB) for this check"
+        if world == 1 and not args.no_cpu_baseline and not args.total_cameras:
+            out["cpu_baseline"] = tracker_cpu_baseline(args)
+            out["speedup_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+            out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["all_cores"], 1)
+    if world == 1 and not args.no_legs and not args.total_cameras and not args.verify:
+        out["legs"] = tracker_legs(args, profile)
+    if world == 1 and not args.no_secondary:
+        out["secondary"] = kernel_secondary(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+def tracker_legs(args, profile):
+    """Extra single-GPU lines of the default run: configs[3] on one GPU (8 cameras
+    x 2048 points, the strong-scaling run's N=1), the GridFAST Run, configs[4]."""
+    legs = {}
+    a3 = argparse.Namespace(**{**vars(args), "total_cameras": 8, "points": 2048, "boxes": 32, "verify": False})
+    r3 = tracker_run(a3, steps=args.leg_steps, warmup=3)
+    l3 = tracker_line(a3, r3, 1, 8, "strong", None)
+    legs["configs3_1gpu"] = {k: l3[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
+    legs["configs3_1gpu"]["roofline"] = {k: l3["roofline"].get(k) for k in ("kernel", "achieved", "frac",
+                                                                            "avg_launch_us", "per_kernel_us")}
+    ag = argparse.Namespace(**{**vars(args), "features": "gridfast", "verify": False})
+    rg = tracker_run(ag, steps=args.leg_steps, warmup=3)
+    lg = tracker_line(ag, rg, 1, args.cameras, "weak", None)
+    legs["gridfast"] = {k: lg[k] for k in ("value", "unit", "ms_per_step", "steps", "config")}
+    legs["config4"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3)["line"]
+    return legs
 
 
 # ---------------------------------------------------------------------------
-# Kernel mode: BASELINE.json configs[1] (the round-1 headline, kept as secondary)
+# Kernel modes: configs[1] (secondary) and configs[4] (4K, 5 levels, SG)
 # ---------------------------------------------------------------------------
 
 def kernel_cpu_baseline(scene, period, npts, win, max_level, budget_s, max_frames):
     """The oracle (reference call schedule: both pyramids + Scharr rebuilt in
-    every calcOpticalFlowPyrLK call) on this host's cores."""
+    every calcOpticalFlowPyrLK call) on this host's allotted cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # cpu_baseline leg only
 
-    threads = cpu_threads()
+    threads = cpu_share_threads()
     frames = [scene.frame(t) for t in range(period)]
     pts = scene.points_at(0)
     oracle.calc_optical_flow_pyr_lk(frames[0], frames[1], pts, win, max_level, nthreads=threads)  # warm
@@ -439,23 +712,24 @@ def kernel_cpu_baseline(scene, period, npts, win, max_level, budget_s, max_frame
             break
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} camera-frames of the same workload (1920x1080, {npts} pts, 21x21, 4 levels), "
-                      f"oracle/lk_oracle.c with OpenMP over points, {dt:.1f} s", **host_info()}
+            "sample": f"{n} camera-frames of the same workload ({scene.width}x{scene.height}, {npts} pts, "
+                      f"{win[0]}x{win[1]}, {max_level + 1} levels), oracle/lk_oracle.c with OpenMP, {dt:.1f} s",
+            **host_info()}
 
 
-def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0):
-    """configs[1]-style LK step: frames resident in HBM, C cameras per GPU, 21x21."""
-    import numpy as np
+def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, H=1080, N=512, levels=4,
+               sg=False):
+    """LK step over frames resident in HBM: C cameras per GPU, 21x21, `levels`
+    pyramid levels; sg: SG(9, 1) Insert of every tracked point's position per
+    frame (status as the active mask), on the same stream."""
     import torch
 
     from mcmtt_opticalflow_amd import dist as pdist
     from mcmtt_opticalflow_amd import lk, synth
 
     device = torch.device("cuda", local_rank)
-    C = max(1, args.kcameras)
     cams = [rank * C + k for k in range(C)]
-    W, H, N, Lv, win = args.width, args.height, args.kpoints, 4, 21
-    R = 4
+    win, R = 21, 4
     scenes = [synth.make_scene(c, W, H, N) for c in cams]
     frames = []
     for sc in scenes:
@@ -465,7 +739,7 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0):
         frames.append(f)
     stream = torch.cuda.Stream(device)
     torch.cuda.set_stream(stream)
-    ctx = lk.LKContext(W, H, ring_slots=R * C, max_level_cap=Lv - 1, device=local_rank)
+    ctx = lk.LKContext(W, H, ring_slots=R * C, max_level_cap=levels - 1, device=local_rank)
     ctx.set_stream(stream.cuda_stream)
     mode = 2 if C == 1 else 1
     ctx.set_ingest_overlap(mode)
@@ -476,7 +750,13 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0):
         hdr.copy_(torch.tensor([[c, 0, N, 0] for c in cams], dtype=torch.int32).view(hdr.shape))
     views[0][1].copy_(torch.from_numpy(np.concatenate([sc.points_at(0) for sc in scenes])))
     gathered = torch.empty((world, sb), dtype=torch.uint8, device=device)
-    params = lk.make_params((win, win), Lv - 1)
+    params = lk.make_params((win, win), levels - 1)
+    smoother = None
+    if sg:
+        smoother = lk.SGSmoother(C * N, 2, 9, 1, device=local_rank)
+        smoother.set_stream(stream.cuda_stream)
+        sg_ref = torch.empty(C * N, dtype=torch.int32, device=device)
+        sg_out = torch.empty((C * N, 9, 2), dtype=torch.float64, device=device)
 
     def push(t):
         for k in range(C):
@@ -492,6 +772,8 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0):
         cur, prv = views[t % 2], views[(t - 1) % 2]
         push(t + 1)
         ctx.track_device(queries[t % R], prv[1].data_ptr(), cur[1].data_ptr(), cur[3].data_ptr(), cur[2].data_ptr())
+        if smoother is not None:  # lost points (status 0) are not inserted
+            smoother.insert_device(cur[1].data_ptr(), 2, cur[3].data_ptr(), sg_ref.data_ptr(), sg_out.data_ptr())
         (cur[0][:, 1] if C > 1 else cur[0][1]).fill_(t)
         if world > 1:
             pdist.allgather_slots(slots[t % 2], world, out=gathered)
@@ -500,7 +782,7 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0):
     for _ in range(warmup):
         step(t)
         t += 1
-    ctx.enable_timing(steps + 1, TIMING_EVERY)
+    ctx.enable_timing(steps + 1, 1)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -510,8 +792,10 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0):
     elapsed = time.perf_counter() - t0
     ts = ctx.timing_stats()
     ctx.close()
+    if smoother is not None:
+        smoother.close()
     torch.cuda.set_stream(torch.cuda.default_stream(device))
-    pyr_b, lk_b = algorithmic_bytes(W, H, Lv, N)
+    pyr_b, lk_b = algorithmic_bytes(W, H, levels, N)
     lk_us = 1e3 * ts["track_ms"] / max(ts["n_track"], 1)
     launch_b = C * lk_b + (pyr_b if mode == 2 else 0)
     return {"fps": C * steps / elapsed, "ms_per_step": 1e3 * elapsed / steps, "lk_us": lk_us,
@@ -520,51 +804,82 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0):
 
 
 def kernel_secondary(args):
-    r = kernel_run(args, 400, 20)
+    r = kernel_run(args, 400, 20, C=max(1, args.kcameras), N=args.kpoints)
     ach = r["launch_bytes"] / (r["lk_us"] * 1e-6) / 1e9
     return {"workload": "BASELINE.json configs[1]: 1 camera, 1920x1080 gray resident in HBM, 512 points, 4 levels, "
                         "21x21 window, fused pyramid build + LK + propagation",
             "value": round(r["fps"], 2), "unit": "frames/s", "ms_per_step": round(r["ms_per_step"], 5),
-            "roofline": {"kernel": "lk_kernel_st+fused_pyramid", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 5), "bytes_per_launch": r["launch_bytes"],
-                         "avg_launch_us": round(r["lk_us"], 3)}}
+            "roofline": {"kernel": "lk_kernel_st+fused_pyramid", "bound": "latency", "achieved": round(ach, 2),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 5),
+                         "bytes_per_launch": r["launch_bytes"], "avg_launch_us": round(r["lk_us"], 3)}}
 
 
-def kernel_main(args):
+def config4_run(args, world, rank, local_rank, steps, warmup):
+    """BASELINE.json configs[4]: 8 cameras sharded over the ranks (strong), 3840x2160,
+    4096 points/camera, 21x21, 5 levels (maxLevel 4), SG(9, 1) post-filter of every
+    tracked point's trajectory (CPSNWhere_SGSmooth, PSNWhere_SGSmooth.cpp:198-274)."""
+    total = 8
+    if total % world:
+        raise SystemExit(f"configs[4] shards 8 cameras: {world} ranks do not divide them")
+    C = total // world
+    W, H, N, levels = 3840, 2160, 4096, 5
+    r = kernel_run(args, steps, warmup, world, rank, local_rank, C=C, W=W, H=H, N=N, levels=levels, sg=True)
     import torch
-    import torch.distributed as dist
 
     from mcmtt_opticalflow_amd import dist as pdist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    elapsed = pdist.max_over_ranks(r["elapsed"], torch.device("cuda", local_rank))
+    fps_all = total * steps / elapsed
+    ach = r["launch_bytes"] / (r["lk_us"] * 1e-6) / 1e9
+    line = {"workload": f"BASELINE.json configs[4]: {total} cameras ({C} per GPU) x 3840x2160 gray resident in HBM, "
+                        f"{N} points/camera, 21x21, 5 levels, SG(9,1) post-filter of every point trajectory",
+            "value": round(fps_all, 2), "unit": "frames/s", "n_gpus": world, "steps": steps,
+            "ms_per_step": round(1e3 * elapsed / steps, 5), "scaling": "strong",
+            "roofline": {"kernel": "lk_kernel_st (all cameras in one launch) + sg_insert_kernel", "bound": "latency",
+                         "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBPS, 5), "bytes_per_launch": r["launch_bytes"],
+                         "avg_launch_us": round(r["lk_us"], 3)}}
+    return {"line": line, "fps": fps_all, "elapsed": elapsed}
+
+
+def kernel_main(args):
+    world, rank, local_rank = dist_env()
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
-        dist.barrier()
-    r = kernel_run(args, args.steps, args.warmup, world, rank, local_rank)
-    elapsed = pdist.max_over_ranks(r["elapsed"], device)
+    if world > 1:  # the slots are device tensors: RCCL (nccl backend) for the all-gather and the timing max
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if args.mode == "config4":
+        res = config4_run(args, world, rank, local_rank, args.steps, args.warmup)
+        if rank == 0:
+            line = res["line"]
+            out = {"metric": METRIC, "value": line["value"], "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                   "warmup": args.warmup, "ms_per_step": line["ms_per_step"], "higher_is_better": True,
+                   "scaling": "strong", "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
+                   "config": {"workload": line["workload"], "cameras": 8, "cameras_per_gpu": 8 // world},
+                   "roofline": line["roofline"], "cpu_baseline": None}
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     C = max(1, args.kcameras)
+    r = kernel_run(args, args.steps, args.warmup, world, rank, local_rank, C=C, N=args.kpoints)
+    from mcmtt_opticalflow_amd import dist as pdist
+
+    elapsed = pdist.max_over_ranks(r["elapsed"], torch.device("cuda", local_rank))
     fps_all = world * C * args.steps / elapsed
     if rank == 0:
         ach = r["launch_bytes"] / (r["lk_us"] * 1e-6) / 1e9
-        traffic = None
-        if args.pmc_summary and os.path.exists(args.pmc_summary):
-            ks = json.load(open(args.pmc_summary)).get("kernels", {})
-            if "lk_kernel_st" in ks:
-                traffic = ks["lk_kernel_st"]["hbm_bytes_per_launch"]
         out = {"metric": METRIC, "value": round(fps_all, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 5), "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
-               "config": {"workload": f"BASELINE.json configs[1] shape: {C} camera(s) per GPU, {args.width}x{args.height} "
+               "config": {"workload": f"BASELINE.json configs[1] shape: {C} camera(s) per GPU, 1920x1080 "
                                       f"gray resident in HBM, {args.kpoints} points, 4 levels, 21x21 window",
                           "cameras": world * C, "cameras_per_gpu": C, "parallelism": f"camera-per-GPU x{world}"},
-               "roofline": {"kernel": "lk_kernel_st" + ("+fused_pyramid" if r["mode"] == 2 else ""), "bound": "hbm",
-                            "limiter": "latency (serial iteration chains)",
+               "roofline": {"kernel": "lk_kernel_st" + ("+fused_pyramid" if r["mode"] == 2 else ""), "bound": "latency",
                             "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                            "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                            "frac": round(ach / HBM_PEAK_GBPS, 5), "traffic": None,
                             "bytes_per_launch": r["launch_bytes"], "avg_launch_us": round(r["lk_us"], 3)},
                "cpu_baseline": None}
         if world == 1 and not args.no_cpu_baseline:
@@ -576,34 +891,87 @@ def kernel_main(args):
         dist.destroy_process_group()
 
 
-def main():
+# ---------------------------------------------------------------------------
+# Dry run: the launcher and the control plane without a GPU
+# ---------------------------------------------------------------------------
+
+def dry_main(args):
+    """No GPU work: every rank joins the gloo control plane, shards the cameras as the
+    real run would, times an empty loop with the barrier + max-over-ranks protocol;
+    rank 0 prints the line's shape (n_gpus, cameras per rank, scaling)."""
+    world, rank, _ = dist_env()
+    init_control_plane(world)
+    import torch.distributed as dist
+
+    from mcmtt_opticalflow_amd import dist as pdist
+
+    cams = cameras_of_rank(args, world, rank)
+    barrier(world)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    barrier(world)
+    elapsed = pdist.max_over_ranks(time.perf_counter() - t0)
+    all_cams = [None] * world
+    if world > 1:
+        dist.all_gather_object(all_cams, cams)
+    else:
+        all_cams = [cams]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": None, "dry_run": True,
+                          "scaling": "strong" if args.total_cameras else "weak",
+                          "cameras_by_rank": all_cams, "elapsed_max_over_ranks": round(elapsed, 4)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["tracker", "kernel"], default="tracker")
+    ap.add_argument("--mode", choices=["tracker", "kernel", "config4"], default="tracker")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--cameras", type=int, default=4, help="tracker mode: cameras per GPU (configs[2]: 4)")
+    ap.add_argument("--total-cameras", type=int, default=0,
+                    help="strong scaling: this many cameras sharded over the ranks (configs[3]: 8)")
     ap.add_argument("--points", type=int, default=512, help="tracker mode: feature points per camera")
     ap.add_argument("--boxes", type=int, default=8, help="tracker mode: detections per camera")
+    ap.add_argument("--features", choices=["given", "gridfast"], default="given",
+                    help="tracker mode: points given (SURVEY 8(d) recipe) or GridFAST on the device")
     ap.add_argument("--ingest", choices=["bgr", "jpeg"], default="bgr",
                     help="tracker mode: frames arrive as BGR arrays (default) or as JPEG files (device decode)")
+    ap.add_argument("--verify", action="store_true", help="check every frame's results against the oracle")
     ap.add_argument("--kcameras", type=int, default=1, help="kernel mode: cameras per GPU")
     ap.add_argument("--kpoints", type=int, default=512, help="kernel mode: points per camera")
     ap.add_argument("--period", type=int, default=10)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--leg-steps", type=int, default=40)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--tracker-pmc-summary", default=os.path.join(ROOT, "profiles", "r02k_tracker_pmc_summary.json"),
-                    help="PMC FETCH/WRITE_SIZE summary of a default (tracker) run, for roofline.traffic")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r02k_kernel_mode_pmc_summary.json"),
-                    help="PMC summary of a kernel-mode run, for roofline.traffic")
-    args = ap.parse_args()
-    if args.mode == "kernel":
-        return kernel_main(args)
+    ap.add_argument("--no-legs", action="store_true")
+    ap.add_argument("--dry-run", action="store_true")
+    ap.add_argument("--profile", default=DEFAULT_PROFILE,
+                    help="round profile summary (tools/profile_summary.py) for roofline.traffic / valu")
+    args = ap.parse_args(argv)
     if args.points % args.boxes:
         raise SystemExit("--points must be a multiple of --boxes")
+    return args
+
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
+    if args.dry_run:
+        return dry_main(args)
+    if args.mode in ("kernel", "config4"):
+        return kernel_main(args)
     return tracker_main(args)
 
 

@@ -181,6 +181,12 @@ int psn_lk_level_size(psn_lk_ctx *ctx, int level, int *w, int *h);
  * milliseconds, and resets. */
 int psn_lk_enable_timing(psn_lk_ctx *ctx, int capacity, int every);
 int psn_lk_timing_stats(psn_lk_ctx *ctx, int *n_push, double *push_ms, int *n_track, double *track_ms);
+/* Per timed track call since psn_lk_enable_timing (before psn_lk_timing_stats,
+ * which resets the counts): its duration in ms (HIP events on the stream it
+ * was launched on) and the kernel it ran: tag = 10 * UPT + (no-tail build) for
+ * lk_kernel_bx<UPT, no-tail>, 1 = lk_kernel_st, 2 = lk_kernel (row-tiled).
+ * *n = the calls written (<= cap). */
+int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *n);
 
 /* Kernel-variant selection for tests and experiments (never read from the
  * environment: a product context always runs the planner's choice). Applies

@@ -95,6 +95,25 @@ _lib = None
 _lib_path = None
 
 
+def timing_launches(L, ctx, cap: int):
+    """psn_lk_timing_launches -> list of (ms, tag) per timed LK call."""
+    ms = (ctypes.c_double * max(cap, 1))()
+    tag = (ctypes.c_int * max(cap, 1))()
+    n = ctypes.c_int()
+    rc = L.psn_lk_timing_launches(ctx, cap, ms, tag, ctypes.byref(n))
+    if rc != 0:
+        raise PsnLkError(rc, "psn_lk_timing_launches")
+    return [(ms[i], tag[i]) for i in range(n.value)]
+
+
+def kernel_of_tag(tag: int) -> str:
+    if tag == 1:
+        return "lk_kernel_st"
+    if tag == 2:
+        return "lk_kernel"
+    return f"lk_kernel_bx<{tag // 10}, {'true' if tag % 10 else 'false'}>"
+
+
 def load(path: str | None = None):
     """The product library (mcmtt_opticalflow_amd/lib/libpsn_lk.so). Only the
     profiling tools pass path (STAMPS_LIB_PATH), before anything else loads it."""
@@ -144,6 +163,8 @@ def load(path: str | None = None):
     L.psn_lk_enable_timing.argtypes = [vp, ip, ip]
     L.psn_lk_timing_stats.argtypes = [vp, ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ip), ctypes.POINTER(ctypes.c_double)]
+    L.psn_lk_timing_launches.argtypes = [vp, ip, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ip),
+                                         ctypes.POINTER(ip)]
     L.psn_lk_debug_set_stamps.argtypes = [vp, vp]
     L.psn_lk_debug_count_samples.argtypes = [vp, ip]
     L.psn_lk_debug_read_samples.argtypes = [vp, ctypes.POINTER(ctypes.c_ulonglong)]

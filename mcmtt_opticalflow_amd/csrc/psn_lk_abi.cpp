@@ -92,6 +92,7 @@ struct psn_lk_ctx {
     // timing: event ring, 2 events per timed call
     int tcap = 0;
     std::vector<hipEvent_t> ev_push, ev_track;
+    std::vector<int> track_tag;            // per timed track call: the kernel it ran (psn_lk_timing_launches)
     long n_push = 0, n_track = 0;          // timed calls
     long calls_push = 0, calls_track = 0;  // all calls since enable_timing
     int every = 1;                         // time every `every`-th call of each kind
@@ -318,6 +319,7 @@ int psn_lk_enable_timing(psn_lk_ctx *c, int capacity, int every) {
         for (auto &e : *v) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     }
     c->tcap = capacity;
+    c->track_tag.assign((size_t)capacity, 0);
     c->every = every;
     c->n_push = c->n_track = 0;
     c->calls_push = c->calls_track = 0;
@@ -350,6 +352,21 @@ int psn_lk_timing_stats(psn_lk_ctx *c, int *n_push, double *push_ms, int *n_trac
     if (track_ms) *track_ms = tm;
     c->n_push = c->n_track = 0;
     c->calls_push = c->calls_track = 0;
+    return PSN_LK_OK;
+}
+
+int psn_lk_timing_launches(psn_lk_ctx *c, int cap, double *ms, int *tag, int *n) {
+    if (!c || cap < 0 || !n || (cap > 0 && (!ms || !tag))) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const long k = std::min<long>(std::min<long>(c->n_track, c->tcap), cap);
+    for (long i = 0; i < k; i++) {
+        HIPCHK(c, hipEventSynchronize(c->ev_track[2 * i + 1]));
+        float t = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&t, c->ev_track[2 * i], c->ev_track[2 * i + 1]));
+        ms[i] = t;
+        tag[i] = c->track_tag[(size_t)i];
+    }
+    *n = (int)k;
     return PSN_LK_OK;
 }
 
@@ -733,6 +750,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                 lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw).total);
             }
             HIPCHK(c, psn::launch_lk_bx(a, wgs, upt_bx, bx_notail, lds_bx, c->stream));
+            if (timed) c->track_tag[(size_t)ti] = 10 * upt_bx + (bx_notail ? 1 : 0);
             continue;
         }
         if (!all_single) {  // the generic kernel runs every query of this launch: re-plan its LDS
@@ -749,6 +767,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             }
         }
         HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, all_single, c->stream));
+        if (timed) c->track_tag[(size_t)ti] = all_single ? 1 : 2;
         if (fused_slot >= 0) {  // readers on other streams wait for the launch that built it
             HIPCHK(c, hipEventRecord(c->slot_ready[fused_slot], c->stream));
             c->ready_rec[fused_slot] = 1;

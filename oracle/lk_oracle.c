@@ -365,12 +365,20 @@ void oracle_bgr2gray(const uint8_t *src, int w, int h, int sstride, uint8_t *dst
 /* pyrDown_<FixPtCast<uchar,8>> [OCV246 imgproc/src/pyramids.cpp]: separable
  * [1 4 6 4 1]^2, (sum + 128) >> 8, reflect-101 on the SOURCE size. Integer,
  * so the row ring buffer / SSE2 vecOp order is immaterial. */
+/* Threads of the full-frame passes (pyrDown, borders, Scharr) inside one
+ * calcOpticalFlowPyrLK call (cpu_baseline legs: they scale with the cores as
+ * the points do); set per call, 1 outside. Integer row passes: the thread
+ * count cannot change a result. */
+static int g_rows_threads = 1;
+#define ROWS_PAR _Pragma("omp parallel for schedule(static) num_threads(g_rows_threads) if(g_rows_threads > 1)")
+
 void oracle_pyr_down(const uint8_t *src, int sw, int sh, int sstride, uint8_t *dst, int dstride) {
     static const int k[5] = {1, 4, 6, 4, 1};
     int dw = (sw + 1) / 2, dh = (sh + 1) / 2;
     int *cx = (int *)malloc(sizeof(int) * 5 * dw);
     for (int x = 0; x < dw; x++)
         for (int j = 0; j < 5; j++) cx[x * 5 + j] = oracle_refl101(2 * x + j - 2, sw);
+    ROWS_PAR
     for (int y = 0; y < dh; y++) {
         const uint8_t *rows[5];
         for (int i = 0; i < 5; i++) rows[i] = src + (long)oracle_refl101(2 * y + i - 2, sh) * sstride;
@@ -391,9 +399,9 @@ void oracle_pyr_down(const uint8_t *src, int sw, int sh, int sstride, uint8_t *d
  * pass with reflect-101 rows, horizontal pass with reflect-101 columns of the
  * filtered rows; interleaved int16 (Ix, Iy). */
 void oracle_scharr(const uint8_t *src, int w, int h, int sstride, int16_t *dst, int dstride) {
-    int *t0 = (int *)malloc(sizeof(int) * (w + 2));
-    int *t1 = (int *)malloc(sizeof(int) * (w + 2));
+    ROWS_PAR
     for (int y = 0; y < h; y++) {
+        int *t0 = (int *)malloc(sizeof(int) * 2 * (w + 2)), *t1 = t0 + w + 2;
         const uint8_t *s0 = src + (long)(y > 0 ? y - 1 : h > 1 ? 1 : 0) * sstride;
         const uint8_t *s1 = src + (long)y * sstride;
         const uint8_t *s2 = src + (long)(y < h - 1 ? y + 1 : h > 1 ? h - 2 : 0) * sstride;
@@ -411,9 +419,8 @@ void oracle_scharr(const uint8_t *src, int w, int h, int sstride, int16_t *dst, 
             d[2 * x] = (int16_t)(t0[x + 2] - t0[x]);
             d[2 * x + 1] = (int16_t)((t1[x + 2] + t1[x]) * 3 + t1[x + 1] * 10);
         }
+        free(t0);
     }
-    free(t0);
-    free(t1);
 }
 
 /* buildOpticalFlowPyramid's stop rule [OCV246 video/src/lkpyramid.cpp]: after
@@ -480,6 +487,7 @@ static void pad_reflect(const uint8_t *src, int cols, int rows, int bw, int bh, 
     int dcols = cols + 2 * bw;
     int *tab = (int *)malloc(sizeof(int) * dcols);
     for (int x = 0; x < dcols; x++) tab[x] = oracle_refl101(x - bw, cols);
+    ROWS_PAR
     for (int y = 0; y < rows + 2 * bh; y++) {
         const uint8_t *s = src + (long)oracle_refl101(y - bh, rows) * cols;
         uint8_t *d = dst + (long)y * dcols;
@@ -493,7 +501,8 @@ static void pad_reflect(const uint8_t *src, int cols, int rows, int bw, int bh, 
 /* Scharr of `src` into a zero-bordered interleaved int16 buffer. */
 static void scharr_padded(const uint8_t *src, int cols, int rows, int bw, int bh, int16_t *dst) {
     int dcols = cols + 2 * bw;
-    memset(dst, 0, sizeof(int16_t) * 2 * (size_t)dcols * (rows + 2 * bh));
+    ROWS_PAR
+    for (int y = 0; y < rows + 2 * bh; y++) memset(dst + (long)y * 2 * dcols, 0, sizeof(int16_t) * 2 * (size_t)dcols);
     oracle_scharr(src, cols, rows, cols, dst + ((long)bh * dcols + bw) * 2, 2 * dcols);
 }
 
@@ -762,6 +771,7 @@ int oracle_lk_track_pyr(const uint8_t *prev_pyr, const uint8_t *next_pyr, int w,
 #else
     (void)nthreads;
 #endif
+    g_rows_threads = nthreads;
     for (int level = max_level; level >= 0; level--) {
         int cols, rows;
         oracle_level_size(w, h, level, &cols, &rows);
@@ -779,7 +789,7 @@ int oracle_lk_track_pyr(const uint8_t *prev_pyr, const uint8_t *next_pyr, int w,
         {
             int16_t *ibuf = (int16_t *)malloc(sizeof(int16_t) * 3 * (size_t)win_w * win_h);
 #ifdef _OPENMP
-#pragma omp for schedule(dynamic, 4)
+#pragma omp for schedule(dynamic, 1)
 #endif
             for (int i = 0; i < npts; i++)
                 lk_point_level(&lv, level, max_level, prev_pts, next_pts, status, err, i, win_w, win_h,
@@ -790,6 +800,7 @@ int oracle_lk_track_pyr(const uint8_t *prev_pyr, const uint8_t *next_pyr, int w,
     free(Ipad);
     free(Jpad);
     free(Dpad);
+    g_rows_threads = 1;
     return 0;
 }
 
@@ -804,8 +815,12 @@ int oracle_calc_optical_flow_pyr_lk(const uint8_t *prev_img, const uint8_t *next
     int ml = oracle_effective_max_level(w, h, win_w, win_h, max_level);
     long total = oracle_level_offset(w, h, ml + 1);
     uint8_t *pp = (uint8_t *)malloc((size_t)total), *np = (uint8_t *)malloc((size_t)total);
+#ifdef _OPENMP
+    g_rows_threads = nthreads > 0 ? nthreads : omp_get_max_threads();
+#endif
     oracle_build_pyramid(prev_img, w, h, stride, ml + 1, pp);
     oracle_build_pyramid(next_img, w, h, stride, ml + 1, np);
+    g_rows_threads = 1;
     int rc = oracle_lk_track_pyr(pp, np, w, h, prev_pts, next_pts, status, err, npts, win_w, win_h, ml,
                                  term_type, max_count, epsilon, flags, min_eig_threshold, accum_mode,
                                  nthreads);

@@ -82,36 +82,24 @@ def local_search_klt(pre_box: Rect, pre: np.ndarray, cur: np.ndarray):
     pre = np.asarray(pre, np.float32).reshape(-1, 2)
     cur = np.asarray(cur, np.float32).reshape(-1, 2)
     n = len(pre)
-    moving, idx, dxs, dys = [], [], [], []
-    for i in range(n):
-        d = cur[i] - pre[i]  # cv::Point2f - cv::Point2f (float32)
-        mx, my = float(d[0]), float(d[1])
-        if math.sqrt(mx * mx + my * my) < 0.1 * SCALE:
-            continue
-        moving.append((mx, my))
-        idx.append(i)
-        dxs.append(mx)
-        dys.append(my)
-    m = len(moving)
+    # vectors as doubles of the float32 differences (cv::Point2f - cv::Point2f),
+    # each step elementwise IEEE double as the reference's scalar loops
+    d = (cur - pre).astype(np.float64)
+    keep = ~(np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) < 0.1 * SCALE)  # :481
+    idx = np.nonzero(keep)[0]
+    moving = d[idx]
+    m = len(idx)
     if float(m) < float(n) * 0.5:
         return Rect(*pre_box.tuple()), []
-    dxs.sort()
-    dys.sort()
+    dxs, dys = np.sort(moving[:, 0]), np.sort(moving[:, 1])
     window = pre_box.w * 0.2 * SCALE
-    max_x = max_y = 0
-    ex = ey = 0.0
-    for d in range(m):
-        nx = sum(1 for c in range(m) if abs(dxs[d] - dxs[c]) < window)
-        ny = sum(1 for c in range(m) if abs(dys[d] - dys[c]) < window)
-        if max_x < nx:
-            ex, max_x = dxs[d], nx
-        if max_y < ny:
-            ey, max_y = dys[d], ny
-    inl = []
-    for v in range(m):
-        vx, vy = moving[v][0] - ex, moving[v][1] - ey
-        if math.sqrt(vx * vx + vy * vy) < window:
-            inl.append(idx[v])
+    # neighbour counts within the window (:505-537); the first maximum wins (strict <)
+    nx = (np.abs(dxs[:, None] - dxs[None, :]) < window).sum(1)
+    ny = (np.abs(dys[:, None] - dys[None, :]) < window).sum(1)
+    ex = float(dxs[int(np.argmax(nx))]) if m and nx.max() > 0 else 0.0
+    ey = float(dys[int(np.argmax(ny))]) if m and ny.max() > 0 else 0.0
+    v = moving - np.array([ex, ey])
+    inl = idx[np.sqrt(v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) < window].tolist()  # :540-546
     box = Rect(*pre_box.tuple())
     box.x += ex
     box.y += ey

@@ -1,0 +1,54 @@
+"""The headline workload itself under oracle parity: bench.py's own Tracker2D
+run (BASELINE.json configs[2] per GPU: 1920x1080 BGR, 4 cameras, 8 detections
+x 64 points, box windows, frames pipelined by psn_t2d_group_complete_next,
+packed result slots), every frame's stTrack2DResult of every camera compared
+bit for bit with oracle/tracker2d_oracle.py's CameraTracker replay of the same
+frames (the reference schedule of CPSNWhere_Tracker2D::Run,
+psn_where/PSNWhere_Tracker2D.cpp:251-373, with the reference's Munkres).
+Also the GridFAST Run and JPEG ingest, and configs[3]'s per-GPU shape.
+Parity with OpenCV itself is unpinned."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+pytestmark = pytest.mark.gpu
+
+
+def _verify(*argv, steps, warmup):
+    import bench
+
+    args = bench.parse_args(["--verify", "--no-legs", "--no-secondary", "--no-cpu-baseline", *argv])
+    r = bench.tracker_run(args, steps=steps, warmup=warmup)
+    v = bench.verify_tracker(args, r)
+    assert v["frames"] == steps + warmup
+    return v
+
+
+def test_headline_configs2_matches_oracle(oracle_mod):
+    v = _verify(steps=3, warmup=2)
+    assert v["cameras"] == 4 and v["camera_frames_checked"] == 20
+    assert v["mismatches"] == 0, v["first_mismatch"]
+    assert v["objects_checked"] >= 4 * 8 * 4  # every detection is reported every frame
+
+
+def test_headline_gridfast_matches_oracle(oracle_mod):
+    v = _verify("--features", "gridfast", "--cameras", "2", steps=2, warmup=2)
+    assert v["mismatches"] == 0, v["first_mismatch"]
+    assert v["objects_checked"] > 0
+
+
+def test_headline_jpeg_ingest_matches_oracle(oracle_mod):
+    pytest.importorskip("PIL")
+    v = _verify("--ingest", "jpeg", "--cameras", "2", steps=2, warmup=1)
+    assert v["mismatches"] == 0, v["first_mismatch"]
+
+
+def test_configs3_shape_matches_oracle(oracle_mod):
+    """configs[3] per GPU at N = 4: 2 cameras x 32 detections x 64 points (2048 per camera)."""
+    v = _verify("--cameras", "2", "--points", "2048", "--boxes", "32", steps=2, warmup=1)
+    assert v["mismatches"] == 0, v["first_mismatch"]
+    assert v["objects_checked"] >= 2 * 32 * 2

@@ -1,24 +1,27 @@
 #!/bin/bash
-# Round profile on the GPU box: kernel trace + stats of the default bench
-# (Tracker2D mode, configs[2]) and of the kernel mode (configs[1]), and separate
-# --pmc passes (FETCH_SIZE, WRITE_SIZE) of both and of the HBM-counter
-# calibration probe. Usage: tools/profile_round.sh r02
+# Round profile of the benched binary on the GPU box -> gpurun_out/prof_<tag>/:
+# kernel trace + stats of the default bench line (configs[2] per GPU) and of
+# the kernel mode (configs[1]); separate --pmc passes (FETCH_SIZE, WRITE_SIZE,
+# SQ counters) of the default line and of the HBM-counter calibration probe;
+# then tools/profile_summary.py -> profile.json (copy it to
+# profiles/<tag>_tracker_profile.json; bench.py --profile reads it).
+# Usage: tools/profile_round.sh r03a
 set -e -o pipefail
-R=${1:-r01}
+R=${1:-r03}
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 B="$ROOT/bench.py"
-Q="--no-cpu-baseline --no-secondary"
+Q="--no-cpu-baseline --no-secondary --no-legs"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$B" --steps 100 --warmup 5 $Q > "$OUT/trace_bench.json" 2> "$OUT/trace.log"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace" -o run --output-format csv -- python3 "$B" --mode kernel --steps 200 --warmup 10 $Q > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.log"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/write.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/kfetch" -o run --output-format csv -- python3 "$B" --mode kernel --steps 50 --warmup 5 $Q > "$OUT/kfetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/kwrite" -o run --output-format csv -- python3 "$B" --mode kernel --steps 50 --warmup 5 $Q > "$OUT/kwrite.log" 2>&1
-timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/cfetch" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cfetch.log" 2>&1
-timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/cwrite" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cwrite.log" 2>&1
-python3 "$ROOT/tools/pmc_summary.py" "$OUT/fetch" "$OUT/write" "$OUT/cfetch" "$OUT/cwrite" "$OUT/pmc_summary.json" > /dev/null
-python3 "$ROOT/tools/pmc_summary.py" "$OUT/kfetch" "$OUT/kwrite" "$OUT/cfetch" "$OUT/cwrite" "$OUT/kpmc_summary.json" > /dev/null
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/fetch.log" 2>&1
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/write.log" 2>&1
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY -d "$OUT/sq" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/sq.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/cfetch" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cfetch.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/cwrite" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cwrite.log" 2>&1
+python3 "$ROOT/tools/profile_summary.py" "$OUT" "$ROOT/mcmtt_opticalflow_amd/lib/libpsn_lk.so" "$OUT/profile.json" > "$OUT/profile_summary.log"
+find "$OUT/trace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+find "$OUT/ktrace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_mode_kernel_stats.csv" \;
 echo "profile $R done"

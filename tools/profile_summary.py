@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""One round's profile summary of a bench command, from its rocprofv3 runs
+(tools/profile_round.sh): per kernel the kernel-trace stats (launches, mean /
+min / max duration), the PMC HBM bytes per launch (FETCH_SIZE / WRITE_SIZE in
+separate passes, corrected by the calibration probe as MI355X_MICROARCH.md's
+HBM section prescribes: byte-wide accesses -> the read_u8 / write_u8
+factors), SQ counters per launch (SQ_INSTS_VALU, SQ_WAVES, SQ_BUSY_CYCLES,
+...), the dispatch resources (VGPRs, scratch bytes per lane), and the sha of
+the profiled libpsn_lk.so (bench.py checks it against the binary it runs).
+
+usage: profile_summary.py OUTDIR LIB OUT.json
+  OUTDIR holds trace/ fetch/ write/ cfetch/ cwrite/ sq/ (rocprofv3 -d dirs)
+"""
+import csv
+import glob
+import hashlib
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import short  # noqa: E402
+
+
+def rows(d, pattern):
+    out = []
+    for f in glob.glob(os.path.join(d, "**", pattern), recursive=True):
+        out.extend(csv.DictReader(open(f)))
+    return out
+
+
+def counters(d):
+    """{kernel: {counter: [per-dispatch values]}, resources}"""
+    per = defaultdict(lambda: defaultdict(list))
+    res = {}
+    for r in rows(d, "*counter_collection.csv"):
+        k = short(r["Kernel_Name"])
+        per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        res[k] = {"vgpr": int(float(r.get("VGPR_Count", 0) or 0)), "sgpr": int(float(r.get("SGPR_Count", 0) or 0)),
+                  "scratch_bytes_per_lane": int(float(r.get("Scratch_Size", 0) or 0)),
+                  "lds_bytes": int(float(r.get("LDS_Block_Size", 0) or 0)),
+                  "workgroup": int(float(r.get("Workgroup_Size", 0) or 0))}
+    return per, res
+
+
+def mean(v):
+    return sum(v) / len(v) if v else 0.0
+
+
+def main():
+    d, lib, out = sys.argv[1:4]
+    gib = float(1 << 30)
+    cal = {}
+    for sub, cname, pref in (("cfetch", "FETCH_SIZE", "read_"), ("cwrite", "WRITE_SIZE", "write_")):
+        per, _ = counters(os.path.join(d, sub))
+        for k, cs in per.items():
+            v = cs.get(cname)
+            if k.startswith(pref) and v and mean(v) > 0:
+                cal[k + ("_fetch_factor" if cname == "FETCH_SIZE" else "_write_factor")] = gib / (mean(v) * 1024.0)
+    ff, wf = cal.get("read_u8_fetch_factor", 2.0), cal.get("write_u8_write_factor", 1.0)
+    fetch, res_f = counters(os.path.join(d, "fetch"))
+    write, _ = counters(os.path.join(d, "write"))
+    sq, res_s = counters(os.path.join(d, "sq"))
+    stats = {}
+    for r in rows(os.path.join(d, "trace"), "*kernel_stats.csv"):
+        stats[short(r["Name"])] = {"launches": int(r["Calls"]), "avg_us": round(float(r["AverageNs"]) / 1e3, 2),
+                                   "min_us": round(float(r["MinNs"]) / 1e3, 2),
+                                   "max_us": round(float(r["MaxNs"]) / 1e3, 2),
+                                   "share_pct": float(r["Percentage"])}
+    kernels = {}
+    for k in set(stats) | set(fetch) | set(write) | set(sq):
+        e = dict(stats.get(k, {}))
+        fv, wv = fetch.get(k, {}).get("FETCH_SIZE", []), write.get(k, {}).get("WRITE_SIZE", [])
+        if fv or wv:
+            e["fetch_kb_reported"] = round(mean(fv), 1)
+            e["write_kb_reported"] = round(mean(wv), 1)
+            e["hbm_bytes_per_launch"] = round(mean(fv) * 1024 * ff + mean(wv) * 1024 * wf)
+        for c, v in sq.get(k, {}).items():
+            e[c] = round(mean(v), 1)
+        e.update(res_s.get(k) or res_f.get(k) or {})
+        kernels[k] = e
+    summary = {"lib_sha16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
+               "calibration": cal, "kernels": dict(sorted(kernels.items(), key=lambda kv: -kv[1].get("share_pct", 0))),
+               "notes": "hbm_bytes_per_launch = FETCH_SIZE x read_u8 factor + WRITE_SIZE x write_u8 factor "
+                        "(KB x 1024); SQ_* are per-launch means of one --pmc pass"}
+    json.dump(summary, open(out, "w"), indent=1)
+    print(json.dumps({k: {kk: v.get(kk) for kk in ("launches", "avg_us", "hbm_bytes_per_launch", "SQ_INSTS_VALU",
+                                                   "scratch_bytes_per_lane", "vgpr")}
+                      for k, v in list(summary["kernels"].items())[:6]}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
