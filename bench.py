@@ -363,14 +363,12 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     # ctypes records of every frame, built outside the timed region; one more
     # frame than completed: the last step launches its successor ahead, as the
     # warm-up's last step did for the first timed frame
-    seq = [group.records(all_dets(t)) for t in range(warmup + steps + 1)]
+    measure = 0 if args.verify else args.measure_steps
+    seq = [group.records(all_dets(t)) for t in range(warmup + steps + measure + 1)]
     t = 0
     for i in range(warmup):
         step(t, seq[i], seq[i + 1])
         t += 1
-    lkh = group.lk_handle()
-    launches = LaunchTimes(L, lkh, 8 * steps + 64)  # every LK launch (forward + 3 chain steps)
-    sampler = SampleCounter(L, lkh)
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -382,10 +380,22 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     barrier(world)
     elapsed = time.perf_counter() - t0
     elapsed = pdist.max_over_ranks(elapsed)
-    per_kernel, ts = launches.read()
-    samples = sampler.read()
+    # after the timed region (events between the launches would perturb it): per-launch
+    # HIP-event durations of every LK launch and the device window-sample count
+    lkh = group.lk_handle()
+    per_kernel, ts, samples = {}, {"n_track": 0, "track_ms": 0.0}, None
+    if measure:
+        launches = LaunchTimes(L, lkh, 8 * measure + 64)  # forward + 3 chain steps per frame
+        sampler = SampleCounter(L, lkh)
+        for i in range(measure):
+            j = warmup + steps + i
+            gathered = step(t, seq[j], seq[j + 1])
+            t += 1
+        torch.cuda.synchronize()
+        per_kernel, ts = launches.read()
+        samples = sampler.read()
     # feature points of the last completed frame (GridFAST mode: what GridFAST kept)
-    arrs, _, nd = seq[warmup + steps - 1]
+    arrs, _, nd = seq[warmup + steps + measure - 1]
     pts_last = sum(int(arrs[c][i].num_features) for c in range(C) for i in range(nd[c])) / C
     objs_last = 0
     if rank == 0:  # the gathered hand-off of the last frame: every camera's result, index == camID
@@ -398,6 +408,7 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     if exch:
         exch.close()
     return {"elapsed": elapsed, "steps": steps, "warmup": warmup, "cams_per_rank": C, "world": world,
+            "measure_steps": measure,
             "per_kernel": per_kernel, "ts": ts, "samples": samples, "objs_last": objs_last,
             "points_per_camera": pts_last, "recorded": recorded, "slot_bytes": slot_bytes, "max_obj": max_obj}
 
@@ -561,7 +572,7 @@ def tracker_roofline(args, r, C, profile):
            "bytes_note": f"SURVEY 8(d) LK bytes 2*S_pyr + 21*N = {lk_b} per camera-frame x {C} camera-frames per "
                          "launch; achieved/peak/frac are the HBM roofline of this kernel (contract fields)",
            "per_kernel_us": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
-                                 "ms_per_step": round(v[1] / r["steps"], 4)} for k, v in sorted(per.items())}}
+                                 "ms_per_step": round(v[1] / max(r["measure_steps"], 1), 4)} for k, v in sorted(per.items())}}
     lib_sha = file_sha16(_lib.LIB_PATH)
     if profile:
         pk = profile.get("kernels", {}).get(name, {})
@@ -580,9 +591,9 @@ def tracker_roofline(args, r, C, profile):
                  "peak_note": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
             # useful lane work of every LK launch of a frame-set vs the lane slots they issued
             lk_vi = sum(kv.get("SQ_INSTS_VALU", 0) * per.get(k, (0, 0))[0]
-                        for k, kv in profile.get("kernels", {}).items() if k.startswith("lk_kernel")) / r["steps"]
+                        for k, kv in profile.get("kernels", {}).items() if k.startswith("lk_kernel")) / max(r["measure_steps"], 1)
             if r["samples"] and lk_vi:
-                useful = r["samples"] / r["steps"] * OPS_PER_SAMPLE
+                useful = r["samples"] / max(r["measure_steps"], 1) * OPS_PER_SAMPLE
                 v["useful_lane_frac"] = round(useful / (lk_vi * 64), 4)
                 v["useful_note"] = (f"SURVEY 8(d) window samples x {OPS_PER_SAMPLE} ops per frame-set / "
                                     "(SQ_INSTS_VALU of every LK launch per frame-set x 64 lanes)")
@@ -599,7 +610,7 @@ def tracker_line(args, r, world, C, scaling, profile):
     per_gpu_fps = C * r["steps"] / r["elapsed"]
     pyr_b, lk_b = algorithmic_bytes(args.width, args.height, 4, args.points, c_in=3)
     frame_b = pyr_b + lk_b
-    cam_frames = C * r["steps"]
+    cam_frames = C * max(r["measure_steps"], 1)
     cfg3 = (args.total_cameras == 8 and args.points == 2048)
     what = ("BASELINE.json configs[3]" if cfg3 else "BASELINE.json configs[2] per GPU"
             if (args.width, args.height, args.cameras, args.points, args.boxes) == (1920, 1080, 4, 512, 8)
@@ -629,7 +640,9 @@ def tracker_line(args, r, world, C, scaling, profile):
                         "bytes_formula": "SURVEY 8(d) c_in*S0 + 4*S_pyr - S_top + 21*N, c_in = 3 (BGR)",
                         "achieved_GBps_per_gpu": round(frame_b * per_gpu_fps / 1e9, 3),
                         "hbm_fraction": round(frame_b * per_gpu_fps / 1e9 / HBM_PEAK_GBPS, 6),
-                        "lk_ms_per_step": round(r["ts"]["track_ms"] / r["steps"], 4)},
+                        "lk_ms_per_step": round(r["ts"]["track_ms"] / max(r["measure_steps"], 1), 4),
+                        "lk_timing_note": "LK launch times from HIP events in the measure_steps frames after the "
+                                          "timed region (no events inside it)"},
         "compute": {"window_samples_per_camera_frame": round(r["samples"] / cam_frames) if r["samples"] else None,
                     "gsamples_per_s_per_gpu": round(r["samples"] / cam_frames * per_gpu_fps / 1e9, 3)
                     if r["samples"] else None,
@@ -782,7 +795,6 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     for _ in range(warmup):
         step(t)
         t += 1
-    ctx.enable_timing(steps + 1, 1)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -790,6 +802,13 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
         t += 1
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
+    # launch durations after the timed region (HIP events on the LK stream)
+    measure = max(1, min(steps, 50))
+    ctx.enable_timing(measure + 1, 1)
+    for _ in range(measure):
+        step(t)
+        t += 1
+    torch.cuda.synchronize(device)
     ts = ctx.timing_stats()
     ctx.close()
     if smoother is not None:
@@ -948,6 +967,8 @@ def parse_args(argv=None):
     ap.add_argument("--period", type=int, default=10)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--leg-steps", type=int, default=40)
+    ap.add_argument("--measure-steps", type=int, default=20,
+                    help="frames after the timed region with per-launch HIP-event timing (roofline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-legs", action="store_true")

@@ -60,6 +60,10 @@ int psn_t2d_chain_step_device(const psn_t2d_chain_dev *c, int step, void *hip_st
  * fewer than PSN_2D_FEATURE_MIN_NUM_TRACK features, :744) or where
  * d_last_step[i] < 1 (nullable: no frame t-1 in that camera's ring), asynchronous. */
 int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *hip_stream);
+/* psn_t2d_gate_counts_device and d_zero[0 .. nzero) = 0 (the chains' step and
+ * set counters) in ONE launch: the start of a frame's device chain. */
+int psn_t2d_chain_begin_device(int *d_cnt, int n, int min_count, const int *d_last_step, int *d_zero, int nzero,
+                               void *hip_stream);
 
 #ifdef __cplusplus
 }

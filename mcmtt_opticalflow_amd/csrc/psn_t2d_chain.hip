@@ -166,19 +166,26 @@ __global__ __launch_bounds__(kLanes) void chain_step_kernel(psn_t2d_chain_dev C,
 
 // Detections whose feature count fails the reference's minimum (:744) get no
 // chain: their count becomes 0, so their workgroups exit at once.
-__global__ void gate_counts_kernel(int *cnt, int n, int min_count, const int *last_step) {
+__global__ void gate_counts_kernel(int *cnt, int n, int min_count, const int *last_step, int *zero, int nzero) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n && (cnt[i] < min_count || (last_step && last_step[i] < 1))) cnt[i] = 0;
+    for (int k = i; k < nzero; k += gridDim.x * blockDim.x) zero[k] = 0;
 }
 
 }  // namespace
 }  // namespace psn
 
 extern "C" int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *stream) {
-    if (n < 0 || (n > 0 && !d_cnt)) return PSN_LK_ERR_ARG;
-    if (n == 0) return PSN_LK_OK;
-    hipLaunchKernelGGL(psn::gate_counts_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_cnt, n,
-                       min_count, d_last_step);
+    return psn_t2d_chain_begin_device(d_cnt, n, min_count, d_last_step, nullptr, 0, stream);
+}
+
+extern "C" int psn_t2d_chain_begin_device(int *d_cnt, int n, int min_count, const int *d_last_step, int *d_zero,
+                                          int nzero, void *stream) {
+    if (n < 0 || nzero < 0 || (n > 0 && !d_cnt) || (nzero > 0 && !d_zero)) return PSN_LK_ERR_ARG;
+    const int m = n > nzero ? n : nzero;
+    if (m == 0) return PSN_LK_OK;
+    hipLaunchKernelGGL(psn::gate_counts_kernel, dim3((m + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_cnt, n,
+                       min_count, d_last_step, d_zero, nzero);
     return hipGetLastError() == hipSuccess ? PSN_LK_OK : PSN_LK_ERR_HIP;
 }
 

@@ -163,18 +163,37 @@ struct Tracker2DFlow::DeviceBuffers {
     double *d_boxes = nullptr, *d_obox = nullptr;
     float *d_sets = nullptr;
     int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr, *d_tot = nullptr, *d_last = nullptr;
-    // forward calls
+    // forward calls: inputs [counts | (256-B aligned) points], outputs [status | (aligned) points] (one copy each)
     float *d_fin = nullptr, *d_fout = nullptr, *d_ferr = nullptr;
     uint8_t *d_fstatus = nullptr;
     int *d_fcnt = nullptr;
+    char *d_fiblk = nullptr, *d_foblk = nullptr, *h_fiblk = nullptr, *h_foblk = nullptr;
+    size_t fi_off_pts = 0, fo_off_pts = 0;
     // pinned staging of the chain inputs (and GridFAST features), two sets: a
     // pass's set is written by its launch and read back by its completion, and
     // the next frame's chains may be launched in between (RunComplete with next)
+    // [boxes f64 x4 | last steps | counts | (256-B aligned) points] per chain, one block per
+    // side so that one copy carries a pass's inputs (carve_in)
     struct Stage {
+        char *h_inblk = nullptr;
         float *h_in = nullptr;
         double *h_boxes = nullptr;
         int *h_cnt = nullptr, *h_rawcnt = nullptr, *h_last = nullptr;
     } stage[2];
+    char *d_inblk = nullptr;
+    size_t in_off_last = 0, in_off_cnt = 0, in_off_in = 0, in_bytes = 0;
+    void layout_in(size_t K, size_t cap) {
+        in_off_last = K * 32;
+        in_off_cnt = in_off_last + K * 4;
+        in_off_in = (in_off_cnt + K * 4 + 255) & ~(size_t)255;
+        in_bytes = in_off_in + K * cap * 8;
+    }
+    void carve_in(char *base, double *&boxes, int *&last, int *&cnt, float *&in) const {
+        boxes = (double *)base;
+        last = (int *)(base + in_off_last);
+        cnt = (int *)(base + in_off_cnt);
+        in = (float *)(base + in_off_in);
+    }
     // pinned staging: forward inputs, then results
     float *h_fin = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
     uint8_t *h_fwd_st = nullptr;
@@ -198,11 +217,12 @@ struct Tracker2DFlow::DeviceBuffers {
             if (p) (void)hipHostFree(p);
     }
     void release_chains() {
-        free_all({d_in, d_out, d_buf[0], d_buf[1], d_err, d_status, d_boxes, d_res, d_cnt, d_tot, d_last}, {h_res});
+        free_all({d_inblk, d_out, d_buf[0], d_buf[1], d_err, d_status, d_res, d_tot}, {h_res});
         for (Stage &g : stage) {
-            free_all({}, {g.h_in, g.h_boxes, g.h_cnt, g.h_rawcnt, g.h_last});
+            free_all({}, {g.h_inblk, g.h_rawcnt});
             g = Stage();
         }
+        d_inblk = nullptr;
         d_in = d_out = d_buf[0] = d_buf[1] = d_err = d_sets = nullptr;
         d_status = nullptr;
         d_boxes = d_obox = nullptr;
@@ -215,7 +235,8 @@ struct Tracker2DFlow::DeviceBuffers {
         nchains = 0;
     }
     void release_forward() {
-        free_all({d_fin, d_fout, d_ferr, d_fstatus, d_fcnt}, {h_fin, h_fwd_out, h_fwd_st, h_fcnt});
+        free_all({d_fiblk, d_foblk, d_ferr}, {h_fiblk, h_foblk});
+        d_fiblk = d_foblk = h_fiblk = h_foblk = nullptr;
         d_fin = d_fout = d_ferr = nullptr;
         d_fstatus = nullptr;
         d_fcnt = nullptr;
@@ -271,26 +292,21 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
     bool ok = true;
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
     auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
-    dm((void **)&b.d_in, npt * 8);
+    b.layout_in(K, cap);
+    dm((void **)&b.d_inblk, b.in_bytes);
     dm((void **)&b.d_out, npt * 8);
     dm((void **)&b.d_buf[0], npt * 8);
     dm((void **)&b.d_buf[1], npt * 8);
     dm((void **)&b.d_err, npt * 4);
     dm((void **)&b.d_status, npt);
-    dm((void **)&b.d_boxes, K * 4 * 8);
     b.res_sets_off = DeviceBuffers::res_box_off(K, S) + K * S * 4 * 8;
     const size_t res_bytes = b.res_sets_off + K * S * cap * 8;
     dm((void **)&b.d_res, res_bytes);
-    dm((void **)&b.d_cnt, K * 4);
     dm((void **)&b.d_tot, K * 4);
-    dm((void **)&b.d_last, K * 4);
     hm((void **)&b.h_res, res_bytes);
     for (DeviceBuffers::Stage &g : b.stage) {
-        hm((void **)&g.h_in, npt * 8);
-        hm((void **)&g.h_boxes, K * 4 * 8);
-        hm((void **)&g.h_cnt, K * 4);
+        hm((void **)&g.h_inblk, b.in_bytes);
         hm((void **)&g.h_rawcnt, K * 4);
-        hm((void **)&g.h_last, K * 4);
     }
     if (!ok) {
         b.release_chains();
@@ -298,6 +314,8 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
         return PSN_LK_ERR_NOMEM;
     }
     b.carve(b.d_res, b.d_obox, b.d_sets, b.d_setcnt, b.d_nsteps, K, S);
+    b.carve_in(b.d_inblk, b.d_boxes, b.d_last, b.d_cnt, b.d_in);
+    for (DeviceBuffers::Stage &g : b.stage) b.carve_in(g.h_inblk, g.h_boxes, g.h_last, g.h_cnt, g.h_in);
     b.carve(b.h_res, b.h_obox, b.h_sets, b.h_setcnt, b.h_nsteps, K, S);
     b.nchains = K;
     return PSN_LK_OK;
@@ -315,20 +333,26 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     bool ok = true;
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
     auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
-    dm((void **)&b.d_fin, F * 8);
-    dm((void **)&b.d_fout, F * 8);
+    b.fi_off_pts = (J * 4 + 255) & ~(size_t)255;
+    b.fo_off_pts = (F + 255) & ~(size_t)255;
+    dm((void **)&b.d_fiblk, b.fi_off_pts + F * 8);
+    dm((void **)&b.d_foblk, b.fo_off_pts + F * 8);
     dm((void **)&b.d_ferr, F * 4);
-    dm((void **)&b.d_fstatus, F);
-    dm((void **)&b.d_fcnt, J * 4);
-    hm((void **)&b.h_fin, F * 8);
-    hm((void **)&b.h_fwd_out, F * 8);
-    hm((void **)&b.h_fwd_st, F);
-    hm((void **)&b.h_fcnt, J * 4);
+    hm((void **)&b.h_fiblk, b.fi_off_pts + F * 8);
+    hm((void **)&b.h_foblk, b.fo_off_pts + F * 8);
     if (!ok) {
         b.release_forward();
         err_ = "forward buffers: allocation failed";
         return PSN_LK_ERR_NOMEM;
     }
+    b.d_fcnt = (int *)b.d_fiblk;
+    b.d_fin = (float *)(b.d_fiblk + b.fi_off_pts);
+    b.h_fcnt = (int *)b.h_fiblk;
+    b.h_fin = (float *)(b.h_fiblk + b.fi_off_pts);
+    b.d_fstatus = (uint8_t *)b.d_foblk;
+    b.d_fout = (float *)(b.d_foblk + b.fo_off_pts);
+    b.h_fwd_st = (uint8_t *)b.h_foblk;
+    b.h_fwd_out = (float *)(b.h_foblk + b.fo_off_pts);
     b.nfwd_pts = F;
     b.nfwd_jobs = J;
     return PSN_LK_OK;
@@ -430,6 +454,8 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
             }
             chk(hipMemcpyAsync(b.h_rawcnt, db.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
             chk(hipMemcpyAsync(b.h_in, db.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
+            // boxes and last steps (GridFAST wrote the counts and points on the device)
+            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, db.in_off_cnt, hipMemcpyHostToDevice, st), "chain boxes");
         } else {
             for (PassCam &p : pc)
                 for (size_t i = 0; i < p.dets->size(); i++) {
@@ -446,14 +472,15 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
                     }
                     b.h_cnt[k] = (int)n;
                 }
-            // whole rows: a chain row's unused tail is never read (counts)
-            chk(hipMemcpyAsync(db.d_in, b.h_in, K * cap * 8, hipMemcpyHostToDevice, st), "chain inputs");
-            chk(hipMemcpyAsync(db.d_cnt, b.h_cnt, K * 4, hipMemcpyHostToDevice, st), "chain counts");
+            // boxes, last steps, counts and points in one copy (whole rows: a chain
+            // row's unused tail is never read)
+            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, db.in_off_in + K * cap * 8, hipMemcpyHostToDevice, st),
+                "chain inputs");
         }
-        chk(hipMemcpyAsync(db.d_last, b.h_last, K * 4, hipMemcpyHostToDevice, st), "chain last steps");
-        if (!rc) rc = psn_t2d_gate_counts_device(db.d_cnt, (int)K, (int)kT2dMinFeatures, db.d_last, st);
-        chk(hipMemcpyAsync(db.d_boxes, b.h_boxes, K * 32, hipMemcpyHostToDevice, st), "chain boxes");
-        chk(hipMemsetAsync(db.d_nsteps, 0, db.nchains * (1 + S) * 4, st), "chain steps and set counts");
+        // the feature-minimum gate and the cleared step / set counters in one launch
+        if (!rc)
+            rc = psn_t2d_chain_begin_device(db.d_cnt, (int)K, (int)kT2dMinFeatures, db.d_last, db.d_nsteps,
+                                            (int)(db.nchains * (1 + S)), st);
         if (rc) return rc;
         psn_t2d_chain_dev cd{};
         cd.ndet = (int)K;
@@ -545,8 +572,8 @@ int Tracker2DFlow::PassLaunchForward(std::vector<PassCam> &pc) {
                 }
             }
         }
-        if (F) chk(hipMemcpyAsync(b.d_fin, b.h_fin, F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
-        chk(hipMemcpyAsync(b.d_fcnt, b.h_fcnt, J * 4, hipMemcpyHostToDevice, fs), "forward counts");
+        // counts and points in one copy
+        chk(hipMemcpyAsync(b.d_fiblk, b.h_fiblk, b.fi_off_pts + F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
         if (rc) return rc;
         rc = psn_lk_set_stream(lk_, fs);
         if (!rc)
@@ -594,8 +621,9 @@ int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
         chk(hipMemcpyAsync(bp->h_res, bp->d_res, bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
             "chain results");
     if (F && bp) {
-        chk(hipMemcpyAsync(bp->h_fwd_out, bp->d_fout, F * 8, hipMemcpyDeviceToHost, fs), "forward points");
-        chk(hipMemcpyAsync(bp->h_fwd_st, bp->d_fstatus, F, hipMemcpyDeviceToHost, fs), "forward status");
+        // status and points in one copy
+        chk(hipMemcpyAsync(bp->h_foblk, bp->d_foblk, bp->fo_off_pts + F * 8, hipMemcpyDeviceToHost, fs),
+            "forward results");
     }
     // everything the pass enqueued on either stream precedes these records
     chk(hipEventRecord((hipEvent_t)ev_chain_, st), "chain results event");

@@ -24,14 +24,15 @@ def main():
 
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     torch.cuda.set_device(0)
-    W, H, C, P, B, period = 1920, 1080, 4, 512, 8, 10
+    args = bench.parse_args([])
+    W, H, C, B = args.width, args.height, args.cameras, args.boxes
     pinned = bench.pinned_allocator()
-    feeds = [bench.CameraFeed(c, W, H, P, B, period, t2d, pinned) for c in range(C)]
+    feeds = [bench.CameraFeed(c, args, pinned) for c in range(C)]
     group = t2d.Group(W, H, list(range(C)), device=0, max_objects=2 * B)
     slot_bytes = t2d.result_slot_bytes(2 * B, 1)
     send = pinned((C, slot_bytes))
     T = t2d.load()
-    seq = [group.records([fd.detections(t) for fd in feeds]) for t in range(steps + 6)]
+    seq = [group.records([fd.detections(t2d, t) for fd in feeds]) for t in range(steps + 6)]
     for k, fd in enumerate(feeds):
         fd.push(group, k, 0)
     rows = []
