@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -52,7 +53,18 @@ struct psn_lk_ctx {
     psn::RingGeo ring{};        // slot/level geometry passed to the single-tile kernel
     std::vector<hipEvent_t> slot_ready;
     std::vector<char> ready_rec;
-    std::vector<std::vector<std::pair<hipStream_t, hipEvent_t>>> slot_free;
+    // per slot: its build generation (slot_ready re-recorded), and per stream the
+    // generation that stream has waited for already (no repeated waits)
+    std::vector<unsigned> build_gen;
+    std::vector<std::vector<std::pair<hipStream_t, unsigned>>> waited;
+    // per slot: per stream the event of the last launch on it that read the slot;
+    // one event per launch, shared by every slot it read (refcounted, pooled)
+    struct SharedEv {
+        hipEvent_t e = nullptr;
+        int refs = 0;
+    };
+    std::vector<SharedEv *> ev_all, ev_free;
+    std::vector<std::vector<std::pair<hipStream_t, SharedEv *>>> slot_free;
     // psn_lk_push_frame_async: per-slot staging buffer of the uploaded frame
     std::vector<uint8_t *> d_stage;
     std::vector<size_t> stage_cap;
@@ -235,6 +247,8 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     c->slot_ready.assign(c->nslots, nullptr);
     c->slot_free.assign(c->nslots, {});
     c->ready_rec.assign(c->nslots, 0);
+    c->build_gen.assign(c->nslots, 0);
+    c->waited.assign(c->nslots, {});
     c->d_stage.assign(c->nslots, nullptr);
     c->stage_cap.assign(c->nslots, 0);
     c->copy_done.assign(c->nslots, nullptr);
@@ -257,8 +271,13 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready, &c->copy_done})
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
-    for (auto &v : c->slot_free)
-        for (auto &se : v) (void)hipEventDestroy(se.second);
+    c->slot_free.clear();
+    for (auto *se : c->ev_all) {
+        (void)hipEventDestroy(se->e);
+        delete se;
+    }
+    c->ev_all.clear();
+    c->ev_free.clear();
     for (uint8_t *p : c->d_stage)
         if (p) (void)hipFree(p);
     if (c->jpeg) psn_jpeg_destroy(c->jpeg);
@@ -390,36 +409,82 @@ static int launch_build(psn_lk_ctx *c, const psn::PyrBuildArgs &a, hipStream_t s
     }
     HIPCHK(c, hipEventRecord(c->slot_ready[slot], s));
     c->ready_rec[slot] = 1;
+    c->build_gen[slot]++;
+    bool mine = false;  // the building stream is ordered after the build
+    for (auto &w : c->waited[slot])
+        if (w.first == s) w.second = c->build_gen[slot], mine = true;
+    if (!mine) c->waited[slot].emplace_back(s, c->build_gen[slot]);
     return PSN_LK_OK;
 }
 
 // Make the current stream wait for the last build of `slot` (a no-op on the
 // device when the build ran earlier on the same stream or has completed).
 static int wait_slot_ready(psn_lk_ctx *c, int slot) {
-    if (slot >= 0 && slot < c->nslots && c->ready_rec[slot])
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot_ready[slot], 0));
+    if (slot < 0 || slot >= c->nslots || !c->ready_rec[slot]) return PSN_LK_OK;
+    // a stream that has waited for this build already is ordered after it
+    for (auto &w : c->waited[slot])
+        if (w.first == c->stream) {
+            if (w.second == c->build_gen[slot]) return PSN_LK_OK;
+            HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot_ready[slot], 0));
+            w.second = c->build_gen[slot];
+            return PSN_LK_OK;
+        }
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot_ready[slot], 0));
+    c->waited[slot].emplace_back(c->stream, c->build_gen[slot]);
     return PSN_LK_OK;
 }
 
-// After a launch on the current stream read `slot`: record that stream's free event.
-static int record_slot_free(psn_lk_ctx *c, int slot) {
-    if (slot < 0 || slot >= c->nslots) return PSN_LK_OK;
-    for (auto &se : c->slot_free[slot])
-        if (se.first == c->stream) {
-            HIPCHK(c, hipEventRecord(se.second, c->stream));
-            return PSN_LK_OK;
+static void ev_unref(psn_lk_ctx *c, psn_lk_ctx::SharedEv *e) {
+    if (e && --e->refs == 0) c->ev_free.push_back(e);
+}
+
+// After a launch on the current stream read `slots`: ONE event recorded behind
+// it becomes that stream's free event of every slot read (a later build into
+// one of them waits for it). An event returns to the pool when no slot refers
+// to it; re-recording a pooled event never moves a live reference.
+static int record_slots_free(psn_lk_ctx *c, const int *slots, int n) {
+    psn_lk_ctx::SharedEv *e = nullptr;
+    if (!c->ev_free.empty()) {
+        e = c->ev_free.back();
+        c->ev_free.pop_back();
+    } else {
+        e = new (std::nothrow) psn_lk_ctx::SharedEv();
+        if (!e) return set_err(c, PSN_LK_ERR_NOMEM, "slot event");
+        if (hipEventCreateWithFlags(&e->e, kSlotEventFlags) != hipSuccess) {
+            delete e;
+            return set_err(c, PSN_LK_ERR_HIP, "hipEventCreateWithFlags (slot event)");
         }
-    hipEvent_t e = nullptr;
-    HIPCHK(c, hipEventCreateWithFlags(&e, kSlotEventFlags));
-    c->slot_free[slot].emplace_back(c->stream, e);
-    HIPCHK(c, hipEventRecord(e, c->stream));
+        c->ev_all.push_back(e);
+    }
+    HIPCHK(c, hipEventRecord(e->e, c->stream));
+    for (int i = 0; i < n; i++) {
+        const int slot = slots[i];
+        if (slot < 0 || slot >= c->nslots) continue;
+        bool found = false;
+        for (auto &se : c->slot_free[slot])
+            if (se.first == c->stream) {
+                if (se.second != e) {
+                    e->refs++;
+                    ev_unref(c, se.second);
+                    se.second = e;
+                }
+                found = true;
+                break;
+            }
+        if (!found) {
+            e->refs++;
+            c->slot_free[slot].emplace_back(c->stream, e);
+        }
+    }
+    if (e->refs == 0) c->ev_free.push_back(e);
     return PSN_LK_OK;
 }
+static int record_slot_free(psn_lk_ctx *c, int slot) { return record_slots_free(c, &slot, 1); }
 
 // Make stream s wait until every recorded read of `slot` is done (before a new build into it).
 static int wait_slot_free(psn_lk_ctx *c, int slot, hipStream_t s) {
     for (auto &se : c->slot_free[slot])
-        if (se.first != s) HIPCHK(c, hipStreamWaitEvent(s, se.second, 0));
+        if (se.first != s) HIPCHK(c, hipStreamWaitEvent(s, se.second->e, 0));
     return PSN_LK_OK;
 }
 
@@ -501,7 +566,10 @@ int psn_lk_push_frame_async(psn_lk_ctx *c, int slot, const uint8_t *host, int st
     // the staging buffer is read only by this slot's previous build (its ready
     // event); the build waits for the upload and for every read of the slot
     if (c->ready_rec[slot]) HIPCHK(c, hipStreamWaitEvent(cs, c->slot_ready[slot], 0));
-    HIPCHK(c, hipMemcpy2DAsync(c->d_stage[slot], row, host, stride, row, c->height, hipMemcpyHostToDevice, cs));
+    if ((size_t)stride == row)  // contiguous rows: one linear copy (the DMA engine's fast path)
+        HIPCHK(c, hipMemcpyAsync(c->d_stage[slot], host, need, hipMemcpyHostToDevice, cs));
+    else
+        HIPCHK(c, hipMemcpy2DAsync(c->d_stage[slot], row, host, stride, row, c->height, hipMemcpyHostToDevice, cs));
     HIPCHK(c, hipEventRecord(c->copy_done[slot], cs));
     rc = wait_slot_free(c, slot, s);
     if (rc) return rc;
@@ -771,6 +839,11 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         if (fused_slot >= 0) {  // readers on other streams wait for the launch that built it
             HIPCHK(c, hipEventRecord(c->slot_ready[fused_slot], c->stream));
             c->ready_rec[fused_slot] = 1;
+            c->build_gen[fused_slot]++;
+            bool mine = false;  // this stream built it: ordered after the build
+            for (auto &w : c->waited[fused_slot])
+                if (w.first == c->stream) w.second = c->build_gen[fused_slot], mine = true;
+            if (!mine) c->waited[fused_slot].emplace_back(c->stream, c->build_gen[fused_slot]);
         }
     }
     if (c->pend) {  // no launch took it (no points)
@@ -781,8 +854,9 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         HIPCHK(c, hipEventRecord(c->ev_track[2 * ti + 1], c->stream));
         c->n_track++;
     }
-    for (int sl : used) {  // the next build into these slots waits for this launch
-        int rc = record_slot_free(c, sl);
+    // the next build into these slots waits for this launch
+    if (!used.empty()) {
+        int rc = record_slots_free(c, used.data(), (int)used.size());
         if (rc) return rc;
     }
     return PSN_LK_OK;
