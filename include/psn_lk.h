@@ -159,6 +159,11 @@ int psn_lk_track_device(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const fl
  * written. Used by the device-side backward chain (psn_t2d_*). */
 int psn_lk_track_device_counted(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const int *d_counts,
                                 const float *d_prev_xy, float *d_next_xy, uint8_t *d_status, float *d_err);
+/* The same with query i's count at d_counts[i * count_stride] (e.g. one
+ * counter of a per-detection record array). */
+int psn_lk_track_device_counted_strided(psn_lk_ctx *ctx, const psn_lk_query *q, int nq, const int *d_counts,
+                                        int count_stride, const float *d_prev_xy, float *d_next_xy, uint8_t *d_status,
+                                        float *d_err);
 
 /* One-shot cv::calcOpticalFlowPyrLK(prevImg, nextImg, prevPts, nextPts, status,
  * err, winSize, maxLevel, criteria, flags, minEigThreshold) on two host gray

@@ -60,10 +60,13 @@ int psn_t2d_chain_step_device(const psn_t2d_chain_dev *c, int step, void *hip_st
  * fewer than PSN_2D_FEATURE_MIN_NUM_TRACK features, :744) or where
  * d_last_step[i] < 1 (nullable: no frame t-1 in that camera's ring), asynchronous. */
 int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *hip_stream);
-/* psn_t2d_gate_counts_device and d_zero[0 .. nzero) = 0 (the chains' step and
- * set counters) in ONE launch: the start of a frame's device chain. */
-int psn_t2d_chain_begin_device(int *d_cnt, int n, int min_count, const int *d_last_step, int *d_zero, int nzero,
-                               void *hip_stream);
+/* The start of a frame's device chain (one launch): per detection k < c->ndet
+ * the step / set counters cleared, set 0 = its features at t (c->cur, the
+ * first min(cnt, cap) points) with set_cnt[k * STEPS] = that count when
+ * cnt[k] >= min_count, then the gate of psn_t2d_gate_counts_device. Set 0 is
+ * what the detection's tracker carries into the next frame's forward call:
+ * its step-1 inliers, or these features when no step keeps 4 inliers. */
+int psn_t2d_chain_begin_device(const psn_t2d_chain_dev *c, int min_count, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -698,7 +698,8 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
 }
 
 static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
-                             uint8_t *d_status, float *d_err, bool allow_scratch, const int *d_counts = nullptr) {
+                             uint8_t *d_status, float *d_err, bool allow_scratch, const int *d_counts = nullptr,
+                             int count_stride = 1) {
     if (d_counts && c->pend) {  // early-exit workgroups cannot take part in a fused build
         int rc = flush_pending(c);
         if (rc) return rc;
@@ -751,7 +752,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             bx_notail &= (qq.params.flags & PSN_LK_ACCUM_SCALAR) == 0 && qq.params.win_w % 8 == 0;
             upt_bx = std::max(upt_bx, bupt);
             lds_bx = std::max(lds_bx, blds);
-            a.q[nqd].qidx = base + i;
+            a.q[nqd].qidx = (base + i) * count_stride;  // the query's count: d_counts[i * count_stride]
             all_single &= single;
             rows_ow = std::max(rows_ow, orows);
             lds_ow = std::max(lds_ow, olds);
@@ -864,9 +865,16 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
 
 int psn_lk_track_device_counted(psn_lk_ctx *c, const psn_lk_query *q, int nq, const int *d_counts,
                                 const float *d_prev, float *d_next, uint8_t *d_status, float *d_err) {
-    if (!c || !d_counts || (nq > 0 && (!q || !d_prev || !d_next || !d_status)) || nq < 0) return PSN_LK_ERR_ARG;
+    return psn_lk_track_device_counted_strided(c, q, nq, d_counts, 1, d_prev, d_next, d_status, d_err);
+}
+
+int psn_lk_track_device_counted_strided(psn_lk_ctx *c, const psn_lk_query *q, int nq, const int *d_counts,
+                                        int count_stride, const float *d_prev, float *d_next, uint8_t *d_status,
+                                        float *d_err) {
+    if (!c || !d_counts || count_stride < 1 || (nq > 0 && (!q || !d_prev || !d_next || !d_status)) || nq < 0)
+        return PSN_LK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    return track_device_impl(c, q, nq, d_prev, d_next, d_status, d_err, false, d_counts);
+    return track_device_impl(c, q, nq, d_prev, d_next, d_status, d_err, false, d_counts, count_stride);
 }
 
 int psn_lk_track_device(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,

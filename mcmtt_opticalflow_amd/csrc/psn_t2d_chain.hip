@@ -166,26 +166,54 @@ __global__ __launch_bounds__(kLanes) void chain_step_kernel(psn_t2d_chain_dev C,
 
 // Detections whose feature count fails the reference's minimum (:744) get no
 // chain: their count becomes 0, so their workgroups exit at once.
-__global__ void gate_counts_kernel(int *cnt, int n, int min_count, const int *last_step, int *zero, int nzero) {
+__global__ void gate_counts_kernel(int *cnt, int n, int min_count, const int *last_step) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n && (cnt[i] < min_count || (last_step && last_step[i] < 1))) cnt[i] = 0;
-    for (int k = i; k < nzero; k += gridDim.x * blockDim.x) zero[k] = 0;
+}
+
+// The start of a frame's device chain, one workgroup per detection: its step and
+// set counters cleared; a detection with enough features (:744) gets set 0 = its
+// features at t -- the tracker features the reference keeps when no chain step
+// finds 4 inliers (:815-818; step 1 overwrites set 0 with its inliers when it
+// does), which the next frame's forward call reads -- then the gate.
+__global__ __launch_bounds__(128) void chain_begin_kernel(psn_t2d_chain_dev C, int min_count) {
+    const int k = blockIdx.x, t = threadIdx.x;
+    const int S = PSN_T2D_CHAIN_STEPS;
+    const int n = C.cnt[k];
+    const bool valid = n >= min_count;
+    const int m = valid ? min(n, C.cap) : 0;
+    const size_t pb = (size_t)k * C.cap * 2;
+    float *s0 = C.sets + (size_t)k * S * C.cap * 2;
+    for (int i = t; i < m; i += blockDim.x) {
+        s0[2 * i] = C.cur[pb + 2 * i];
+        s0[2 * i + 1] = C.cur[pb + 2 * i + 1];
+    }
+    __syncthreads();  // every lane has read cnt[k] before lane 0 gates it
+    if (t == 0) {
+        C.nsteps[k] = 0;
+        C.set_cnt[(size_t)k * S] = m;
+        for (int s = 1; s < S; s++) C.set_cnt[(size_t)k * S + s] = 0;
+        if (!valid || (C.last_step && C.last_step[k] < 1)) C.cnt[k] = 0;
+    }
 }
 
 }  // namespace
 }  // namespace psn
 
 extern "C" int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *stream) {
-    return psn_t2d_chain_begin_device(d_cnt, n, min_count, d_last_step, nullptr, 0, stream);
+    if (n < 0 || (n > 0 && !d_cnt)) return PSN_LK_ERR_ARG;
+    if (n == 0) return PSN_LK_OK;
+    hipLaunchKernelGGL(psn::gate_counts_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_cnt, n,
+                       min_count, d_last_step);
+    return hipGetLastError() == hipSuccess ? PSN_LK_OK : PSN_LK_ERR_HIP;
 }
 
-extern "C" int psn_t2d_chain_begin_device(int *d_cnt, int n, int min_count, const int *d_last_step, int *d_zero,
-                                          int nzero, void *stream) {
-    if (n < 0 || nzero < 0 || (n > 0 && !d_cnt) || (nzero > 0 && !d_zero)) return PSN_LK_ERR_ARG;
-    const int m = n > nzero ? n : nzero;
-    if (m == 0) return PSN_LK_OK;
-    hipLaunchKernelGGL(psn::gate_counts_kernel, dim3((m + 255) / 256), dim3(256), 0, (hipStream_t)stream, d_cnt, n,
-                       min_count, d_last_step, d_zero, nzero);
+extern "C" int psn_t2d_chain_begin_device(const psn_t2d_chain_dev *c, int min_count, void *stream) {
+    if (!c || c->ndet < 0 || c->cap <= 0 || c->cap > 128 || (c->ndet > 0 && (!c->cnt || !c->cur || !c->sets ||
+                                                                             !c->set_cnt || !c->nsteps)))
+        return PSN_LK_ERR_ARG;
+    if (c->ndet == 0) return PSN_LK_OK;
+    hipLaunchKernelGGL(psn::chain_begin_kernel, dim3(c->ndet), dim3(128), 0, (hipStream_t)stream, *c, min_count);
     return hipGetLastError() == hipSuccess ? PSN_LK_OK : PSN_LK_ERR_HIP;
 }
 

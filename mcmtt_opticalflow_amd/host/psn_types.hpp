@@ -87,6 +87,7 @@ struct Tracker2D {  // stTracker2D (.h:31-47)
     std::vector<Point2f> featurePoints, trackedPoints;
     double lastPosition[3] = {0, 0, 0};
     double height = 0.0;
+    int srcDet = -1;  // the detection (index in its frame) that last set featurePoints (this build)
 };
 
 struct Object2DInfo {  // stObject2DInfo (PSNWhere_Types.h:190-198)

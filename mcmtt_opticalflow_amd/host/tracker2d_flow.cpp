@@ -148,6 +148,20 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
     }
     ev_chain_ = e1;
     ev_fwd_ = e2;
+    for (int r = 0; r < kT2dResBlocks; r++) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+            err_ = "result block events";
+            return PSN_LK_ERR_HIP;
+        }
+        ev_set0_[r] = a;
+        ev_fread_[r] = b;
+        fread_rec_[r] = false;
+        chain_info_[r] = ChainInfo();
+    }
+    next_rb_ = 0;
+    last_rb_ = -1;
     return psn_lk_set_stream(lk_, cs);
 }
 
@@ -160,9 +174,8 @@ struct Tracker2DFlow::DeviceBuffers {
     // chains: inputs, LK outputs, ping-pong point sets, err/status
     float *d_in = nullptr, *d_out = nullptr, *d_buf[2] = {nullptr, nullptr}, *d_err = nullptr;
     uint8_t *d_status = nullptr;
-    double *d_boxes = nullptr, *d_obox = nullptr;
-    float *d_sets = nullptr;
-    int *d_cnt = nullptr, *d_setcnt = nullptr, *d_nsteps = nullptr, *d_tot = nullptr, *d_last = nullptr;
+    double *d_boxes = nullptr;
+    int *d_cnt = nullptr, *d_tot = nullptr, *d_last = nullptr;
     // forward calls: inputs [counts | (256-B aligned) points], outputs [status | (aligned) points] (one copy each)
     float *d_fin = nullptr, *d_fout = nullptr, *d_ferr = nullptr;
     uint8_t *d_fstatus = nullptr;
@@ -195,14 +208,27 @@ struct Tracker2DFlow::DeviceBuffers {
         in = (float *)(base + in_off_in);
     }
     // pinned staging: forward inputs, then results
-    float *h_fin = nullptr, *h_fwd_out = nullptr, *h_sets = nullptr;
+    float *h_fin = nullptr, *h_fwd_out = nullptr;
     uint8_t *h_fwd_st = nullptr;
-    double *h_obox = nullptr;
-    int *h_fcnt = nullptr, *h_setcnt = nullptr, *h_nsteps = nullptr;
+    int *h_fcnt = nullptr;
     // the chain's results live in one block per side, [nsteps | set counts | boxes | sets], so that
     // one memset clears the counters and one copy returns every used byte
-    char *d_res = nullptr, *h_res = nullptr;
+    // Three result blocks, used by consecutive passes in turn: a pass's block is
+    // read by the next frame's forward launch (its set 0: the trackers' features)
+    // while the chains of the frame after write theirs.
+    static constexpr int kResBlocks = kT2dResBlocks;
+    char *d_res[kResBlocks] = {}, *h_res[kResBlocks] = {};
     size_t res_sets_off = 0;
+    struct ResView {
+        int *nsteps, *setcnt;
+        double *obox;
+        float *sets;
+    };
+    ResView view(char *base) const {
+        ResView v{};
+        carve(base, v.obox, v.sets, v.setcnt, v.nsteps, nchains, PSN_T2D_CHAIN_STEPS);
+        return v;
+    }
     void carve(char *base, double *&obox, float *&sets, int *&setcnt, int *&nsteps, size_t K, size_t S) const {
         nsteps = (int *)base;
         setcnt = nsteps + K;
@@ -217,21 +243,18 @@ struct Tracker2DFlow::DeviceBuffers {
             if (p) (void)hipHostFree(p);
     }
     void release_chains() {
-        free_all({d_inblk, d_out, d_buf[0], d_buf[1], d_err, d_status, d_res, d_tot}, {h_res});
+        free_all({d_inblk, d_out, d_buf[0], d_buf[1], d_err, d_status, d_res[0], d_res[1], d_res[2], d_tot},
+                 {h_res[0], h_res[1], h_res[2]});
         for (Stage &g : stage) {
             free_all({}, {g.h_inblk, g.h_rawcnt});
             g = Stage();
         }
         d_inblk = nullptr;
-        d_in = d_out = d_buf[0] = d_buf[1] = d_err = d_sets = nullptr;
+        d_in = d_out = d_buf[0] = d_buf[1] = d_err = nullptr;
         d_status = nullptr;
-        d_boxes = d_obox = nullptr;
-        d_res = nullptr;
-        d_cnt = d_setcnt = d_nsteps = d_tot = d_last = nullptr;
-        h_sets = nullptr;
-        h_obox = nullptr;
-        h_res = nullptr;
-        h_setcnt = h_nsteps = nullptr;
+        d_boxes = nullptr;
+        for (int r = 0; r < kResBlocks; r++) d_res[r] = h_res[r] = nullptr;
+        d_cnt = d_tot = d_last = nullptr;
         nchains = 0;
     }
     void release_forward() {
@@ -270,7 +293,8 @@ void Tracker2DFlow::Finalize() {
         (void)hipStreamDestroy((hipStream_t)chain_stream_);
         chain_stream_ = nullptr;
     }
-    for (void **e : {&ev_chain_, &ev_fwd_})
+    for (void **e : {&ev_chain_, &ev_fwd_, &ev_set0_[0], &ev_set0_[1], &ev_set0_[2], &ev_fread_[0], &ev_fread_[1],
+                     &ev_fread_[2]})
         if (*e) {
             (void)hipEventDestroy((hipEvent_t)*e);
             *e = nullptr;
@@ -286,7 +310,13 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
     DeviceBuffers &b = *dev_;
     if (b.nchains >= nchains && b.d_in) return PSN_LK_OK;
     if (lk_) psn_lk_sync(lk_);
+    // a forward launch may still read a result block's set 0
+    if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
     b.release_chains();
+    for (int r = 0; r < DeviceBuffers::kResBlocks; r++) {
+        chain_info_[r].valid = false;
+        fread_rec_[r] = false;
+    }
     const size_t K = std::max<size_t>(nchains, 16);
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, npt = K * cap;
     bool ok = true;
@@ -301,9 +331,9 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
     dm((void **)&b.d_status, npt);
     b.res_sets_off = DeviceBuffers::res_box_off(K, S) + K * S * 4 * 8;
     const size_t res_bytes = b.res_sets_off + K * S * cap * 8;
-    dm((void **)&b.d_res, res_bytes);
+    for (int r = 0; r < DeviceBuffers::kResBlocks; r++) dm((void **)&b.d_res[r], res_bytes);
     dm((void **)&b.d_tot, K * 4);
-    hm((void **)&b.h_res, res_bytes);
+    for (int r = 0; r < DeviceBuffers::kResBlocks; r++) hm((void **)&b.h_res[r], res_bytes);
     for (DeviceBuffers::Stage &g : b.stage) {
         hm((void **)&g.h_inblk, b.in_bytes);
         hm((void **)&g.h_rawcnt, K * 4);
@@ -313,10 +343,8 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
         err_ = "chain buffers: allocation failed";
         return PSN_LK_ERR_NOMEM;
     }
-    b.carve(b.d_res, b.d_obox, b.d_sets, b.d_setcnt, b.d_nsteps, K, S);
     b.carve_in(b.d_inblk, b.d_boxes, b.d_last, b.d_cnt, b.d_in);
     for (DeviceBuffers::Stage &g : b.stage) b.carve_in(g.h_inblk, g.h_boxes, g.h_last, g.h_cnt, g.h_in);
-    b.carve(b.h_res, b.h_obox, b.h_sets, b.h_setcnt, b.h_nsteps, K, S);
     b.nchains = K;
     return PSN_LK_OK;
 }
@@ -328,6 +356,13 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     DeviceBuffers &b = *dev_;
     if (b.nfwd_pts >= nfwd_pts && b.nfwd_jobs >= nfwd_jobs && b.d_fin) return PSN_LK_OK;
     if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+    // results of a pass not unpacked yet (its copy was enqueued) move to the new buffers
+    std::vector<uint8_t> keep_st;
+    std::vector<float> keep_pts;
+    if (b.h_foblk) {
+        keep_st.assign(b.h_fwd_st, b.h_fwd_st + b.nfwd_pts);
+        keep_pts.assign(b.h_fwd_out, b.h_fwd_out + 2 * b.nfwd_pts);
+    }
     b.release_forward();
     const size_t F = std::max<size_t>(nfwd_pts, 1024), J = std::max<size_t>(nfwd_jobs, 16);
     bool ok = true;
@@ -353,6 +388,10 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     b.d_fout = (float *)(b.d_foblk + b.fo_off_pts);
     b.h_fwd_st = (uint8_t *)b.h_foblk;
     b.h_fwd_out = (float *)(b.h_foblk + b.fo_off_pts);
+    if (!keep_st.empty()) {
+        std::memcpy(b.h_fwd_st, keep_st.data(), keep_st.size());
+        std::memcpy(b.h_fwd_out, keep_pts.data(), keep_pts.size() * sizeof(float));
+    }
     b.nfwd_pts = F;
     b.nfwd_jobs = J;
     return PSN_LK_OK;
@@ -363,6 +402,13 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
 static int window_error(int win) {
     if (win <= 2) return PSN_LK_ERR_WINSIZE;
     if ((long)win * win > PSN_LK_MAX_WIN_PIXELS) return PSN_LK_ERR_UNSUPPORTED;
+    return PSN_LK_OK;
+}
+
+// The same for a forward call's box window (:877).
+int Tracker2DFlow::forward_window_error(int w, int h) {
+    if (w <= 2 || h <= 2) return PSN_LK_ERR_WINSIZE;
+    if ((long)w * h > PSN_LK_MAX_WIN_PIXELS) return PSN_LK_ERR_UNSUPPORTED;
     return PSN_LK_OK;
 }
 
@@ -392,7 +438,7 @@ int Tracker2DFlow::PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t 
 
 // 1-2 of the pass: features and the backward chains, on the chain stream.
 int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uint32_t seed) {
-    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS;
+    const size_t cap = PSN_T2D_CHAIN_CAP;
     size_t K = 0;
     for (PassCam &p : pc) {
         p.k0 = K;
@@ -400,10 +446,35 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
     }
     const int si = stage_;  // this pass's staging set
     stage_ ^= 1;
-    for (PassCam &p : pc) p.set = si;
+    const int rb = next_rb_;  // this pass's result block
+    next_rb_ = (rb + 1) % DeviceBuffers::kResBlocks;
+    last_rb_ = rb;
+    for (PassCam &p : pc) {
+        p.set = si;
+        p.rb = rb;
+    }
     std::vector<char> &win_bad_ = win_bad_sets_[si];
     win_bad_.assign(K, 0);
-    if (K == 0) return PSN_LK_OK;
+    // what the next frame's forward launch reads of this pass: per detection the
+    // forward window of its box (the tracker it becomes keeps the box, :1087)
+    ChainInfo &ci = chain_info_[rb];
+    ci.K = K;
+    ci.valid = false;
+    ci.k0.assign(cams_.size(), 0);
+    ci.ndet.assign(cams_.size(), 0);
+    ci.win.assign(K, {0, 0});
+    for (PassCam &p : pc) {
+        ci.k0[p.cam] = p.k0;
+        ci.ndet[p.cam] = p.dets->size();
+        for (size_t i = 0; i < p.dets->size(); i++) {
+            const Rect box = (*p.dets)[i].box.scale(kFlowScale);
+            ci.win[p.k0 + i] = {(int)(box.w * kWinSizeRatio), (int)(box.h * kWinSizeRatio)};
+        }
+    }
+    if (K == 0) {
+        ci.valid = true;
+        return PSN_LK_OK;
+    }
     int rc = EnsureChains(K);
     if (rc) return rc;
     DeviceBuffers::Stage &b = dev_->stage[si];
@@ -477,21 +548,24 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
             chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, db.in_off_in + K * cap * 8, hipMemcpyHostToDevice, st),
                 "chain inputs");
         }
-        // the feature-minimum gate and the cleared step / set counters in one launch
-        if (!rc)
-            rc = psn_t2d_chain_begin_device(db.d_cnt, (int)K, (int)kT2dMinFeatures, db.d_last, db.d_nsteps,
-                                            (int)(db.nchains * (1 + S)), st);
         if (rc) return rc;
+        // the result block's last reader (a forward launch three frames back) first
+        if (fread_rec_[rb]) chk(hipStreamWaitEvent(st, (hipEvent_t)ev_fread_[rb], 0), "result block reuse");
+        const DeviceBuffers::ResView rv = db.view(db.d_res[rb]);
         psn_t2d_chain_dev cd{};
         cd.ndet = (int)K;
         cd.cap = (int)cap;
         cd.boxes = db.d_boxes;
         cd.cnt = db.d_cnt;
-        cd.out_boxes = db.d_obox;
-        cd.sets = db.d_sets;
-        cd.set_cnt = db.d_setcnt;
-        cd.nsteps = db.d_nsteps;
+        cd.cur = db.d_in;
+        cd.out_boxes = rv.obox;
+        cd.sets = rv.sets;
+        cd.set_cnt = rv.setcnt;
+        cd.nsteps = rv.nsteps;
         cd.last_step = db.d_last;
+        // cleared counters, set 0 = the features at t, the feature-minimum gate: one launch
+        if (!rc) rc = psn_t2d_chain_begin_device(&cd, (int)kT2dMinFeatures, st);
+        if (rc) return rc;
         for (int step = 1; step <= max_steps; step++) {
             queries_.clear();
             for (PassCam &p : pc) {
@@ -520,9 +594,76 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
             cd.next_in = db.d_buf[(step + 1) & 1];
             rc = psn_t2d_chain_step_device(&cd, step, st);
             if (rc) return fail(rc, "psn_t2d_chain_step_device");
+            // set 0 is final after step 1: the next frame's forward launch may read it
+            if (step == 1) chk(hipEventRecord((hipEvent_t)ev_set0_[rb], st), "set-0 event");
         }
+        if (max_steps == 0) chk(hipEventRecord((hipEvent_t)ev_set0_[rb], st), "set-0 event");
+        ci.valid = rc == PSN_LK_OK;
     }
     return rc;
+}
+
+// The forward calls of frame t+1 (:871-877) straight from frame t's chain pass
+// (result block src_rb): every detection of frame t becomes an active tracker
+// -- matched ones take the detection's box and its set 0, new ones start from
+// them (:1087, :1104, :1112-1147) -- so their LK inputs are on the device before
+// the host has matched frame t. One counted launch on the forward stream, after
+// the pass's set 0 is final and the frames are built: query k reads set 0 of
+// detection k (count = its set-0 count, 0 for a detection that is no tracker)
+// with the window of its box; the outputs land at the same index in the forward
+// result block. pc: the pass of frame t+1 (its frames adopted).
+int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb) {
+    for (PassCam &p : pc) p.fwd_rb = -1;
+    if (src_rb < 0 || !chain_info_[src_rb].valid || chain_info_[src_rb].K == 0 || !dev_ || !dev_->d_res[src_rb])
+        return PSN_LK_OK;
+    const ChainInfo &ci = chain_info_[src_rb];
+    const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, K = ci.K;
+    int rc = EnsureForward(K * S * cap, K);
+    if (rc) return rc;
+    DeviceBuffers &b = *dev_;
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    fwd_queries_.assign(K, psn_lk_query{});
+    for (PassCam &p : pc) {
+        if (p.cam >= ci.k0.size()) continue;
+        const Cam &cam = cams_[p.cam];
+        for (size_t i = 0; i < ci.ndet[p.cam]; i++) {
+            const size_t k = ci.k0[p.cam] + i;
+            psn_lk_query &q = fwd_queries_[k];
+            psn_lk_default_params(&q.params);  // maxLevel 3, (COUNT|EPS, 30, 0.01), minEig 1e-4
+            q.prev_slot = cam.ring[kT2dInterval - 2];  // frame t -> t+1
+            q.next_slot = cam.ring[kT2dInterval - 1];
+            q.first_pt = (int)(k * S * cap);
+            q.num_pts = (int)cap;
+            const int ww = ci.win[k].first, wh = ci.win[k].second;
+            // a window the LK cannot run: a placeholder (the frame fails at its
+            // completion if that detection became a tracker, as the reference's
+            // CV_Assert would)
+            const bool ok = forward_window_error(ww, wh) == PSN_LK_OK;
+            q.params.win_w = ok ? ww : 3;
+            q.params.win_h = ok ? wh : 3;
+        }
+    }
+    const DeviceBuffers::ResView rv = b.view(b.d_res[src_rb]);
+    if (hipStreamWaitEvent(fs, (hipEvent_t)ev_set0_[src_rb], 0) != hipSuccess) {
+        err_ = "forward: set-0 event";
+        return PSN_LK_ERR_HIP;
+    }
+    rc = psn_lk_set_stream(lk_, fs);
+    if (!rc)
+        rc = psn_lk_track_device_counted_strided(lk_, fwd_queries_.data(), (int)K, rv.setcnt, (int)S, rv.sets, b.d_fout,
+                                                 b.d_fstatus, b.d_ferr);
+    const int rs = psn_lk_set_stream(lk_, st);
+    if (rc || rs) return fail(rc ? rc : rs, "forward launch");
+    if (hipEventRecord((hipEvent_t)ev_fread_[src_rb], fs) != hipSuccess) {
+        err_ = "forward: read event";
+        return PSN_LK_ERR_HIP;
+    }
+    fread_rec_[src_rb] = true;
+    for (PassCam &p : pc) {
+        p.fwd_rb = src_rb;
+        p.fwd_n = K * S * cap;
+    }
+    return PSN_LK_OK;
 }
 
 // 3 of the pass: the forward calls of every camera's trackers, on the forward
@@ -617,9 +758,11 @@ int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
             for (const Job &jb : *p.fwd) F += jb.in->size();
     }
     hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
-    if (K && bp)
-        chk(hipMemcpyAsync(bp->h_res, bp->d_res, bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
+    const int rb = pc.empty() ? -1 : pc[0].rb;
+    if (K && bp && rb >= 0)
+        chk(hipMemcpyAsync(bp->h_res[rb], bp->d_res[rb], bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
             "chain results");
+    if (!pc.empty() && pc[0].fwd_rb >= 0) F = pc[0].fwd_n;  // the forward launch from the previous frame's chains
     if (F && bp) {
         // status and points in one copy
         chk(hipMemcpyAsync(bp->h_foblk, bp->d_foblk, bp->fo_off_pts + F * 8, hipMemcpyDeviceToHost, fs),
@@ -684,20 +827,36 @@ void Tracker2DFlow::PassUnpack(std::vector<PassCam> &pc) {
     for (PassCam &p : pc) {
         std::vector<Chain> chains;
         BackwardBegin(*p.dets, *p.features, *p.out, chains);  // valid detections, in order
+        const DeviceBuffers::ResView hv = p.out->empty() ? DeviceBuffers::ResView{} : bp->view(bp->h_res[p.rb]);
         for (DetectedObject &ob : *p.out) {
             const size_t k = p.k0 + ob.id;  // the detection index = its device chain
-            const int ns = bp->h_nsteps[k];
+            const int ns = hv.nsteps[k];
             for (int s2 = 1; s2 <= ns; s2++) {
-                const double *r = bp->h_obox + (k * S + s2) * 4;
+                const double *r = hv.obox + (k * S + s2) * 4;
                 ob.boxes.push_back(Rect(r[0], r[1], r[2], r[3]).scale(1.0 / kFlowScale));
             }
             for (int r = 0; ns > 0 && r <= ns; r++) {
-                const int m = bp->h_setcnt[k * S + r];
-                const float *pp = bp->h_sets + (k * S + r) * cap * 2;
+                const int m = hv.setcnt[k * S + r];
+                const float *pp = hv.sets + (k * S + r) * cap * 2;
                 std::vector<Point2f> v((size_t)m);
                 for (int i = 0; i < m; i++) v[(size_t)i] = Point2f{pp[2 * i], pp[2 * i + 1]};
                 ob.vecvecTrackedFeatures.push_back(std::move(v));
             }
+        }
+        if (p.fwd_rb >= 0) {  // forward outputs of the camera's trackers, at their source detection's index
+            Cam &cam = cams_[p.cam];
+            cam.fstatus.assign(cam.trackers.size(), {});
+            for (size_t j = 0; j < cam.trackers.size(); j++) {
+                Tracker2D *tr = cam.trackers[j];
+                const size_t off = (cam.fwd_k0 + (size_t)tr->srcDet) * S * cap, m = tr->featurePoints.size();
+                tr->trackedPoints.resize(m);
+                cam.fstatus[j].resize(m);
+                for (size_t i = 0; i < m; i++) {
+                    tr->trackedPoints[i] = Point2f{bp->h_fwd_out[2 * (off + i)], bp->h_fwd_out[2 * (off + i) + 1]};
+                    cam.fstatus[j][i] = bp->h_fwd_st[off + i];
+                }
+            }
+            continue;
         }
         if (!p.fwd) continue;
         for (size_t j = 0, off = p.f0; j < p.fwd->size(); j++) {
@@ -1199,8 +1358,12 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
     if (rc) return rc;
     run_frame_ = frameIdx;
     run_gridfast_ = gridfast;
-    AttachForward(run_pass_);
-    rc = PassLaunch(run_pass_, gridfast, seed);
+    // frame t's forward calls from frame t-1's chain pass (when it left trackers),
+    // then frame t's features and chains
+    bool any = false;
+    for (const Cam &cam : cams_) any = any || !cam.active.empty();
+    rc = any ? LaunchForwardFromChains(run_pass_, last_rb_) : PSN_LK_OK;
+    if (!rc) rc = PassLaunchChains(run_pass_, gridfast, seed);
     if (rc) {
         (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
@@ -1209,17 +1372,6 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
     return rc;
 }
 
-// the forward calls of every camera's active trackers (m_queueActiveTracker2D
-// after the previous frame's update) into the pass
-void Tracker2DFlow::AttachForward(std::vector<PassCam> &pass) {
-    for (size_t c = 0; c < cams_.size(); c++) {
-        Cam &cam = cams_[c];
-        cam.trackers.assign(cam.active.begin(), cam.active.end());
-        cam.fwd.clear();
-        ForwardJobs(c, cam.trackers, cam.fstatus, cam.fwd);
-        pass[c].fwd = &cam.fwd;
-    }
-}
 
 // Wait for the frame's device work, then per camera: overlap flags (:824-835),
 // matching costs + majority gate (:906-1022), assignment and tracker update
@@ -1245,29 +1397,38 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     const clk::time_point t0 = clk::now();
     auto stamp = [&](int i) { host_us_[i] += std::chrono::duration<double, std::micro>(clk::now() - t0).count(); };
     frame_completed_ = false;
+    const int cur_rb = run_pass_.empty() ? -1 : run_pass_[0].rb;
+    std::vector<size_t> cur_k0(cams_.size(), 0);
+    for (const PassCam &p : run_pass_) cur_k0[p.cam] = p.k0;
     int rc = PassCopy(run_pass_);
     const bool early = !rc && next && ChainsFit(*next);
     int prc = PSN_LK_OK;
     std::vector<PassCam> pre;
-    // a next frame that cannot be launched leaves no trace: its chains drained,
-    // its frames staged again (the rings as before), frame t still completed
+    const int saved_next_rb = next_rb_, saved_last_rb = last_rb_;
+    // a next frame that cannot be launched leaves no trace: its work drained, its
+    // frames staged again (the rings as before), frame t still completed
     auto abandon_next = [&]() {
         (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
         UnadoptFrames();
+        next_rb_ = saved_next_rb;
+        last_rb_ = saved_last_rb;
         pre.clear();
     };
+    // frame t+1: its forward calls straight from frame t's chains (every detection
+    // of frame t becomes a tracker), then its features and chains
     auto prelaunch = [&]() {
         prc = AdoptFrames(*next, nextGridfast, pre);
         if (prc) {
             pre.clear();
             return;
         }
-        prc = PassLaunchChains(pre, nextGridfast, nextSeed);
+        prc = LaunchForwardFromChains(pre, cur_rb);
+        if (!prc) prc = PassLaunchChains(pre, nextGridfast, nextSeed);
         if (prc) abandon_next();
     };
     if (early) prelaunch();
-    stamp(0);  // copies + next chains enqueued
+    stamp(0);  // copies + next frame's forward + chains enqueued
     if (!rc) rc = PassSync();
     stamp(1);  // device work done
     if (!rc) rc = PassFeatures(run_pass_, run_gridfast_);
@@ -1283,24 +1444,30 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     for (size_t c = 0; c < cams_.size(); c++) {
         Cam &cam = cams_[c];
         CamFrame &f = io[c];
+        // a tracker whose box window the forward LK cannot run: CV_Assert in the reference
+        for (const Tracker2D *tr : cam.trackers) {
+            const Rect b = tr->boxes.back().scale(kFlowScale);
+            const int we = forward_window_error((int)(b.w * kWinSizeRatio), (int)(b.h * kWinSizeRatio));
+            if (we) {
+                err_ = "camera " + std::to_string(c) + ": tracker " + std::to_string(tr->id) + " forward window";
+                if (next && !prc && !pre.empty()) abandon_next();
+                return we;
+            }
+        }
         BackwardEnd(f.objects, f.features);
         ForwardDone(cam.trackers, cam.fstatus, f.objects, f.cost);
         const std::vector<int> match = AssignDetections(f.cost, f.objects.size(), cam.trackers.size());
         MatchingAndUpdating(f.objects, cam.active, cam.storage, match, run_frame_, cam.newTrackerID, f.result);
         f.result.camID = cam.camID;
+        // the next frame's forward calls (launched from this frame's chains): these trackers
+        cam.trackers.assign(cam.active.begin(), cam.active.end());
+        cam.fwd_k0 = cur_k0[c];
     }
     stamp(3);  // matched, trackers updated
     host_calls_++;
     frame_completed_ = true;
     if (!next || prc) return prc;
-    // frame t+1's forward calls: the trackers as frame t's update left them
-    AttachForward(pre);
-    prc = PassLaunchForward(pre);
-    stamp(4);  // next forward enqueued
-    if (prc) {
-        abandon_next();
-        return prc;
-    }
+    stamp(4);
     run_pass_ = std::move(pre);
     run_frame_ = nextFrameIdx;
     run_gridfast_ = nextGridfast;

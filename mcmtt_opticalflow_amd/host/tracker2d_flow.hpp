@@ -28,6 +28,7 @@ constexpr int kT2dInterval = 4;          // PSN_2D_BACKTRACKING_INTERVAL (:16)
 constexpr int kSlotsPerCam = kT2dInterval + 1;  // the ring + one slot the next frame is staged in
 constexpr size_t kT2dMinFeatures = 4;    // PSN_2D_FEATURE_MIN_NUM_TRACK (:12)
 constexpr size_t kT2dMaxFeatures = 100;  // PSN_2D_FEATURE_MAX_NUM_TRACK (:13)
+constexpr int kT2dResBlocks = 3;         // chain result blocks used in turn by consecutive passes
 constexpr double kFlowScale = 1.0;       // PSN_2D_OPTICALFLOW_SCALE (:18)
 constexpr double kWinSizeRatio = 1.0;    // PSN_2D_FEATURE_WIN_SIZE_RATIO (:15)
 
@@ -157,6 +158,7 @@ class Tracker2DFlow {
         std::deque<Tracker2D *> active;
         unsigned newTrackerID = 0;
         std::vector<Tracker2D *> trackers;               // this frame's forward inputs
+        size_t fwd_k0 = 0;  // first chain, in the pass that made them, of the detections they came from
         std::vector<std::vector<uint8_t>> fstatus;
         std::vector<Job> fwd;
     };
@@ -170,10 +172,27 @@ class Tracker2DFlow {
         std::vector<Job> *fwd;
         size_t k0, j0, f0;  // first chain / forward job / forward point of this camera in the pass
         int set;            // the pass's staging set of chain inputs
+        int rb = -1;        // the pass's result block
+        int fwd_rb = -1;    // the result block its forward calls read (LaunchForwardFromChains), or -1
+        size_t fwd_n = 0;   // forward outputs to copy back (that launch's index range)
     };
     int PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);  // chains, then forward
     int PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);
     int PassLaunchForward(std::vector<PassCam> &pc);
+    int LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb);
+    static int forward_window_error(int w, int h);
+    // what a chain pass leaves for the next frame's forward launch
+    struct ChainInfo {
+        bool valid = false;
+        size_t K = 0;
+        std::vector<size_t> k0, ndet;                // per camera
+        std::vector<std::pair<int, int>> win;        // per chain: the forward window of the detection's box
+    };
+    ChainInfo chain_info_[kT2dResBlocks];
+    int next_rb_ = 0, last_rb_ = -1;
+    void *ev_set0_[3] = {nullptr, nullptr, nullptr};   // hipEvent_t: a block's set 0 is final (chain stream)
+    void *ev_fread_[3] = {nullptr, nullptr, nullptr};  // hipEvent_t: the forward launch reading a block is done
+    bool fread_rec_[3] = {false, false, false};
     int PassComplete(std::vector<PassCam> &pc, bool gridfast);  // PassWait + PassFeatures + PassUnpack
     int PassWait(std::vector<PassCam> &pc);  // PassCopy + PassSync
     int PassCopy(std::vector<PassCam> &pc);  // enqueue the result copies, record the completion events
@@ -222,7 +241,6 @@ class Tracker2DFlow {
     void UnadoptFrames();  // AdoptFrames undone: frame t's slot back to staging, the oldest back in the ring
     bool frame_completed_ = false;
     std::vector<PassCam> run_pass_;  // the pass between RunLaunch and RunComplete
-    void AttachForward(std::vector<PassCam> &pass);
     std::vector<CamFrame> *pre_io_ = nullptr;  // the io of a frame RunComplete launched ahead
     bool launched_ahead_ = false;              // run_pass_ is that frame, awaiting its RunLaunch
     double host_us_[5] = {0, 0, 0, 0, 0};

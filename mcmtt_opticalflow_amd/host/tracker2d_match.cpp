@@ -312,6 +312,7 @@ void MatchingAndUpdating(std::vector<DetectedObject> &dets, std::deque<Tracker2D
         result.object2DInfos.push_back(std::move(info));
         tr->featurePoints = det.vecvecTrackedFeatures.front();
         tr->trackedPoints.clear();
+        tr->srcDet = (int)det.id;
     }
     for (DetectedObject &det : dets) {
         if (det.bMatchedWithTracker) continue;
@@ -323,6 +324,7 @@ void MatchingAndUpdating(std::vector<DetectedObject> &dets, std::deque<Tracker2D
         nt.boxes.push_back(det.detection.box);
         nt.heads.push_back(det.detection.vecPartBoxes.empty() ? Rect() : det.detection.vecPartBoxes.front());
         nt.featurePoints = det.vecvecTrackedFeatures.front();
+        nt.srcDet = (int)det.id;
         nt.confidence = 1.0;
         for (int k = 0; k < 3; k++) nt.lastPosition[k] = det.location[k];
         nt.height = det.height;
