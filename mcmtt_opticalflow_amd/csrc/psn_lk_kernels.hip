@@ -20,6 +20,8 @@
 #include <float.h>
 #include <limits.h>
 
+#include <type_traits>
+
 #include "psn_gridfast.h"
 #include "psn_lk_kernels.h"
 
@@ -2494,12 +2496,22 @@ __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax
     do {            \
     } while (0)
 #endif
+// XCD-aware workgroup order (MI355X_MICROARCH.md, workgroup dispatch: blocks are
+// dealt round-robin over the 8 XCDs, each with its own L2): hardware block b
+// runs logical workgroup xcd_remap(b), so that logical workgroups [x*q, ...) --
+// consecutive points of one box, whose windows overlap -- share one XCD's L2.
+// A bijection for any n (speed only, never correctness).
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7, j = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
+
 template <int UPT, bool NOTAIL>
 __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NT = kBxNT;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int g = blockIdx.x;
+    const int g = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
     const LkQueryDev &Q = A.q[qi];
@@ -2932,7 +2944,10 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             int dmax = 0;
             unsigned zm;
             asm volatile("v_mov_b32 %0, 0" : "=v"(zm));
-            {
+            // every term d * g is an exact float unless |g| > 2^24 / 8160 (|d| <= 8160):
+            // below that in the whole wave, the pass keeps no max |d|
+            const bool dtrack = __ballot(gmax > kExact / 8160) != 0ull;
+            auto bmain = [&](auto trk) {
                 // the unit's J row in dwords, stepped unit by unit (row-major units: +1, or
                 // to the next row's first quad); opaque start: no per-unit address hoisting
                 int q = q0, off = (oy + y0) * JRP4 + (ox >> 2) + q0;
@@ -2949,7 +2964,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         const int gy = ((i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]));
                         t1[i] = __mul24(d[i], gx);
                         t2[i] = __mul24(d[i], gy);
-                        dmax = max(dmax, abs(d[i]));
+                        if constexpr (decltype(trk)::value) dmax = max(dmax, abs(d[i]));
                     }
                     if (NOTAIL) {  // every unit feeds lane chains 0-3
 #pragma unroll
@@ -2984,7 +2999,11 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     asm volatile("" : "+v"(M2[0]), "+v"(M2[1]), "+v"(M2[2]), "+v"(M2[3]), "+v"(M2[4]), "+v"(m2[0]),
                                  "+v"(m2[1]), "+v"(m2[2]), "+v"(m2[3]), "+v"(m2[4]), "+v"(dmax));
                 }
-            }
+            };
+            if (dtrack)
+                bmain(std::true_type());
+            else
+                bmain(std::false_type());
             // masked pixels carry zero gradients but any d: only real terms count
             const bool bad = (long long)dmax * gmax > (long long)kExact;
             int T[10], M[10], m[10];
@@ -3275,7 +3294,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
         BX_CLK(t_end);
         bx_acc[15] = t_end - bx_t0;
         if (tid == 0 && A.stamps)  // thread 0: also the chain lane of the tile stamps 12-14
-            for (int i = 0; i < 16; i++) A.stamps[(size_t)blockIdx.x * 64 + i] = bx_acc[i];
+            for (int i = 0; i < 16; i++) A.stamps[(size_t)g * 64 + i] = bx_acc[i];
     }
 #endif
     if (tid == 0) {

@@ -1441,11 +1441,10 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     run_pass_.clear();
     if (next && !early) prelaunch();
     stamp(2);  // unpacked
-    for (size_t c = 0; c < cams_.size(); c++) {
-        Cam &cam = cams_[c];
-        CamFrame &f = io[c];
-        // a tracker whose box window the forward LK cannot run: CV_Assert in the reference
-        for (const Tracker2D *tr : cam.trackers) {
+    // a tracker whose box window the forward LK cannot run (CV_Assert in the
+    // reference) fails the frame before any camera is updated
+    for (size_t c = 0; c < cams_.size(); c++)
+        for (const Tracker2D *tr : cams_[c].trackers) {
             const Rect b = tr->boxes.back().scale(kFlowScale);
             const int we = forward_window_error((int)(b.w * kWinSizeRatio), (int)(b.h * kWinSizeRatio));
             if (we) {
@@ -1454,6 +1453,9 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
                 return we;
             }
         }
+    for (size_t c = 0; c < cams_.size(); c++) {
+        Cam &cam = cams_[c];
+        CamFrame &f = io[c];
         BackwardEnd(f.objects, f.features);
         ForwardDone(cam.trackers, cam.fstatus, f.objects, f.cost);
         const std::vector<int> match = AssignDetections(f.cost, f.objects.size(), cam.trackers.size());
