@@ -135,11 +135,14 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
         return PSN_LK_ERR_HIP;
     }
     fwd_stream_ = fs;
-    if (hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, greatest) != hipSuccess) {
-        err_ = "chain stream";
-        return PSN_LK_ERR_HIP;
+    for (int i = 0; i < 2; i++) {
+        if (hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, greatest) != hipSuccess) {
+            err_ = "chain stream";
+            return PSN_LK_ERR_HIP;
+        }
+        chain_streams_[i] = cs;
     }
-    chain_stream_ = cs;
+    cs = (hipStream_t)chain_streams_[0];
     hipEvent_t e1 = nullptr, e2 = nullptr;
     if (hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&e2, hipEventDisableTiming) != hipSuccess) {
@@ -148,6 +151,13 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
     }
     ev_chain_ = e1;
     ev_fwd_ = e2;
+    hipEvent_t e3 = nullptr;
+    if (hipEventCreateWithFlags(&e3, hipEventDisableTiming) != hipSuccess) {
+        err_ = "gridfast event";
+        return PSN_LK_ERR_HIP;
+    }
+    ev_gf_ = e3;
+    gf_rec_ = false;
     for (int r = 0; r < kT2dResBlocks; r++) {
         hipEvent_t a = nullptr, b = nullptr;
         if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
@@ -172,10 +182,15 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
 struct Tracker2DFlow::DeviceBuffers {
     size_t nchains = 0, nfwd_pts = 0, nfwd_jobs = 0;
     // chains: inputs, LK outputs, ping-pong point sets, err/status
-    float *d_in = nullptr, *d_out = nullptr, *d_buf[2] = {nullptr, nullptr}, *d_err = nullptr;
-    uint8_t *d_status = nullptr;
-    double *d_boxes = nullptr;
-    int *d_cnt = nullptr, *d_tot = nullptr, *d_last = nullptr;
+    // per staging set (a pass and its chain stream): inputs, LK outputs, ping-pong
+    // point sets, err/status -- consecutive passes run on the two chain streams at once
+    struct Scratch {
+        char *d_inblk = nullptr;
+        float *d_in = nullptr, *d_out = nullptr, *d_buf[2] = {nullptr, nullptr}, *d_err = nullptr;
+        uint8_t *d_status = nullptr;
+        double *d_boxes = nullptr;
+        int *d_cnt = nullptr, *d_tot = nullptr, *d_last = nullptr;
+    } sc[2];
     // forward calls: inputs [counts | (256-B aligned) points], outputs [status | (aligned) points] (one copy each)
     float *d_fin = nullptr, *d_fout = nullptr, *d_ferr = nullptr;
     uint8_t *d_fstatus = nullptr;
@@ -193,7 +208,6 @@ struct Tracker2DFlow::DeviceBuffers {
         double *h_boxes = nullptr;
         int *h_cnt = nullptr, *h_rawcnt = nullptr, *h_last = nullptr;
     } stage[2];
-    char *d_inblk = nullptr;
     size_t in_off_last = 0, in_off_cnt = 0, in_off_in = 0, in_bytes = 0;
     void layout_in(size_t K, size_t cap) {
         in_off_last = K * 32;
@@ -243,18 +257,16 @@ struct Tracker2DFlow::DeviceBuffers {
             if (p) (void)hipHostFree(p);
     }
     void release_chains() {
-        free_all({d_inblk, d_out, d_buf[0], d_buf[1], d_err, d_status, d_res[0], d_res[1], d_res[2], d_tot},
-                 {h_res[0], h_res[1], h_res[2]});
+        free_all({d_res[0], d_res[1], d_res[2]}, {h_res[0], h_res[1], h_res[2]});
+        for (Scratch &x : sc) {
+            free_all({x.d_inblk, x.d_out, x.d_buf[0], x.d_buf[1], x.d_err, x.d_status, x.d_tot}, {});
+            x = Scratch();
+        }
         for (Stage &g : stage) {
             free_all({}, {g.h_inblk, g.h_rawcnt});
             g = Stage();
         }
-        d_inblk = nullptr;
-        d_in = d_out = d_buf[0] = d_buf[1] = d_err = nullptr;
-        d_status = nullptr;
-        d_boxes = nullptr;
         for (int r = 0; r < kResBlocks; r++) d_res[r] = h_res[r] = nullptr;
-        d_cnt = d_tot = d_last = nullptr;
         nchains = 0;
     }
     void release_forward() {
@@ -274,6 +286,11 @@ struct Tracker2DFlow::DeviceBuffers {
     }
 };
 
+void Tracker2DFlow::SyncChains() {
+    for (void *cs : chain_streams_)
+        if (cs) (void)hipStreamSynchronize((hipStream_t)cs);
+}
+
 void Tracker2DFlow::Finalize() {
     if (dev_) {
         if (lk_) psn_lk_sync(lk_);
@@ -289,11 +306,13 @@ void Tracker2DFlow::Finalize() {
     }
     if (lk_) psn_lk_destroy(lk_);
     lk_ = nullptr;
-    if (chain_stream_) {
-        (void)hipStreamDestroy((hipStream_t)chain_stream_);
-        chain_stream_ = nullptr;
-    }
-    for (void **e : {&ev_chain_, &ev_fwd_, &ev_set0_[0], &ev_set0_[1], &ev_set0_[2], &ev_fread_[0], &ev_fread_[1],
+    for (void *&cs : chain_streams_)
+        if (cs) {
+            (void)hipStreamSynchronize((hipStream_t)cs);
+            (void)hipStreamDestroy((hipStream_t)cs);
+            cs = nullptr;
+        }
+    for (void **e : {&ev_chain_, &ev_fwd_, &ev_gf_, &ev_set0_[0], &ev_set0_[1], &ev_set0_[2], &ev_fread_[0], &ev_fread_[1],
                      &ev_fread_[2]})
         if (*e) {
             (void)hipEventDestroy((hipEvent_t)*e);
@@ -308,8 +327,9 @@ void Tracker2DFlow::Finalize() {
 int Tracker2DFlow::EnsureChains(size_t nchains) {
     if (!dev_) dev_ = new DeviceBuffers();
     DeviceBuffers &b = *dev_;
-    if (b.nchains >= nchains && b.d_in) return PSN_LK_OK;
+    if (b.nchains >= nchains && b.sc[0].d_in) return PSN_LK_OK;
     if (lk_) psn_lk_sync(lk_);
+    SyncChains();
     // a forward launch may still read a result block's set 0
     if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
     b.release_chains();
@@ -323,16 +343,18 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
     auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
     b.layout_in(K, cap);
-    dm((void **)&b.d_inblk, b.in_bytes);
-    dm((void **)&b.d_out, npt * 8);
-    dm((void **)&b.d_buf[0], npt * 8);
-    dm((void **)&b.d_buf[1], npt * 8);
-    dm((void **)&b.d_err, npt * 4);
-    dm((void **)&b.d_status, npt);
+    for (DeviceBuffers::Scratch &x : b.sc) {
+        dm((void **)&x.d_inblk, b.in_bytes);
+        dm((void **)&x.d_out, npt * 8);
+        dm((void **)&x.d_buf[0], npt * 8);
+        dm((void **)&x.d_buf[1], npt * 8);
+        dm((void **)&x.d_err, npt * 4);
+        dm((void **)&x.d_status, npt);
+        dm((void **)&x.d_tot, K * 4);
+    }
     b.res_sets_off = DeviceBuffers::res_box_off(K, S) + K * S * 4 * 8;
     const size_t res_bytes = b.res_sets_off + K * S * cap * 8;
     for (int r = 0; r < DeviceBuffers::kResBlocks; r++) dm((void **)&b.d_res[r], res_bytes);
-    dm((void **)&b.d_tot, K * 4);
     for (int r = 0; r < DeviceBuffers::kResBlocks; r++) hm((void **)&b.h_res[r], res_bytes);
     for (DeviceBuffers::Stage &g : b.stage) {
         hm((void **)&g.h_inblk, b.in_bytes);
@@ -343,7 +365,7 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
         err_ = "chain buffers: allocation failed";
         return PSN_LK_ERR_NOMEM;
     }
-    b.carve_in(b.d_inblk, b.d_boxes, b.d_last, b.d_cnt, b.d_in);
+    for (DeviceBuffers::Scratch &x : b.sc) b.carve_in(x.d_inblk, x.d_boxes, x.d_last, x.d_cnt, x.d_in);
     for (DeviceBuffers::Stage &g : b.stage) b.carve_in(g.h_inblk, g.h_boxes, g.h_last, g.h_cnt, g.h_in);
     b.nchains = K;
     return PSN_LK_OK;
@@ -478,8 +500,13 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
     int rc = EnsureChains(K);
     if (rc) return rc;
     DeviceBuffers::Stage &b = dev_->stage[si];
-    DeviceBuffers &db = *dev_;
-    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_);
+    DeviceBuffers &dall = *dev_;
+    DeviceBuffers::Scratch &db = dall.sc[si];
+    // the pass's chain stream (consecutive passes alternate: frame t+1's chains run
+    // beside frame t's tail); every LK launch of the pass goes to it
+    hipStream_t st = (hipStream_t)ChainStream(si);
+    rc = psn_lk_set_stream(lk_, st);
+    if (rc) return fail(rc, "chain stream");
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !rc) {
             err_ = std::string(what) + ": " + hipGetErrorString(e);
@@ -507,6 +534,9 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
             psn_gridfast_default_params(&gp);
             gp.cap = (int)cap;  // kT2dMaxFeatures
             std::vector<int> rois;
+            // the detector's cell scratch lives in the LK context: the previous
+            // pass's detections (on the other chain stream) are done with it first
+            if (gf_rec_) chk(hipStreamWaitEvent(st, (hipEvent_t)ev_gf_, 0), "gridfast scratch");
             for (PassCam &p : pc) {
                 const size_t n = p.dets->size();
                 if (!n) continue;
@@ -523,10 +553,12 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
                                                 db.d_in + 2 * cap * p.k0, db.d_cnt + p.k0, db.d_tot + p.k0);
                 if (rc) return fail(rc, "psn_gridfast_detect_device");
             }
+            chk(hipEventRecord((hipEvent_t)ev_gf_, st), "gridfast event");
+            gf_rec_ = !rc;
             chk(hipMemcpyAsync(b.h_rawcnt, db.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
             chk(hipMemcpyAsync(b.h_in, db.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
             // boxes and last steps (GridFAST wrote the counts and points on the device)
-            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, db.in_off_cnt, hipMemcpyHostToDevice, st), "chain boxes");
+            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, dall.in_off_cnt, hipMemcpyHostToDevice, st), "chain boxes");
         } else {
             for (PassCam &p : pc)
                 for (size_t i = 0; i < p.dets->size(); i++) {
@@ -545,13 +577,13 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
                 }
             // boxes, last steps, counts and points in one copy (whole rows: a chain
             // row's unused tail is never read)
-            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, db.in_off_in + K * cap * 8, hipMemcpyHostToDevice, st),
+            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, dall.in_off_in + K * cap * 8, hipMemcpyHostToDevice, st),
                 "chain inputs");
         }
         if (rc) return rc;
         // the result block's last reader (a forward launch three frames back) first
         if (fread_rec_[rb]) chk(hipStreamWaitEvent(st, (hipEvent_t)ev_fread_[rb], 0), "result block reuse");
-        const DeviceBuffers::ResView rv = db.view(db.d_res[rb]);
+        const DeviceBuffers::ResView rv = dall.view(dall.d_res[rb]);
         psn_t2d_chain_dev cd{};
         cd.ndet = (int)K;
         cd.cap = (int)cap;
@@ -757,7 +789,8 @@ int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
         if (p.fwd)
             for (const Job &jb : *p.fwd) F += jb.in->size();
     }
-    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    hipStream_t st = (hipStream_t)(pc.empty() ? psn_lk_get_stream(lk_) : ChainStream(pc[0].set)),
+                fs = (hipStream_t)fwd_stream_;
     const int rb = pc.empty() ? -1 : pc[0].rb;
     if (K && bp && rb >= 0)
         chk(hipMemcpyAsync(bp->h_res[rb], bp->d_res[rb], bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
@@ -875,7 +908,7 @@ void Tracker2DFlow::PassUnpack(std::vector<PassCam> &pc) {
 bool Tracker2DFlow::ChainsFit(const std::vector<CamFrame> &io) const {
     size_t K = 0;
     for (const CamFrame &f : io) K += f.dets.size();
-    return K == 0 || (dev_ && dev_->d_in && dev_->nchains >= K);
+    return K == 0 || (dev_ && dev_->sc[0].d_in && dev_->nchains >= K);
 }
 
 // One camera (0), one pass, synchronous.
@@ -890,7 +923,7 @@ int Tracker2DFlow::DevicePass(const std::vector<Detection> &dets, std::vector<st
     out.clear();
     int rc = PassLaunch(pc, gridfast, seed);
     if (rc) {  // drain what was enqueued before returning the error
-        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+        SyncChains();
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
         return rc;
     }
@@ -1365,7 +1398,7 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
     rc = any ? LaunchForwardFromChains(run_pass_, last_rb_) : PSN_LK_OK;
     if (!rc) rc = PassLaunchChains(run_pass_, gridfast, seed);
     if (rc) {
-        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+        SyncChains();
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
         run_pass_.clear();
     }
@@ -1408,7 +1441,7 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     // a next frame that cannot be launched leaves no trace: its work drained, its
     // frames staged again (the rings as before), frame t still completed
     auto abandon_next = [&]() {
-        (void)hipStreamSynchronize((hipStream_t)psn_lk_get_stream(lk_));
+        SyncChains();
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
         UnadoptFrames();
         next_rb_ = saved_next_rb;

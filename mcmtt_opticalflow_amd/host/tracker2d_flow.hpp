@@ -222,7 +222,13 @@ class Tracker2DFlow {
 
     psn_lk_ctx *lk_ = nullptr;
     void *fwd_stream_ = nullptr;    // hipStream_t of the forward launch, beside the chain's launches (lowest priority)
-    void *chain_stream_ = nullptr;  // the LK context's stream: the backward chains, the critical path (highest priority)
+    // the backward chains (highest priority): pass i of the staging set si runs on
+    // chain_streams_[si], so the chains of frame t+1 start beside frame t's last steps
+    void *ev_gf_ = nullptr;  // after a pass's GridFAST launches (the context's detector scratch)
+    bool gf_rec_ = false;
+    void *chain_streams_[2] = {nullptr, nullptr};
+    void *ChainStream(int si) const { return chain_streams_[si & 1]; }
+    void SyncChains();
     std::vector<psn_lk_query> fwd_queries_;
     std::vector<Cam> cams_;
     int width_ = 0, height_ = 0;
