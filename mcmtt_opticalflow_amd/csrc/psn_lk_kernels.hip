@@ -2364,19 +2364,39 @@ __device__ __forceinline__ void bx_publish(int (&T)[NC], int *rec, bool no_tail)
 #pragma unroll
     for (int c = 0; c < NC; c++) T[c] = incl[c] - T[c];
 }
-template <int NC>
-__device__ __forceinline__ void bx_check(const int (&E)[NC], const int (&M)[NC], const int (&m)[NC], bool bad, int *rec,
-                                         bool no_tail) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    bool fail = bad;
+// one wave's test (WV: its index, a compile-time constant of the caller's
+// scalar switch): the earlier waves' totals, then the extreme prefixes of all
+// chains folded by v_max3 / v_min3 into one comparison each
+template <int NC, int WV>
+__device__ __forceinline__ bool bx_check_wave(const int (&E)[NC], const int (&M)[NC], const int (&m)[NC], const int *rec,
+                                              bool no_tail) {
+    int hi = 0, lo = 0;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
         if (no_tail && c % 5 == 4) continue;
-        const int4 t = *(const int4 *)(rec + 8 * c);
-        const int p = (wv > 0 ? t.x : 0) + (wv > 1 ? t.y : 0) + (wv > 2 ? t.z : 0) + E[c];
-        fail |= (p + M[c] > kExact) | (p + m[c] < -kExact);
+        const int *r = rec + 8 * c;
+        int p = E[c];
+        if (WV > 0) p += r[0];
+        if (WV > 1) p += r[1];
+        if (WV > 2) p += r[2];
+        hi = max(hi, p + M[c]);
+        lo = min(lo, p + m[c]);
     }
-    const unsigned long long f = __ballot(fail);
+    return (hi > kExact) | (lo < -kExact);
+}
+template <int NC>
+__device__ __forceinline__ void bx_check(const int (&E)[NC], const int (&M)[NC], const int (&m)[NC], bool bad, int *rec,
+                                         bool no_tail) {
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);  // uniform: a scalar switch
+    bool fail;
+    switch (wv) {
+        case 0: fail = bx_check_wave<NC, 0>(E, M, m, rec, no_tail); break;
+        case 1: fail = bx_check_wave<NC, 1>(E, M, m, rec, no_tail); break;
+        case 2: fail = bx_check_wave<NC, 2>(E, M, m, rec, no_tail); break;
+        default: fail = bx_check_wave<NC, 3>(E, M, m, rec, no_tail); break;
+    }
+    const unsigned long long f = __ballot(fail | bad);
     if (lane == 0) rec[kBxHalfRec + wv] = f == 0ull ? 8 : 2 * wv + ((unsigned)f == 0u ? 1 : 0);
 }
 template <int NC>
@@ -2403,16 +2423,69 @@ __device__ __forceinline__ void run_add(int &T, int &M, int &m, int t) {
 
 __device__ __forceinline__ int lo16(unsigned v) { return (int)(short)(v & 0xffffu); }
 __device__ __forceinline__ int hi16(unsigned v) { return (int)v >> 16; }
+// v_dot2_i32_i16 in the VOP3 form with a scalar accumulator (a constant in an
+// SGPR: no copy into a tied VOP2 destination per use)
+__device__ __forceinline__ int sdot2k(unsigned a, unsigned b, int c) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+}
+// v_mad_i32_i16: int16 a (low half) x int16 half BH of b + c -- one instruction
+// for a chain term's extraction, product and running sum (op_sel picks the half)
+template <int BH>
+__device__ __forceinline__ int mad16(int a, unsigned b, int c) {
+    int r;
+    if constexpr (BH)
+        asm("v_mad_i32_i16 %0, %1, %2, %3 op_sel:[0,1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    else
+        asm("v_mad_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// the same with a's half AH: squares and cross products of packed gradient pairs
+template <int AH, int BH>
+__device__ __forceinline__ int mad16p(unsigned a, unsigned b, int c) {
+    int r;
+    if constexpr (AH && BH)
+        asm("v_mad_i32_i16 %0, %1, %2, %3 op_sel:[1,1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    else if constexpr (AH)
+        asm("v_mad_i32_i16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    else if constexpr (BH)
+        asm("v_mad_i32_i16 %0, %1, %2, %3 op_sel:[0,1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    else
+        asm("v_mad_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// two terms of one chain run: total, maximum and minimum prefix (v_max3 / v_min3)
+__device__ __forceinline__ void run2(int &T, int &M, int &m, int ta, int tb) {
+    M = max(M, max(ta, tb));
+    m = min(m, min(ta, tb));
+    T = tb;
+}
+// an opaque 256 of the caller's loop (one VGPR): the accumulator constant below
+// is then not loop-invariant, so no unit's constants are hoisted out of the loop
+__device__ __forceinline__ int opaque256() {
+    int c;
+    asm volatile("v_mov_b32 %0, 256" : "=v"(c));
+    return c;
+}
+// 256 - 512 I of the pair half picked by the scalar selector pair k ((-512, 0) or
+// (0, -512)): one VOP3 v_dot2 (separate accumulator: no copy of c per use)
+__device__ __forceinline__ int cw_dot(unsigned ip, unsigned k, int c) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(ip), "s"(k), "v"(c));
+    return r;
+}
 // J - I of one unit (4 pixels) from the byte J region: rows jp and jp + JRP4
 // (dwords), pairs selected by the uniform v_perm selectors s0..s3, packed-dot
 // bilinear with the diff folded into the accumulator constant 256 - 512 I
-// (I = the unit's window values, packed pairs ip).
+// (I = the unit's window values, packed pairs ip; one v_dot2 each with the
+// selector pairs (-512, 0) / (0, -512) and c256 = 256).
 __device__ __forceinline__ void bx_diffs(const uint32_t *jp, int JRP4, unsigned W0, unsigned W1, unsigned s0,
-                                         unsigned s1, unsigned s2, unsigned s3, const unsigned (&ipr)[2], int (&d)[4],
-                                         unsigned z) {
+                                         unsigned s1, unsigned s2, unsigned s3, const unsigned (&ip)[2], int (&d)[4],
+                                         int c256) {
     const uint32_t a0 = jp[0], a1 = jp[1], b0 = jp[JRP4], b1 = jp[JRP4 + 1];
-    const unsigned ip[2] = {ipr[0] ^ z, ipr[1] ^ z};  // z: an opaque zero of the caller's loop (no hoisting)
-    const int cw[4] = {256 - 512 * lo16(ip[0]), 256 - 512 * hi16(ip[0]), 256 - 512 * lo16(ip[1]), 256 - 512 * hi16(ip[1])};
+    const unsigned kl = 0x0000fe00u, kh = 0xfe000000u;  // (-512, 0), (0, -512)
+    const int cw[4] = {cw_dot(ip[0], kl, c256), cw_dot(ip[0], kh, c256), cw_dot(ip[1], kl, c256), cw_dot(ip[1], kh, c256)};
     d[0] = sdot2(__builtin_amdgcn_perm(b1, b0, s0), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s0), W0, cw[0])) >> 9;
     d[1] = sdot2(__builtin_amdgcn_perm(b1, b0, s1), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s1), W0, cw[1])) >> 9;
     d[2] = sdot2(__builtin_amdgcn_perm(b1, b0, s2), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s2), W0, cw[2])) >> 9;
@@ -2509,6 +2582,7 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
 template <int UPT, bool NOTAIL>
 __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    static_assert(UPT % 2 == 0, "units are processed in pairs");
     constexpr int NT = kBxNT;
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = xcd_remap((int)blockIdx.x, (int)gridDim.x);
@@ -2536,6 +2610,28 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
 
     const int u0 = tid * UPT;
     const int y0 = u0 / QW, q0 = u0 - y0 * QW;
+    // per unit of the thread: the byte offset of its J dwords in the region (row
+    // y * JRP + 4 q; 0 past the window, where the gradients are zero), two units
+    // per register (the b pass adds a half to the iteration's base: SDWA), and
+    // whether it is an SSE2 unit of the b chains (bit k)
+    unsigned UB[UPT / 2];
+    unsigned sseB = 0;
+    {
+        int y = y0, q = q0;
+#pragma unroll
+        for (int k = 0; k < UPT; k++) {
+            const unsigned o = u0 + k < U ? (unsigned)(y * JRP + 4 * q) : 0u;
+            if (k & 1)
+                UB[k >> 1] |= o << 16;
+            else
+                UB[k >> 1] = o;
+            sseB |= (unsigned)(q < nqB) << k;
+            if (++q == QW) {
+                q = 0;
+                y++;
+            }
+        }
+    }
 
     const float hwx = __fmul_rn((float)(w - 1), 0.5f), hwy = __fmul_rn((float)(h - 1), 0.5f);
     const float px0 = A.prev[2 * pi], py0 = A.prev[2 * pi + 1];
@@ -2610,7 +2706,13 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             const int sh = (ipx - 1) & 3;
             int T11[5] = {0, 0, 0, 0, 0}, T22[5] = {0, 0, 0, 0, 0}, T12[5] = {0, 0, 0, 0, 0};
             int M12[5] = {0, 0, 0, 0, 0}, m12[5] = {0, 0, 0, 0, 0};
-            gmax = 0;
+            int gmx = 0, gmn = 0;  // max / min gradient of the thread's pixels
+            // every derivative the window reads inside the image (columns ipx .. ipx +
+            // 4 QW + 1, rows ipy .. ipy + h): no border masks (uniform)
+            const bool interior = ipx >= 0 && ipy >= 0 && ipx + 4 * QW + 2 <= cols && ipy + h + 1 <= rows;
+            const int c256 = 1 << 8, c8192 = 1 << 13;  // scalar accumulators of the VOP3 v_dot2
+            auto apass = [&](auto inner) {
+            constexpr bool IN = decltype(inner)::value;
             int y = y0, q = q0;
             asm volatile("" : "+v"(y), "+v"(q));  // opaque: no per-unit address hoisting (VGPRs)
 #pragma unroll
@@ -2638,15 +2740,16 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 unsigned cm[3];
 #pragma unroll
                 for (int kk = 0; kk < 3; kk++)
-                    cm[kk] = ((unsigned)(ipx + 4 * qq + 2 * kk) < (unsigned)cols ? 0xffffu : 0u) |
-                             ((unsigned)(ipx + 4 * qq + 2 * kk + 1) < (unsigned)cols ? 0xffff0000u : 0u);
+                    cm[kk] = IN ? ~0u
+                                : ((unsigned)(ipx + 4 * qq + 2 * kk) < (unsigned)cols ? 0xffffu : 0u) |
+                                      ((unsigned)(ipx + 4 * qq + 2 * kk + 1) < (unsigned)cols ? 0xffff0000u : 0u);
                 // Scharr on packed pairs (|values| <= 4080: exact in 16 bits): DX/DY pairs
                 // (2k, 2k+1) of the two derivative rows o = 0, 1
                 unsigned DXp[2][3], DYp[2][3];
                 const s16x2 k3 = {3, 3}, k10 = {10, 10};
 #pragma unroll
                 for (int o = 0; o < 2; o++) {
-                    const unsigned rm = (unsigned)(ipy + yy + o) < (unsigned)rows ? ~0u : 0u;
+                    const unsigned rm = IN || (unsigned)(ipy + yy + o) < (unsigned)rows ? ~0u : 0u;
                     s16x2 SV[4], DV[4];
 #pragma unroll
                     for (int kk = 0; kk < 4; kk++) {
@@ -2673,19 +2776,20 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 int ix[4], iy[4], iv[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const bool pv = uv && 4 * qq + i < w;
+                    const bool pv = uv && (NOTAIL || 4 * qq + i < w);
                     const int h = i >> 1;
                     // pairs (i, i+1): even i from the stored pairs, odd i shifted by 16 bits
                     const unsigned x0 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[0][h + 1], DXp[0][h], 2) : DXp[0][h];
                     const unsigned x1 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[1][h + 1], DXp[1][h], 2) : DXp[1][h];
                     const unsigned y0_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[0][h + 1], DYp[0][h], 2) : DYp[0][h];
                     const unsigned y1_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[1][h + 1], DYp[1][h], 2) : DYp[1][h];
-                    iv[i] = sdot2(b2p[i], Wb, sdot2(b1p[i], Wa, 1 << 8)) >> 9;
-                    const int gx = sdot2(x1, Wb, sdot2(x0, Wa, 1 << 13)) >> 14;
-                    const int gy = sdot2(y1_, Wb, sdot2(y0_, Wa, 1 << 13)) >> 14;
+                    iv[i] = sdot2(b2p[i], Wb, sdot2k(b1p[i], Wa, c256)) >> 9;
+                    const int gx = sdot2(x1, Wb, sdot2k(x0, Wa, c8192)) >> 14;
+                    const int gy = sdot2(y1_, Wb, sdot2k(y0_, Wa, c8192)) >> 14;
                     ix[i] = gx & -(int)pv;
                     iy[i] = gy & -(int)pv;
-                    gmax = max(gmax, max(abs(ix[i]), abs(iy[i])));
+                    gmx = max(gmx, max(ix[i], iy[i]));
+                    gmn = min(gmn, min(ix[i], iy[i]));
                 }
                 IP[k][0] = pack_w(iv[0], iv[1]);
                 IP[k][1] = pack_w(iv[2], iv[3]);
@@ -2696,42 +2800,70 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 // materialize the unit's results here: no sinking of its arithmetic
                 // past later units (which would keep its patch bytes live)
                 asm volatile("" : "+v"(IP[k][0]), "+v"(IP[k][1]), "+v"(XP[k][0]), "+v"(XP[k][1]), "+v"(YP[k][0]),
-                             "+v"(YP[k][1]), "+v"(gmax));
+                             "+v"(YP[k][1]), "+v"(gmx), "+v"(gmn));
                 if (++q == QW) {
                     q = 0;
                     y++;
                 }
                 __builtin_amdgcn_sched_barrier(0);  // one unit at a time (register pressure)
             }
-            // A products of the window values, unit by unit (a second pass keeps
-            // the Scharr temporaries and the chain runs apart)
-            q = q0;
+            };
+            if (interior)
+                apass(std::true_type());
+            else
+                apass(std::false_type());
+            gmax = max(gmx, -gmn);
+            // A products of the window values, units in pairs (a second pass keeps
+            // the Scharr temporaries and the chain runs apart): v_mad_i32_i16 on the
+            // packed gradient halves, one v_max3 / v_min3 per two A12 prefixes
+            int q = q0;
             asm volatile("" : "+v"(q));
 #pragma unroll
-            for (int k = 0; k < UPT; k++) {
-                const bool sA = NOTAIL || q < nqA;
+            for (int k = 0; k < UPT; k += 2) {
+                unsigned xs[2][2], ys[2][2], xt[2][2], yt[2][2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    // SSE2 unit: pixel i feeds lane chain i; else the tail chain, row-major
+                    // (branch-free: the other chain's gradients are masked to zero)
+                    const unsigned ms = (NOTAIL || q < nqA) ? ~0u : 0u;
+#pragma unroll
+                    for (int hh = 0; hh < 2; hh++) {
+                        xs[u][hh] = XP[k + u][hh] & ms;
+                        ys[u][hh] = YP[k + u][hh] & ms;
+                        xt[u][hh] = XP[k + u][hh] & ~ms;
+                        yt[u][hh] = YP[k + u][hh] & ~ms;
+                    }
+                    if (++q == QW) q = 0;
+                }
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const int gx = (i & 1) ? hi16(XP[k][i >> 1]) : lo16(XP[k][i >> 1]);
-                    const int gy = (i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]);
-                    const int xx = __mul24(gx, gx), yy2 = __mul24(gy, gy), xy = __mul24(gx, gy);
-                    if (NOTAIL) {  // every unit is an SSE2 unit: pixel i feeds lane chain i
-                        T11[i] += xx;
-                        T22[i] += yy2;
-                        run_add(T12[i], M12[i], m12[i], xy);
-                        continue;
+                    const int hh = i >> 1;
+                    int ta, tb;
+                    if (i & 1) {
+                        T11[i] = mad16p<1, 1>(xs[1][hh], xs[1][hh], mad16p<1, 1>(xs[0][hh], xs[0][hh], T11[i]));
+                        T22[i] = mad16p<1, 1>(ys[1][hh], ys[1][hh], mad16p<1, 1>(ys[0][hh], ys[0][hh], T22[i]));
+                        ta = mad16p<1, 1>(xs[0][hh], ys[0][hh], T12[i]);
+                        tb = mad16p<1, 1>(xs[1][hh], ys[1][hh], ta);
+                    } else {
+                        T11[i] = mad16p<0, 0>(xs[1][hh], xs[1][hh], mad16p<0, 0>(xs[0][hh], xs[0][hh], T11[i]));
+                        T22[i] = mad16p<0, 0>(ys[1][hh], ys[1][hh], mad16p<0, 0>(ys[0][hh], ys[0][hh], T22[i]));
+                        ta = mad16p<0, 0>(xs[0][hh], ys[0][hh], T12[i]);
+                        tb = mad16p<0, 0>(xs[1][hh], ys[1][hh], ta);
                     }
-                    // SSE2 unit: pixel i feeds lane chain i; else the tail chain, row-major
-                    // (branch-free: the other chain gets a zero term)
-                    const int ms = -(int)sA;
-                    T11[i] += xx & ms;
-                    T22[i] += yy2 & ms;
-                    run_add(T12[i], M12[i], m12[i], xy & ms);
-                    T11[4] += xx & ~ms;
-                    T22[4] += yy2 & ~ms;
-                    run_add(T12[4], M12[4], m12[4], xy & ~ms);
+                    run2(T12[i], M12[i], m12[i], ta, tb);
                 }
-                if (++q == QW) q = 0;
+                if (!NOTAIL) {  // the tail chain: unit k's pixels 0-3, then unit k+1's
+#pragma unroll
+                    for (int u = 0; u < 2; u++)
+#pragma unroll
+                        for (int hh = 0; hh < 2; hh++) {
+                            T11[4] = mad16p<1, 1>(xt[u][hh], xt[u][hh], mad16p<0, 0>(xt[u][hh], xt[u][hh], T11[4]));
+                            T22[4] = mad16p<1, 1>(yt[u][hh], yt[u][hh], mad16p<0, 0>(yt[u][hh], yt[u][hh], T22[4]));
+                            const int ta = mad16p<0, 0>(xt[u][hh], yt[u][hh], T12[4]);
+                            const int tb = mad16p<1, 1>(xt[u][hh], yt[u][hh], ta);
+                            run2(T12[4], M12[4], m12[4], ta, tb);
+                        }
+                }
                 asm volatile("" : "+v"(T11[0]), "+v"(T11[1]), "+v"(T11[2]), "+v"(T11[3]), "+v"(T11[4]), "+v"(T22[0]),
                              "+v"(T22[1]), "+v"(T22[2]), "+v"(T22[3]), "+v"(T22[4]));
                 asm volatile("" : "+v"(T12[0]), "+v"(T12[1]), "+v"(T12[2]), "+v"(T12[3]), "+v"(T12[4]), "+v"(M12[0]),
@@ -2941,69 +3073,114 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             const unsigned s0 = bx_sel(sj, 0), s1 = bx_sel(sj, 1), s2 = bx_sel(sj, 2), s3 = bx_sel(sj, 3);
             int T1[5] = {0, 0, 0, 0, 0}, M1[5] = {0, 0, 0, 0, 0}, m1[5] = {0, 0, 0, 0, 0};
             int T2[5] = {0, 0, 0, 0, 0}, M2[5] = {0, 0, 0, 0, 0}, m2[5] = {0, 0, 0, 0, 0};
-            int dmax = 0;
-            unsigned zm;
-            asm volatile("v_mov_b32 %0, 0" : "=v"(zm));
+            int dmx = 0, dmn = 0;  // max / min d of the thread's pixels (when tracked)
+            const int c256 = opaque256();
             // every term d * g is an exact float unless |g| > 2^24 / 8160 (|d| <= 8160):
             // below that in the whole wave, the pass keeps no max |d|
             const bool dtrack = __ballot(gmax > kExact / 8160) != 0ull;
             auto bmain = [&](auto trk) {
-                // the unit's J row in dwords, stepped unit by unit (row-major units: +1, or
-                // to the next row's first quad); opaque start: no per-unit address hoisting
-                int q = q0, off = (oy + y0) * JRP4 + (ox >> 2) + q0;
-                asm volatile("" : "+v"(off), "+v"(q));
+                const uint8_t *jb = (const uint8_t *)(JR32 + oy * JRP4 + (ox >> 2));  // the iteration's base
+                // units in pairs (UPT is even): each chain takes its two terms by
+                // v_mad_i32_i16 (gradient half, product and sum in one) and one
+                // v_max3 / v_min3 of the two new prefixes
 #pragma unroll
-                for (int k = 0; k < UPT; k++) {
-                    const bool uv = u0 + k < U;
-                    int d[4];
-                    bx_diffs(JR32 + (uv ? off : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, zm);
-                    int t1[4], t2[4];
+                for (int k = 0; k < UPT; k += 2) {
+                    int d[2][4], ms[2];
+                    asm volatile("" : "+v"(UB[k >> 1]));  // opaque per iteration: its halves stay packed
 #pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const int gx = ((i & 1) ? hi16(XP[k][i >> 1]) : lo16(XP[k][i >> 1]));
-                        const int gy = ((i & 1) ? hi16(YP[k][i >> 1]) : lo16(YP[k][i >> 1]));
-                        t1[i] = __mul24(d[i], gx);
-                        t2[i] = __mul24(d[i], gy);
-                        if constexpr (decltype(trk)::value) dmax = max(dmax, abs(d[i]));
+                    for (int u = 0; u < 2; u++) {
+                        const unsigned o = u ? UB[k >> 1] >> 16 : UB[k >> 1] & 0xffffu;
+                        bx_diffs((const uint32_t *)(jb + o), JRP4, W0, W1, s0, s1, s2, s3, IP[k + u], d[u], c256);
+                        ms[u] = -(int)((sseB >> (k + u)) & 1u);  // SSE2 unit -> lane chains 0-3, else the tail chain
+                    }
+                    if constexpr (decltype(trk)::value) {
+#pragma unroll
+                        for (int u = 0; u < 2; u++) {
+                            dmx = max(dmx, max(d[u][0], d[u][1]));
+                            dmx = max(dmx, max(d[u][2], d[u][3]));
+                            dmn = min(dmn, min(d[u][0], d[u][1]));
+                            dmn = min(dmn, min(d[u][2], d[u][3]));
+                        }
                     }
                     if (NOTAIL) {  // every unit feeds lane chains 0-3
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
-                            run_add(T1[i], M1[i], m1[i], t1[i]);
-                            run_add(T2[i], M2[i], m2[i], t2[i]);
+                            const int h = i >> 1;
+                            int ta, tb;
+                            if (i & 1) {
+                                ta = mad16<1>(d[0][i], XP[k][h], T1[i]);
+                                tb = mad16<1>(d[1][i], XP[k + 1][h], ta);
+                            } else {
+                                ta = mad16<0>(d[0][i], XP[k][h], T1[i]);
+                                tb = mad16<0>(d[1][i], XP[k + 1][h], ta);
+                            }
+                            run2(T1[i], M1[i], m1[i], ta, tb);
+                            if (i & 1) {
+                                ta = mad16<1>(d[0][i], YP[k][h], T2[i]);
+                                tb = mad16<1>(d[1][i], YP[k + 1][h], ta);
+                            } else {
+                                ta = mad16<0>(d[0][i], YP[k][h], T2[i]);
+                                tb = mad16<0>(d[1][i], YP[k + 1][h], ta);
+                            }
+                            run2(T2[i], M2[i], m2[i], ta, tb);
                         }
                     } else {
-                        // SSE2 unit -> lane chains 0-3, else the tail chain (branch-free)
-                        const int ms = -(int)(q < nqB);
+                        // branch-free: the other chain gets zero terms (masked d); the tail
+                        // chain first (unit k's pixels 0-3, then unit k+1's, in order)
 #pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            run_add(T1[i], M1[i], m1[i], t1[i] & ms);
-                            run_add(T2[i], M2[i], m2[i], t2[i] & ms);
+                        for (int u = 0; u < 2; u++) {
+                            const unsigned *xp = XP[k + u], *yp = YP[k + u];
+                            const int nm = ~ms[u];
+                            int a0 = mad16<0>(d[u][0] & nm, xp[0], T1[4]);
+                            int a1 = mad16<1>(d[u][1] & nm, xp[0], a0);
+                            run2(T1[4], M1[4], m1[4], a0, a1);
+                            a0 = mad16<0>(d[u][2] & nm, xp[1], T1[4]);
+                            a1 = mad16<1>(d[u][3] & nm, xp[1], a0);
+                            run2(T1[4], M1[4], m1[4], a0, a1);
+                            a0 = mad16<0>(d[u][0] & nm, yp[0], T2[4]);
+                            a1 = mad16<1>(d[u][1] & nm, yp[0], a0);
+                            run2(T2[4], M2[4], m2[4], a0, a1);
+                            a0 = mad16<0>(d[u][2] & nm, yp[1], T2[4]);
+                            a1 = mad16<1>(d[u][3] & nm, yp[1], a0);
+                            run2(T2[4], M2[4], m2[4], a0, a1);
                         }
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
-                            run_add(T1[4], M1[4], m1[4], t1[i] & ~ms);
-                            run_add(T2[4], M2[4], m2[4], t2[i] & ~ms);
+                            const int h = i >> 1;
+                            const int e0 = d[0][i] & ms[0], e1 = d[1][i] & ms[1];
+                            int ta, tb;
+                            if (i & 1) {
+                                ta = mad16<1>(e0, XP[k][h], T1[i]);
+                                tb = mad16<1>(e1, XP[k + 1][h], ta);
+                            } else {
+                                ta = mad16<0>(e0, XP[k][h], T1[i]);
+                                tb = mad16<0>(e1, XP[k + 1][h], ta);
+                            }
+                            run2(T1[i], M1[i], m1[i], ta, tb);
+                            if (i & 1) {
+                                ta = mad16<1>(e0, YP[k][h], T2[i]);
+                                tb = mad16<1>(e1, YP[k + 1][h], ta);
+                            } else {
+                                ta = mad16<0>(e0, YP[k][h], T2[i]);
+                                tb = mad16<0>(e1, YP[k + 1][h], ta);
+                            }
+                            run2(T2[i], M2[i], m2[i], ta, tb);
                         }
                     }
-                    {
-                        const bool wrap = q == QW - 1;
-                        off += wrap ? JRP4 - QW + 1 : 1;
-                        q = wrap ? 0 : q + 1;
-                    }
-                    // materialize the runs per unit (no sinking across units)
+                    // materialize the runs per unit pair (no sinking across pairs)
                     asm volatile("" : "+v"(T1[0]), "+v"(T1[1]), "+v"(T1[2]), "+v"(T1[3]), "+v"(T1[4]), "+v"(M1[0]),
                                  "+v"(M1[1]), "+v"(M1[2]), "+v"(M1[3]), "+v"(M1[4]));
                     asm volatile("" : "+v"(m1[0]), "+v"(m1[1]), "+v"(m1[2]), "+v"(m1[3]), "+v"(m1[4]), "+v"(T2[0]),
                                  "+v"(T2[1]), "+v"(T2[2]), "+v"(T2[3]), "+v"(T2[4]));
                     asm volatile("" : "+v"(M2[0]), "+v"(M2[1]), "+v"(M2[2]), "+v"(M2[3]), "+v"(M2[4]), "+v"(m2[0]),
-                                 "+v"(m2[1]), "+v"(m2[2]), "+v"(m2[3]), "+v"(m2[4]), "+v"(dmax));
+                                 "+v"(m2[1]), "+v"(m2[2]), "+v"(m2[3]), "+v"(m2[4]), "+v"(dmx), "+v"(dmn));
                 }
             };
             if (dtrack)
                 bmain(std::true_type());
             else
                 bmain(std::false_type());
+            const int dmax = max(dmx, -dmn);
             // masked pixels carry zero gradients but any d: only real terms count
             const bool bad = (long long)dmax * gmax > (long long)kExact;
             int T[10], M[10], m[10];
@@ -3053,7 +3230,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 };
                 // one unit's b products into the tile's chain regions
                 auto tile_unit = [&](int yk, int qk, bool uv, const unsigned (&ip)[2], const unsigned (&xp)[2],
-                                     const unsigned (&yp)[2], float *buf, int S, int P, int sa, int ta, unsigned zf) {
+                                     const unsigned (&yp)[2], float *buf, int S, int P, int sa, int ta, int zf) {
                     if (!uv) return;
                     int d[4];
                     bx_diffs(JR32 + (oy + yk) * JRP4 + (ox >> 2) + qk, JRP4, W0, W1, s0, s1, s2, s3, ip, d, zf);
@@ -3083,8 +3260,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     return first ? r[0] : r[1];
                 };
                 auto write_tile = [&](int g, float *buf) {
-                    unsigned zf;  // opaque zero per tile: no diff constants hoisted out of the tile loop
-                    asm volatile("v_mov_b32 %0, 0" : "=v"(zf));
+                    const int zf = opaque256();  // per tile: no diff constants hoisted out of the tile loop
                     int sa, ta, nsse, ntail;
                     if (split) {
                         if ((ftid >> 6) != (g >> 1)) return;
@@ -3237,7 +3413,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 for (int k = 0; k < UPT; k++) {
                     const bool uv = u0 + k < U;
                     int d[4];
-                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, 0u);
+                    bx_diffs(JR32 + (oy + (uv ? y : 0)) * JRP4 + (ox >> 2) + (uv ? q : 0), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, 256);
 #pragma unroll
                     for (int i = 0; i < 4; i++)
                         if (uv && 4 * q + i < w) e += (unsigned)abs(d[i]);
@@ -3267,7 +3443,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     for (int k = 0; k < UPT; k++) {
                         if (u0 + k < U && yk >= r0 && yk < r0 + tr) {
                             int d[4];
-                            bx_diffs(JR32 + (oy + (yk)) * JRP4 + (ox >> 2) + (qk), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, 0u);
+                            bx_diffs(JR32 + (oy + (yk)) * JRP4 + (ox >> 2) + (qk), JRP4, W0, W1, s0, s1, s2, s3, IP[k], d, 256);
 #pragma unroll
                             for (int i = 0; i < 4; i++)
                                 if (4 * qk + i < w) PL[(yk - r0) * w + 4 * qk + i] = (float)abs(d[i]);

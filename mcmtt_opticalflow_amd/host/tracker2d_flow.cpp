@@ -172,6 +172,7 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
     }
     next_rb_ = 0;
     last_rb_ = -1;
+    trk_rb_ = -1;
     return psn_lk_set_stream(lk_, cs);
 }
 
@@ -468,7 +469,11 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
     }
     const int si = stage_;  // this pass's staging set
     stage_ ^= 1;
-    const int rb = next_rb_;  // this pass's result block
+    // this pass's result block: neither the previous pass's (in flight) nor the
+    // one the current trackers' set 0 lives in (their next forward call reads it
+    // when a frame fails)
+    int rb = next_rb_;
+    while (rb == last_rb_ || rb == trk_rb_) rb = (rb + 1) % DeviceBuffers::kResBlocks;
     next_rb_ = (rb + 1) % DeviceBuffers::kResBlocks;
     last_rb_ = rb;
     for (PassCam &p : pc) {
@@ -644,10 +649,23 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
 // detection k (count = its set-0 count, 0 for a detection that is no tracker)
 // with the window of its box; the outputs land at the same index in the forward
 // result block. pc: the pass of frame t+1 (its frames adopted).
-int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb) {
+int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb, bool host_fallback) {
     for (PassCam &p : pc) p.fwd_rb = -1;
-    if (src_rb < 0 || !chain_info_[src_rb].valid || chain_info_[src_rb].K == 0 || !dev_ || !dev_->d_res[src_rb])
-        return PSN_LK_OK;
+    if (src_rb < 0 || !chain_info_[src_rb].valid || chain_info_[src_rb].K == 0 || !dev_ || !dev_->d_res[src_rb]) {
+        if (!host_fallback) return PSN_LK_OK;
+        // the chain results are gone (the chain buffers grew since): the trackers'
+        // set 0 from the host, one call per tracker; a window the LK cannot run is
+        // a placeholder (the frame fails at its completion, as from the device)
+        for (PassCam &p : pc) {
+            Cam &cam = cams_[p.cam];
+            cam.fwd.clear();
+            ForwardJobs(p.cam, cam.trackers, cam.fstatus, cam.fwd);
+            for (Job &jb : cam.fwd)
+                if (forward_window_error(jb.win_w, jb.win_h)) jb.win_w = jb.win_h = 3;
+            p.fwd = &cam.fwd;
+        }
+        return PassLaunchForward(pc);
+    }
     const ChainInfo &ci = chain_info_[src_rb];
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, K = ci.K;
     int rc = EnsureForward(K * S * cap, K);
@@ -1208,6 +1226,13 @@ void Tracker2DFlow::ForwardDone(const std::vector<Tracker2D *> &trackers, std::v
             const size_t len = std::min((size_t)kT2dInterval, std::min(tr->boxes.size(), det.boxes.size()));
             size_t tb = (size_t)tr->duration;  // duration = #boxes - 1
             for (size_t b = 0; b < len; b++, tb--) {
+                // after a failed frame a tracker's duration (frame based, :1085) runs
+                // past its boxes: the reference reads outside the vector (undefined);
+                // here the pair cannot match (as oracle/tracker2d_oracle.py)
+                if (tb >= tr->boxes.size()) {
+                    boxCost = std::numeric_limits<double>::infinity();
+                    break;
+                }
                 const Rect &db = det.boxes[b], &trb = tr->boxes[tb];
                 if (!db.overlap(trb) || kBoxMaxDistance < db.distance(trb) ||
                     kMinOverlapRatio > db.overlappedArea(trb) / std::min(db.area(), trb.area()) ||
@@ -1395,12 +1420,16 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
     // then frame t's features and chains
     bool any = false;
     for (const Cam &cam : cams_) any = any || !cam.active.empty();
-    rc = any ? LaunchForwardFromChains(run_pass_, last_rb_) : PSN_LK_OK;
+    const int saved_next_rb = next_rb_, saved_last_rb = last_rb_, saved_stage = stage_;
+    rc = any ? LaunchForwardFromChains(run_pass_, trk_rb_, true) : PSN_LK_OK;
     if (!rc) rc = PassLaunchChains(run_pass_, gridfast, seed);
-    if (rc) {
+    if (rc) {  // nothing of the frame stays in flight; the result blocks as before
         SyncChains();
         (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
         run_pass_.clear();
+        next_rb_ = saved_next_rb;
+        last_rb_ = saved_last_rb;
+        stage_ = saved_stage;
     }
     return rc;
 }
@@ -1456,7 +1485,7 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
             pre.clear();
             return;
         }
-        prc = LaunchForwardFromChains(pre, cur_rb);
+        prc = LaunchForwardFromChains(pre, cur_rb, false);
         if (!prc) prc = PassLaunchChains(pre, nextGridfast, nextSeed);
         if (prc) abandon_next();
     };
@@ -1498,6 +1527,7 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
         cam.trackers.assign(cam.active.begin(), cam.active.end());
         cam.fwd_k0 = cur_k0[c];
     }
+    trk_rb_ = cur_rb;  // the trackers' set 0
     stamp(3);  // matched, trackers updated
     host_calls_++;
     frame_completed_ = true;

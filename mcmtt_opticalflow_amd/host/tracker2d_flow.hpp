@@ -179,7 +179,7 @@ class Tracker2DFlow {
     int PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);  // chains, then forward
     int PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);
     int PassLaunchForward(std::vector<PassCam> &pc);
-    int LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb);
+    int LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb, bool host_fallback);
     static int forward_window_error(int w, int h);
     // what a chain pass leaves for the next frame's forward launch
     struct ChainInfo {
@@ -190,6 +190,7 @@ class Tracker2DFlow {
     };
     ChainInfo chain_info_[kT2dResBlocks];
     int next_rb_ = 0, last_rb_ = -1;
+    int trk_rb_ = -1;  // the result block holding the current trackers' set 0 (their next forward call)
     void *ev_set0_[3] = {nullptr, nullptr, nullptr};   // hipEvent_t: a block's set 0 is final (chain stream)
     void *ev_fread_[3] = {nullptr, nullptr, nullptr};  // hipEvent_t: the forward launch reading a block is done
     bool fread_rec_[3] = {false, false, false};

@@ -251,6 +251,9 @@ def forward_tracking(ring, trackers, dets):
             length = min(INTERVAL, min(len(tr.boxes), len(det.boxes)))
             tb = tr.duration
             for b in range(length):
+                if not 0 <= tb < len(tr.boxes):  # past a failed frame: undefined in the reference (:948-952)
+                    box_cost = math.inf
+                    break
                 db, tbx = det.boxes[b], tr.boxes[tb]
                 if (not db.overlap(tbx) or 1.0 < db.distance(tbx)
                         or 0.3 > db.overlapped_area(tbx) / min(db.area(), tbx.area())

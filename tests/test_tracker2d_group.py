@@ -194,3 +194,43 @@ def test_group_window_errors():
         few = t2d.make_detection((10, 10, 2, 30), np.float32([[11, 12], [11, 20]]))
         (dets, res), = g.run(2, [[few]])
         assert dets[0].valid == 0 and res["objects"] == []
+
+
+def test_group_failed_frame_after_regrow_matches_oracle(oracle_mod):
+    """A frame that grows the chain buffers and then fails (a 2-px-wide detection
+    with >= 4 features, CV_Assert(winSize > 2)) leaves the trackers of the frame
+    before it; the next frame's forward calls then come from their host set 0
+    (the device chain results were reallocated) -- bit for bit the reference,
+    whose failed Run has pushed the frame and kept its trackers."""
+    W, H, T = 640, 480, 4
+    sc = synth.make_scene(77, W, H, 120, nboxes=3, box_w=32, box_h=80, max_speed=3.0)
+    ref = ORC.CameraTracker(cam_id=5)
+    rng = np.random.default_rng(9)
+    grays = [sc.frame(t) for t in range(T)]
+    per_frame = [_camera_dets(sc, t, rng) for t in range(T)]
+    boxes, extra, feats = per_frame[1]
+    for i in range(20):  # frame 1: enough detections to grow the chain buffers (16)
+        x, y = float(rng.integers(10, W - 50)), float(rng.integers(10, H - 100))
+        boxes.append((x, y, 32.0, 80.0))
+        extra.append(((x + 8, y, 16.0, 10.0), (x, y, 0.0), 1700.0))
+        feats.append(np.stack([rng.uniform(x + 2, x + 30, 30), rng.uniform(y + 2, y + 78, 30)], 1).astype(np.float32))
+    boxes.append((300.0, 200.0, 2.0, 30.0))
+    extra.append(((300.0, 200.0, 2.0, 4.0), (0.0, 0.0, 0.0), 1700.0))
+    feats.append(np.float32([[300.5, 202], [301, 210], [300.2, 215], [300.7, 225]]))
+    frames = [[t2d.make_detection(b, f, head=e[0], location=e[1], height=e[2])
+               for b, e, f in zip(*per_frame[t])] for t in range(T)]
+    with t2d.Group(W, H, [5]) as g:
+        for t in range(T):
+            g.push_frame(0, grays[t])
+            boxes, extra, feats = per_frame[t]
+            args = (grays[t], [ORC.Rect(*b) for b in boxes], feats, t, [(ORC.Rect(*e[0]), e[1], e[2]) for e in extra])
+            if t == 1:
+                with pytest.raises(t2d.T2dError):
+                    g.run(t, [frames[t]])
+                with pytest.raises(Exception):
+                    ref.run(*args)
+                continue
+            (g_out, g_res), = g.run(t, [frames[t]])
+            objs, _, r_res = ref.run(*args)
+            _check_result(g_res, r_res, f"frame {t}")
+            assert len([d for d in g_out if d.valid]) == len(objs), f"frame {t}"
