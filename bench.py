@@ -72,6 +72,11 @@ OPS_PER_SAMPLE = 8  # ~8 integer ops per window sample per itera
 DEFAULT_PROFILE = os.path.join(ROOT, "profiles", "r03_tracker_profile.json")
 
 
+def progress(msg):
+    """A progress line on stderr (long legs stay visibly alive; stdout keeps the one JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def level_sizes(w, h, nlev):
     out = []
     for _ in range(nlev):
@@ -496,15 +501,18 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
     scenes = [synth.make_scene(c, W, H, args.points, nboxes=args.boxes) for c in range(C)]
     grays = [[oracle.bgr2gray(synth.to_bgr(sc.frame(t))) for t in range(args.period)] for sc in scenes]
 
-    def leg(threads, shared, budget):
+    def leg(threads, shared, budget, ncams=C):
         T2.NTHREADS, T2.SHARED_PYRAMIDS = threads, shared
-        cams = [T2.CameraTracker(c) for c in range(C)]
+        cams = [T2.CameraTracker(c) for c in range(ncams)]
         n, t0 = 0, None
+        progress(f"cpu baseline leg: {threads} threads, shared pyramids {shared}, {ncams} cameras, {budget:.0f} s")
         for t in range(n_frames_cap + 2):
             if t == 2:  # the ring holds frames: the steady state starts
                 t0 = time.perf_counter()
             f = ping_pong(t, args.period)
-            for c, sc in enumerate(scenes):
+            if t < 4 or t % 10 == 0:
+                progress(f"  frame {t}")
+            for c, sc in enumerate(scenes[:ncams]):
                 boxes = detection_boxes(sc, f)
                 pts = sc.points_at(f)
                 feats = [pts[sc.pt_box == k] for k in range(args.boxes)]
@@ -520,7 +528,7 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
 
     share, allc = cpu_share_threads(), len(os.sched_getaffinity(0))
     v, n, dt = leg(share, False, args.cpu_budget)
-    v1, n1, dt1 = leg(1, False, args.cpu_budget / 2)
+    v1, n1, dt1 = leg(1, False, args.cpu_budget / 2, ncams=1)  # one camera: bounded warm-up
     va, na, dta = leg(allc, False, args.cpu_budget / 2)
     vs, ns, dts = leg(share, True, args.cpu_budget / 2)
     return {"value": round(v, 4), "unit": "frames/s", "cores": share, "kind": "port",
@@ -529,7 +537,7 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
                       "Munkres matching) through oracle/tracker2d_oracle.py + oracle/lk_oracle.c, OpenMP over "
                       "points and over the rows of every pyramid/border/Scharr pass, reference call schedule "
                       "(both pyramids rebuilt in every calcOpticalFlowPyrLK)",
-            "single_thread": round(v1, 4), "single_thread_sample": f"{n1} camera-frames, {dt1:.1f} s",
+            "single_thread": round(v1, 4), "single_thread_sample": f"{n1} camera-frames (camera 0), {dt1:.1f} s",
             "all_cores": round(va, 4), "all_cores_threads": allc, "all_cores_sample": f"{na} camera-frames, {dta:.1f} s",
             "shared_pyramid": round(vs, 4), "shared_pyramid_sample": f"{ns} camera-frames, {dts:.1f} s, {share} threads",
             "cores_note": "cores = the host cores this GPU's job is allotted (the box sets OMP_NUM_THREADS to its "
@@ -659,7 +667,9 @@ def tracker_main(args):
     world, rank, local_rank = dist_env()
     init_control_plane(world)
     profile = load_profile(args.profile)
+    progress(f"rank {rank}: tracker run, {args.warmup} warm-up + {args.steps} timed frames")
     r = tracker_run(args, world, rank, local_rank)
+    progress(f"rank {rank}: tracker run done ({r['elapsed']:.3f} s timed)")
     C = r["cams_per_rank"]
     out = None
     if rank == 0:
@@ -672,8 +682,10 @@ def tracker_main(args):
             out["speedup_vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
             out["speedup_vs_cpu_all_cores"] = round(out["value"] / out["cpu_baseline"]["all_cores"], 1)
     if world == 1 and not args.no_legs and not args.total_cameras and not args.verify:
+        progress("legs")
         out["legs"] = tracker_legs(args, profile)
     if world == 1 and not args.no_secondary:
+        progress("secondary (kernel mode)")
         out["secondary"] = kernel_secondary(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
