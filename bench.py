@@ -116,6 +116,27 @@ def host_info():
     return info
 
 
+def cpu_quota_cores():
+    """The CPU quota of this process's cgroup in cores (cgroup v2 cpu.max or v1
+    cfs quota), else the affinity set: more OpenMP threads than that only
+    time-slice (spinning barriers make such a leg crawl)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, min(n, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, min(n, q // p))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_share_threads():
     """The host cores allotted to this GPU's job: the affinity set, capped by
     OMP_NUM_THREADS when the box sets it (16 per GPU on the GPU box)."""
@@ -526,7 +547,9 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
         T2.NTHREADS, T2.SHARED_PYRAMIDS = 0, False
         return n / dt, n, dt
 
-    share, allc = cpu_share_threads(), len(os.sched_getaffinity(0))
+    # all cores: every core this process may run on at once (the affinity set,
+    # capped by the cgroup's CPU quota), the thread count set explicitly
+    share, allc = cpu_share_threads(), cpu_quota_cores()
     v, n, dt = leg(share, False, args.cpu_budget)
     v1, n1, dt1 = leg(1, False, args.cpu_budget / 2, ncams=1)  # one camera: bounded warm-up
     va, na, dta = leg(allc, False, args.cpu_budget / 2)
@@ -541,7 +564,8 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
             "all_cores": round(va, 4), "all_cores_threads": allc, "all_cores_sample": f"{na} camera-frames, {dta:.1f} s",
             "shared_pyramid": round(vs, 4), "shared_pyramid_sample": f"{ns} camera-frames, {dts:.1f} s, {share} threads",
             "cores_note": "cores = the host cores this GPU's job is allotted (the box sets OMP_NUM_THREADS to its "
-                          "per-GPU CPU share); all_cores = every core of the affinity set (the whole machine)",
+                          "per-GPU CPU share); all_cores = every core this process may run on at once (the affinity "
+                          f"set of {len(os.sched_getaffinity(0))} CPUs capped by the cgroup CPU quota)",
             **host_info()}
 
 

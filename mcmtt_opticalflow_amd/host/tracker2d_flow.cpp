@@ -3,6 +3,7 @@
 #include "tracker2d_flow.hpp"
 
 #include <hip/hip_runtime_api.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
@@ -826,15 +827,22 @@ int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
     return rc;
 }
 
-// Spin on the completion events (a blocking stream sync sleeps and wakes
-// ~0.1 ms late; the next frame's work is enqueued right after this returns).
+// Poll the completion events (a blocking stream sync sleeps and wakes ~0.1 ms
+// late; the next frame's work is enqueued right after this returns). Past a
+// short spin every poll yields the core: ranks sharing a GPU's CPU allotment
+// keep their cores for the host work of their own frames.
 int Tracker2DFlow::PassSync() {
     for (int i = 0; i < 2; i++) {
         bool &w = i ? wait_fwd_ : wait_chain_;
         if (!w) continue;
         hipEvent_t e = (hipEvent_t)(i ? ev_fwd_ : ev_chain_);
         hipError_t q;
-        while ((q = hipEventQuery(e)) == hipErrorNotReady) __builtin_ia32_pause();
+        for (unsigned n = 0; (q = hipEventQuery(e)) == hipErrorNotReady; n++) {
+            if (n < 256)
+                __builtin_ia32_pause();
+            else
+                sched_yield();
+        }
         w = false;
         if (q != hipSuccess) {
             err_ = std::string(i ? "forward" : "chain") + " sync: " + hipGetErrorString(q);
