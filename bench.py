@@ -597,7 +597,7 @@ def tracker_roofline(args, r, C, profile):
     avg_ms = tot / n
     launch_b = C * lk_b
     ach = launch_b / (avg_ms * 1e-3) / 1e9
-    out = {"kernel": name, "bound": "valu",
+    out = {"kernel": name, "bound": "latency",
            "achieved": round(ach, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 6),
            "traffic": None, "bytes_per_launch": launch_b, "avg_launch_us": round(1e3 * avg_ms, 2),
            "launches_timed": n,
@@ -629,10 +629,33 @@ def tracker_roofline(args, r, C, profile):
                 v["useful_lane_frac"] = round(useful / (lk_vi * 64), 4)
                 v["useful_note"] = (f"SURVEY 8(d) window samples x {OPS_PER_SAMPLE} ops per frame-set / "
                                     "(SQ_INSTS_VALU of every LK launch per frame-set x 64 lanes)")
-            for key in ("SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+            # the whole frame-set: every profiled kernel's VALU instructions x its timed
+            # launches per frame-set, over the step time
+            ms_step = r["elapsed"] / r["steps"] * 1e3
+            frame_vi = sum(kv.get("SQ_INSTS_VALU", 0) * per.get(k, (0, 0))[0]
+                           for k, kv in profile.get("kernels", {}).items()) / max(r["measure_steps"], 1)
+            if frame_vi:
+                v["frame_set_frac"] = round(frame_vi / (VALU_PEAK_WAVE_INSTR * ms_step * 1e-3), 4)
+                v["frame_set_note"] = "SQ_INSTS_VALU of every LK launch of a frame-set / issue capacity over ms_per_step"
+            for key in ("SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
+                        "SQ_WAIT_INST_ANY"):
                 if key in pk:
                     v[key + "_per_launch"] = int(pk[key])
+            if pk.get("SQ_WAVE_CYCLES") and pk.get("SQ_WAIT_INST_ANY"):
+                v["wait_frac"] = round(pk["SQ_WAIT_INST_ANY"] / pk["SQ_WAVE_CYCLES"], 4)
             out["valu"] = v
+            # what bounds it, from the counters: VALU issue when either issue fraction
+            # nears the peak; the HBM roofline when the PMC traffic rate does; else the
+            # workgroups' dependency latency (serial ordered chains, barriers) at the
+            # occupancy the registers and LDS allow
+            hbm_rate = (out["traffic"] or 0) / (avg_ms * 1e-3) / 1e9
+            if max(v["frac"], v.get("frame_set_frac", 0)) >= 0.6:
+                out["bound"] = "valu"
+            elif hbm_rate >= 0.6 * HBM_PEAK_GBPS:
+                out["bound"] = "hbm"
+            out["bound_note"] = (f"VALU issue {v['frac']:.0%} of peak over the launch, "
+                                 f"{v.get('frame_set_frac', 0):.0%} over the frame-set; PMC HBM "
+                                 f"{hbm_rate:.0f} GB/s; below 60 % of either peak the kernel is latency-bound")
     return out
 
 

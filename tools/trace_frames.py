@@ -15,7 +15,7 @@ def main():
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                  r["Kernel_Name"].split("(")[0].replace("void ", "").replace("psn::", "")
                  .replace("(anonymous namespace)::", "")[:24], r["Queue_Id"]) for r in rows)
-    fw = [i for i, e in enumerate(ev) if "bx<10>" in e[2]]
+    fw = [i for i, e in enumerate(ev) if "bx<10" in e[2]]
     i0, i1 = fw[first], fw[first + nsets]
     t0 = ev[i0][0]
     for s, e, n, q in ev[i0 - 12:i1]:
