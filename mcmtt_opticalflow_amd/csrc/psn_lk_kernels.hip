@@ -1114,6 +1114,15 @@ __device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int g
     }
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// A workgroup barrier that leaves vector-memory loads in flight (__syncthreads'
+// fence would wait for them): every thread's LDS data it orders was already
+// waited for (dma_wait / lgkmcnt) by the thread that wrote it. The empty asm
+// keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void barrier_inflight() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 
 // Element walk of a region with m elements per row: this thread's first
@@ -2693,9 +2702,11 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
 
         __syncthreads();  // the previous level is done with LDS
         dma_patch<NT>(UN, I, ipy - 1, ipx - 1, w + 3, h + 3, PM, Q.dv_bxpm);
-        dma_patch<NT>(JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
         dma_wait();
-        __syncthreads();
+        // the J region moves while the A phase reads the I patch: waited for
+        // before the A publish barrier, which makes it visible to every wave
+        dma_patch<NT>(JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
+        barrier_inflight();  // the I patch (waited above) for every wave; J still moving
         BX_MARK(0);  // level setup + staging
 
         // ---- A phase: Scharr + bilinear window values of the thread's units from
@@ -2882,6 +2893,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
             bx_publish<15>(T, rec, NOTAIL || tA == 0);
+            dma_wait();  // this thread's J region loads (the barrier: every thread's)
             __syncthreads();
             bx_check<15>(T, M, m, false, rec, NOTAIL || tA == 0);
             __syncthreads();
