@@ -118,11 +118,13 @@ def load(path: str | None = None):
     """The product library (mcmtt_opticalflow_amd/lib/libpsn_lk.so). Only the
     profiling tools pass path (STAMPS_LIB_PATH), before anything else loads it."""
     global _lib, _lib_path
-    path = path or LIB_PATH
     if _lib is not None:
-        if path != _lib_path:
+        # load() without a path returns whatever is loaded (a tool's diagnostic
+        # build, loaded first); an explicit different path is an error
+        if path is not None and os.path.abspath(path) != os.path.abspath(_lib_path):
             raise RuntimeError(f"{_lib_path} is loaded already (asked for {path})")
         return _lib
+    path = path or LIB_PATH
     if not os.path.exists(path):
         raise ImportError(f"{path} is missing: run __graft_entry__.build() (no CPU fallback exists)")
     L = ctypes.CDLL(path)
