@@ -285,6 +285,11 @@ int psn_t2d_group_complete_next(psn_t2d_group *g, psn_t2d_detection *const *dets
  * work done, unpacked, matched and updated, next forward calls enqueued), and
  * out6[5] = the number of completes */
 int psn_t2d_group_debug_host_times(psn_t2d_group *g, double *out6);
+/* diagnostic: host microseconds accumulated since the last call by the parts of
+ * the completes' matching phase, over all cameras: overlap flags (:824-835),
+ * forward matching costs + majority gate (:906-1022), assignment (:1038-1060),
+ * tracker update + results (:1062-1164) */
+int psn_t2d_group_debug_host_match_times(psn_t2d_group *g, double *out4);
 /* camera c's active trackers (m_queueActiveTracker2D) after the last complete */
 int psn_t2d_group_trackers(psn_t2d_group *g, int cam, psn_t2d_tracker *out, int cap, int *n);
 

@@ -2530,6 +2530,19 @@ __device__ __forceinline__ float add16m(float acc, const bxf4 &a, const bxf4 &b,
     t = t + d.x; t = t + d.y; t = t + d.z; t = t + d.w;
     return on ? t : acc;
 }
+// Wave priority of the latency-critical sections of lk_kernel_bx (from the end of
+// a main pass to the start of the next: publish, check, eval, results, solve,
+// iteration head; the A publish / eval) over the throughput sections (A window,
+// main passes) of the other workgroups on the SIMD; the ordered chains run at 3.
+#ifndef PSN_BX_PRIO
+#define PSN_BX_PRIO 1
+#endif
+__device__ __forceinline__ void bx_prio_hi() { __builtin_amdgcn_s_setprio(PSN_BX_PRIO); }
+__device__ __forceinline__ void bx_prio_lo() { __builtin_amdgcn_s_setprio(0); }
+// UNIFORM (no-tail builds): every chain lane has nbmax blocks, so no block is
+// masked and the adds carry no select on the dependent chain; an odd last
+// block is summed after the loop.
+template <bool UNIFORM>
 __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax, float acc) {
     unsigned ad = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float *)p;
     const int nb = (len + 15) >> 4;
@@ -2540,17 +2553,34 @@ __device__ __forceinline__ float chain_sum_pl(const float *p, int len, int nbmax
     __builtin_amdgcn_s_setprio(3);
     bxf4 a0, a1, a2, a3, c0, c1, c2, c3;
     BX_LD(a0, a1, a2, a3, ad, 0, 16, 32, 48);
-    for (int b = 0; b < nbmax; b += 2) {
-        BX_LD(c0, c1, c2, c3, ad, 64, 80, 96, 112);
-        BX_WAIT4(a0, a1, a2, a3);
-        acc = add16m(acc, a0, a1, a2, a3, b < nb);
-        BX_LD(a0, a1, a2, a3, ad, 128, 144, 160, 176);
-        BX_WAIT4(c0, c1, c2, c3);
-        acc = add16m(acc, c0, c1, c2, c3, b + 1 < nb);
-        ad += 128u;
+    if constexpr (UNIFORM) {
+        int b = 0;
+        for (; b + 1 < nbmax; b += 2) {
+            BX_LD(c0, c1, c2, c3, ad, 64, 80, 96, 112);
+            BX_WAIT4(a0, a1, a2, a3);
+            acc = add16m(acc, a0, a1, a2, a3, true);
+            BX_LD(a0, a1, a2, a3, ad, 128, 144, 160, 176);
+            BX_WAIT4(c0, c1, c2, c3);
+            acc = add16m(acc, c0, c1, c2, c3, true);
+            ad += 128u;
+        }
+        if (b < nbmax) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : : "memory");
+            acc = add16m(acc, a0, a1, a2, a3, true);
+        }
+    } else {
+        for (int b = 0; b < nbmax; b += 2) {
+            BX_LD(c0, c1, c2, c3, ad, 64, 80, 96, 112);
+            BX_WAIT4(a0, a1, a2, a3);
+            acc = add16m(acc, a0, a1, a2, a3, b < nb);
+            BX_LD(a0, a1, a2, a3, ad, 128, 144, 160, 176);
+            BX_WAIT4(c0, c1, c2, c3);
+            acc = add16m(acc, c0, c1, c2, c3, b + 1 < nb);
+            ad += 128u;
+        }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : : "memory");
-    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(PSN_BX_PRIO);
     return acc;
 }
 
@@ -2708,6 +2738,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
         dma_patch<NT>(JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
         barrier_inflight();  // the I patch (waited above) for every wave; J still moving
         BX_MARK(0);  // level setup + staging
+        bx_prio_lo();
 
         // ---- A phase: Scharr + bilinear window values of the thread's units from
         // the I patch bytes; the 15 A chains (sum x class) as runs ----
@@ -2890,6 +2921,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 T[10 + c] = T22[c], M[10 + c] = T22[c], m[10 + c] = 0;
             }
             BX_MARK(1);  // A window values + runs
+            bx_prio_hi();
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
             bx_publish<15>(T, rec, NOTAIL || tA == 0);
@@ -3017,7 +3049,8 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
                         // (no-tail: every chain lane's length is nsse)
                         const int nbmax = NOTAIL ? (nsse + 15) >> 4 : __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
-                        if (chl) acc = chain_sum_pl(cur + cs * P + cc * S, len, nbmax, acc);
+                        // (no-tail: the tail-chain lanes keep acc = 0)
+                        if (chl && (!NOTAIL || cc < 4)) acc = chain_sum_pl<NOTAIL>(cur + cs * P + cc * S, len, nbmax, acc);
                         if (g + HW <= g_last) padA(g + HW, nxt);
                     }
                     __syncthreads();
@@ -3078,6 +3111,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 __syncthreads();
             }
             BX_MARK(3);  // iteration head (restage)
+            bx_prio_lo();
             BX_COUNT(10);
             nwin++;
             const unsigned W0 = pack_w(w00, w01), W1 = pack_w(w10, w11);
@@ -3202,6 +3236,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                 T[5 + c] = T2[c], M[5 + c] = M2[c], m[5 + c] = m2[c];
             }
             BX_MARK(4);  // b main pass
+            bx_prio_hi();
             int *rec = X + par * 4 * kBxRecInts;
             par ^= 1;
             bx_publish<10>(T, rec, NOTAIL || tB == 0);
@@ -3336,7 +3371,8 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
                         // (no-tail: every chain lane's length is nsse)
                         const int nbmax = NOTAIL ? (nsse + 15) >> 4 : __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
-                        if (chl) acc = chain_sum_pl(cur + cs * P + cc * S, len, nbmax, acc);
+                        // (no-tail: the tail-chain lanes keep acc = 0)
+                        if (chl && (!NOTAIL || cc < 4)) acc = chain_sum_pl<NOTAIL>(cur + cs * P + cc * S, len, nbmax, acc);
                         if (g + HW <= g_last) pad_tile(g + HW, nxt);
                     }
 #ifdef PSN_LK_STAMPS

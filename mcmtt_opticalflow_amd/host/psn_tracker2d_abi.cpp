@@ -602,6 +602,12 @@ int psn_t2d_group_debug_host_times(psn_t2d_group *g, double *out6) {
     return 0;
 }
 
+int psn_t2d_group_debug_host_match_times(psn_t2d_group *g, double *out4) {
+    if (!g || !out4) return PSN_LK_ERR_ARG;
+    g->flow.HostMatchTimes(out4);
+    return 0;
+}
+
 int psn_t2d_group_trackers(psn_t2d_group *g, int cam, psn_t2d_tracker *out, int cap, int *n) {
     if (!g || cam < 0 || (size_t)cam >= g->io().size() || !n || cap < 0 || (cap > 0 && !out)) return PSN_LK_ERR_ARG;
     const std::deque<psn::Tracker2D *> &a = g->flow.ActiveTrackers((size_t)cam);

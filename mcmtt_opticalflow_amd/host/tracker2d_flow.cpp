@@ -1526,10 +1526,20 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     for (size_t c = 0; c < cams_.size(); c++) {
         Cam &cam = cams_[c];
         CamFrame &f = io[c];
+        clk::time_point p = clk::now();
+        auto part = [&](int i) {
+            const clk::time_point q = clk::now();
+            host_us_[5 + i] += std::chrono::duration<double, std::micro>(q - p).count();
+            p = q;
+        };
         BackwardEnd(f.objects, f.features);
+        part(0);
         ForwardDone(cam.trackers, cam.fstatus, f.objects, f.cost);
+        part(1);
         const std::vector<int> match = AssignDetections(f.cost, f.objects.size(), cam.trackers.size());
+        part(2);
         MatchingAndUpdating(f.objects, cam.active, cam.storage, match, run_frame_, cam.newTrackerID, f.result);
+        part(3);
         f.result.camID = cam.camID;
         // the next frame's forward calls (launched from this frame's chains): these trackers
         cam.trackers.assign(cam.active.begin(), cam.active.end());

@@ -129,6 +129,12 @@ class Tracker2DFlow {
         out[5] = host_calls_;
         host_calls_ = 0;
     }
+    // diagnostic: accumulated host microseconds of the matching phase's parts over
+    // the cameras (overlap flags, forward matching costs, assignment, tracker
+    // update + results); reset on read
+    void HostMatchTimes(double out[4]) {
+        for (int i = 0; i < 4; i++) out[i] = host_us_[5 + i], host_us_[5 + i] = 0;
+    }
 
     // backward chain steps on the device (default) or on the host (single-camera API)
     void SetDeviceChain(bool on) { device_chain_ = on; }
@@ -250,7 +256,7 @@ class Tracker2DFlow {
     std::vector<PassCam> run_pass_;  // the pass between RunLaunch and RunComplete
     std::vector<CamFrame> *pre_io_ = nullptr;  // the io of a frame RunComplete launched ahead
     bool launched_ahead_ = false;              // run_pass_ is that frame, awaiting its RunLaunch
-    double host_us_[5] = {0, 0, 0, 0, 0};
+    double host_us_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     long host_calls_ = 0;
     unsigned run_frame_ = 0;
     bool run_gridfast_ = false;

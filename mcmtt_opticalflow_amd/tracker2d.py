@@ -174,6 +174,7 @@ def load():
                                               ctypes.c_uint32]
     L.psn_t2d_group_trackers.argtypes = [vp, ip, ctypes.POINTER(Tracker), ip, ctypes.POINTER(ip)]
     L.psn_t2d_group_debug_host_times.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.psn_t2d_group_debug_host_match_times.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
     _lib = L
     return L
 
@@ -514,7 +515,11 @@ class Group:
         self._check(self._L.psn_t2d_group_debug_host_times(self._h, out), "debug_host_times")
         n = max(out[5], 1.0)
         keys = ["next_chains_enqueued", "device_done", "unpacked", "matched", "next_forward_enqueued"]
-        return {k: round(out[i] / n, 1) for i, k in enumerate(keys)} | {"completes": int(out[5])}
+        m = (ctypes.c_double * 4)()
+        self._check(self._L.psn_t2d_group_debug_host_match_times(self._h, m), "debug_host_match_times")
+        parts = ["overlap_flags", "forward_costs", "assignment", "update_results"]
+        return ({k: round(out[i] / n, 1) for i, k in enumerate(keys)} | {"completes": int(out[5])}
+                | {"match_parts_us": {k: round(m[i] / n, 1) for i, k in enumerate(parts)}})
 
     def trackers(self, cam: int, cap: int = 256) -> list[Tracker]:
         out = (Tracker * cap)()
