@@ -46,19 +46,41 @@ Rect LocalSearchKLT(Rect preBox, const std::vector<Point2f> &preFeatures, const 
     const double windowSize = preBox.w * kNeighborRatio * kFlowScale;
     size_t maxX = 0, maxY = 0;
     Point2D est(0.0, 0.0);
+    // neighbour counts |v[d] - v[c]| < windowSize of every d. On sorted finite
+    // values with windowSize > 0 the neighbours of d are one index range [lo, hi)
+    // whose ends never decrease with d (fl(a - b) is monotone in a and b, and
+    // |fl(a - b)| = fl(b - a)), so two pointers count exactly what the reference's
+    // double loop counts; otherwise (NaN, windowSize <= 0) that loop itself.
+    const bool finite = windowSize > 0 &&
+                        std::all_of(vecDx.begin(), vecDx.end(), [](double v) { return std::isfinite(v); }) &&
+                        std::all_of(vecDy.begin(), vecDy.end(), [](double v) { return std::isfinite(v); });
+    auto counts = [&](const std::vector<double> &v, std::vector<size_t> &cnt) {
+        cnt.assign(numMoving, 0);
+        if (finite) {
+            size_t lo = 0, hi = 0;
+            for (size_t d = 0; d < numMoving; d++) {
+                while (!(v[d] - v[lo] < windowSize)) lo++;  // lo <= d: v[d] - v[d] = 0 < windowSize
+                if (hi < d + 1) hi = d + 1;
+                while (hi < numMoving && v[hi] - v[d] < windowSize) hi++;
+                cnt[d] = hi - lo;
+            }
+        } else {
+            for (size_t d = 0; d < numMoving; d++)
+                for (size_t c = 0; c < numMoving; c++)
+                    if (std::abs(v[d] - v[c]) < windowSize) cnt[d]++;
+        }
+    };
+    std::vector<size_t> cntX, cntY;
+    counts(vecDx, cntX);
+    counts(vecDy, cntY);
     for (size_t d = 0; d < numMoving; d++) {
-        size_t nx = 0, ny = 0;
-        for (size_t c = 0; c < numMoving; c++) {
-            if (std::abs(vecDx[d] - vecDx[c]) < windowSize) nx++;
-            if (std::abs(vecDy[d] - vecDy[c]) < windowSize) ny++;
-        }
-        if (maxX < nx) {
+        if (maxX < cntX[d]) {
             est.x = vecDx[d];
-            maxX = nx;
+            maxX = cntX[d];
         }
-        if (maxY < ny) {
+        if (maxY < cntY[d]) {
             est.y = vecDy[d];
-            maxY = ny;
+            maxY = cntY[d];
         }
     }
     for (size_t v = 0; v < numMoving; v++)

@@ -91,6 +91,24 @@ def test_local_search_klt_matches_oracle(kind):
         assert g_inl == r_inl, (kind, trial)
 
 
+def test_local_search_klt_window_edges():
+    # neighbour counts at the window's edge (integer moves, integer windows
+    # 0.2 * w), empty windows (w <= 0) and long runs of equal moves: the
+    # two-pointer count of the host code must equal the restatement's double loop
+    rng = np.random.default_rng(7)
+    for trial in range(300):
+        n = int(rng.integers(1, 101))
+        pre = rng.uniform(0, 100, (n, 2)).astype(np.float32)
+        d = rng.integers(-4, 5, (n, 2)).astype(np.float64) * rng.choice([0.5, 1.0, 2.0])
+        cur = (pre + d).astype(np.float32)
+        w = float(rng.choice([0.0, -5.0, 5.0, 10.0, 15.0, 20.0, 25.0, 7.5, 12.5]))
+        box = (rng.uniform(0, 200), rng.uniform(0, 200), w, 40.0)
+        g_box, g_inl = t2d.local_search_klt(box, pre, cur)
+        r_box, r_inl = ORC.local_search_klt(ORC.Rect(*box), pre, cur)
+        assert g_box == r_box.tuple(), trial
+        assert g_inl == r_inl, trial
+
+
 def test_local_search_klt_semantics():
     # fewer than half the points move >= 0.1 px: the box stays and no inliers
     pre = np.zeros((10, 2), np.float32)
