@@ -2537,6 +2537,11 @@ __device__ __forceinline__ float add16m(float acc, const bxf4 &a, const bxf4 &b,
 #ifndef PSN_BX_PRIO
 #define PSN_BX_PRIO 1
 #endif
+// b fallback: tiles handed from their writer waves to the chain lanes through
+// LDS flags (three buffers) rather than one workgroup barrier per tile
+#ifndef PSN_BX_FLAGS
+#define PSN_BX_FLAGS 1
+#endif
 __device__ __forceinline__ void bx_prio_hi() { __builtin_amdgcn_s_setprio(PSN_BX_PRIO); }
 __device__ __forceinline__ void bx_prio_lo() { __builtin_amdgcn_s_setprio(0); }
 // UNIFORM (no-tail builds): every chain lane has nbmax blocks, so no block is
@@ -2641,6 +2646,10 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
     int *X = (int *)smem;                      // chain-check records, two parities
     float *RS = (float *)(X + kBxXInts);       // serial-chain results (wave 0 -> all)
     int *EP = (int *)(RS + 16);                // err partial sums per wave
+    // b-fallback tile hand-off flags (PSN_BX_FLAGS): ready[3], consumed[3]
+    volatile int *FLG = (volatile int *)(RS + 24);
+    if (threadIdx.x < 6) FLG[threadIdx.x] = -1;  // ordered by the first level barrier
+    int fb_epoch = 0;
     uint8_t *JR = smem + lay.jr;
     const uint32_t *JR32 = (const uint32_t *)JR;
     uint8_t *UN = smem + lay.un;
@@ -3289,7 +3298,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
                         const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
                         const bool on = 4 * qk + i < w;
-                        float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 4 * PC;
+                        float *d1 = on ? buf + (su ? i * S + base : base + i) : PL + 6 * PC;  // past 3 buffers
                         d1[0] = (float)__mul24(d[i], gx);
                         d1[on ? P : 1] = (float)__mul24(d[i], gy);
                     }
@@ -3353,6 +3362,53 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     float *rg = buf + cs * P + cc * S;
                     for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
                 };
+#if PSN_BX_FLAGS
+                if (split) {
+                    // Three tile buffers, handed over through LDS flags instead of a
+                    // workgroup barrier per tile: wave w writes its tiles 2w, 2w+1 as
+                    // soon as their buffers are free (tile g waits for the chain lanes
+                    // to finish tile g - 3), wave 0 first writes its own tiles, then
+                    // its chain lanes sum tile after tile as each one is flagged ready.
+                    // No cycle: tile g's writer waits only for tiles of lower waves.
+                    const int ep = ++fb_epoch, wv = ftid >> 6, fl = ftid & 63;
+                    auto tag = [&](int g) { return ep * 16 + g; };
+                    auto spin = [&](int idx, int want) {
+                        for (int n = 0; n < (1 << 22); n++) {  // (a bound: never a hang)
+                            if (__builtin_amdgcn_readfirstlane(FLG[idx]) == want) break;
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                        asm volatile("" ::: "memory");
+                    };
+                    for (int g = max(h0, 2 * wv); g <= min(2 * wv + 1, g_last); g++) {
+                        const int b = (g - h0) % 3;
+                        if (g - h0 >= 3) spin(3 + b, tag(g - 3));
+                        write_tile(g, PL + b * 2 * PC);
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        if (fl == 0) FLG[b] = tag(g);
+                    }
+                    BX_MARK(6);  // serial b: own tiles' products
+                    if (wv == 0) {
+                        for (int g = h0; g <= g_last; g++) {
+                            const int b = (g - h0) % 3;
+                            spin(b, tag(g));
+                            float *cur = PL + b * 2 * PC;
+                            int sa, ta, nsse, ntail;
+                            tile_geo(g, sa, ta, nsse, ntail);
+                            const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                            const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
+                            if (chl) {  // zero this chain's pad (its writer never touches it)
+                                float *rg = cur + cs * P + cc * S;
+                                for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
+                            }
+                            const int nbmax = NOTAIL ? (nsse + 15) >> 4 : __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
+                            if (chl && (!NOTAIL || cc < 4)) acc = chain_sum_pl<NOTAIL>(cur + cs * P + cc * S, len, nbmax, acc);
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                            if (fl == 0) FLG[3 + b] = tag(g);
+                        }
+                    }
+                } else
+#endif
+                {
                 write_tile(h0, PL);
                 pad_tile(h0, PL);
                 __syncthreads();
@@ -3385,6 +3441,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     bx_acc[13] += tc2 - tc1;  // barrier wait
                     bx_acc[14]++;
 #endif
+                }
                 }
                 BX_MARK(7);  // serial b: pipelined products + chains
                 BX_COUNT(11);
