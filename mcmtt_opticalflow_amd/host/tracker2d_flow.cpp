@@ -181,6 +181,17 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
     }
     ev_gf_ = e3;
     gf_rec_ = false;
+    for (int p = 0; p < 2; p++) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+            err_ = "forward block events";
+            return PSN_LK_ERR_HIP;
+        }
+        ev_fend_[p] = a;
+        ev_fcopied_[p] = b;
+    }
+    fwd_par_ = 0;
     for (int r = 0; r < kT2dResBlocks; r++) {
         hipEvent_t a = nullptr, b = nullptr;
         if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess ||
@@ -216,10 +227,10 @@ struct Tracker2DFlow::DeviceBuffers {
         int *d_cnt = nullptr, *d_tot = nullptr, *d_last = nullptr;
     } sc[2];
     // forward calls: inputs [counts | (256-B aligned) points], outputs [status | (aligned) points] (one copy each)
-    float *d_fin = nullptr, *d_fout = nullptr, *d_ferr = nullptr;
-    uint8_t *d_fstatus = nullptr;
+    float *d_fin = nullptr, *d_fout[2] = {nullptr, nullptr}, *d_ferr = nullptr;
+    uint8_t *d_fstatus[2] = {nullptr, nullptr};
     int *d_fcnt = nullptr;
-    char *d_fiblk = nullptr, *d_foblk = nullptr, *h_fiblk = nullptr, *h_foblk = nullptr;
+    char *d_fiblk = nullptr, *d_foblk[2] = {nullptr, nullptr}, *h_fiblk = nullptr, *h_foblk = nullptr;
     size_t fi_off_pts = 0, fo_off_pts = 0;
     // pinned staging of the chain inputs (and GridFAST features), two sets: a
     // pass's set is written by its launch and read back by its completion, and
@@ -294,10 +305,10 @@ struct Tracker2DFlow::DeviceBuffers {
         nchains = 0;
     }
     void release_forward() {
-        free_all({d_fiblk, d_foblk, d_ferr}, {h_fiblk, h_foblk});
-        d_fiblk = d_foblk = h_fiblk = h_foblk = nullptr;
-        d_fin = d_fout = d_ferr = nullptr;
-        d_fstatus = nullptr;
+        free_all({d_fiblk, d_foblk[0], d_foblk[1], d_ferr}, {h_fiblk, h_foblk});
+        d_fiblk = d_foblk[0] = d_foblk[1] = h_fiblk = h_foblk = nullptr;
+        d_fin = d_fout[0] = d_fout[1] = d_ferr = nullptr;
+        d_fstatus[0] = d_fstatus[1] = nullptr;
         d_fcnt = nullptr;
         h_fin = h_fwd_out = nullptr;
         h_fwd_st = nullptr;
@@ -337,7 +348,7 @@ void Tracker2DFlow::Finalize() {
             cs = nullptr;
         }
     for (void **e : {&ev_chain_, &ev_fwd_, &ev_gf_, &ev_set0_[0], &ev_set0_[1], &ev_set0_[2], &ev_fread_[0], &ev_fread_[1],
-                     &ev_fread_[2]})
+                     &ev_fread_[2], &ev_fend_[0], &ev_fend_[1], &ev_fcopied_[0], &ev_fcopied_[1]})
         if (*e) {
             (void)hipEventDestroy((hipEvent_t)*e);
             *e = nullptr;
@@ -402,6 +413,7 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     DeviceBuffers &b = *dev_;
     if (b.nfwd_pts >= nfwd_pts && b.nfwd_jobs >= nfwd_jobs && b.d_fin) return PSN_LK_OK;
     if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+    SyncChains();  // result copies of the forward blocks run on the chain streams
     // results of a pass not unpacked yet (its copy was enqueued) move to the new buffers
     std::vector<uint8_t> keep_st;
     std::vector<float> keep_pts;
@@ -417,7 +429,8 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     b.fi_off_pts = (J * 4 + 255) & ~(size_t)255;
     b.fo_off_pts = (F + 255) & ~(size_t)255;
     dm((void **)&b.d_fiblk, b.fi_off_pts + F * 8);
-    dm((void **)&b.d_foblk, b.fo_off_pts + F * 8);
+    dm((void **)&b.d_foblk[0], b.fo_off_pts + F * 8);
+    dm((void **)&b.d_foblk[1], b.fo_off_pts + F * 8);
     dm((void **)&b.d_ferr, F * 4);
     hm((void **)&b.h_fiblk, b.fi_off_pts + F * 8);
     hm((void **)&b.h_foblk, b.fo_off_pts + F * 8);
@@ -430,8 +443,10 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     b.d_fin = (float *)(b.d_fiblk + b.fi_off_pts);
     b.h_fcnt = (int *)b.h_fiblk;
     b.h_fin = (float *)(b.h_fiblk + b.fi_off_pts);
-    b.d_fstatus = (uint8_t *)b.d_foblk;
-    b.d_fout = (float *)(b.d_foblk + b.fo_off_pts);
+    for (int p = 0; p < 2; p++) {
+        b.d_fstatus[p] = (uint8_t *)b.d_foblk[p];
+        b.d_fout[p] = (float *)(b.d_foblk[p] + b.fo_off_pts);
+    }
     b.h_fwd_st = (uint8_t *)b.h_foblk;
     b.h_fwd_out = (float *)(b.h_foblk + b.fo_off_pts);
     if (!keep_st.empty()) {
@@ -717,16 +732,23 @@ int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb,
         }
     }
     const DeviceBuffers::ResView rv = b.view(b.d_res[src_rb]);
-    if (hipStreamWaitEvent(fs, (hipEvent_t)ev_set0_[src_rb], 0) != hipSuccess) {
-        err_ = "forward: set-0 event";
+    const int par = fwd_par_ ^ 1;  // the block the last-but-one launch wrote: its copy waited for below
+    if (hipStreamWaitEvent(fs, (hipEvent_t)ev_set0_[src_rb], 0) != hipSuccess ||
+        hipStreamWaitEvent(fs, (hipEvent_t)ev_fcopied_[par], 0) != hipSuccess) {
+        err_ = "forward: set-0 / block events";
         return PSN_LK_ERR_HIP;
     }
     rc = psn_lk_set_stream(lk_, fs);
     if (!rc)
-        rc = psn_lk_track_device_counted_strided(lk_, fwd_queries_.data(), (int)K, rv.setcnt, (int)S, rv.sets, b.d_fout,
-                                                 b.d_fstatus, b.d_ferr);
+        rc = psn_lk_track_device_counted_strided(lk_, fwd_queries_.data(), (int)K, rv.setcnt, (int)S, rv.sets,
+                                                 b.d_fout[par], b.d_fstatus[par], b.d_ferr);
     const int rs = psn_lk_set_stream(lk_, st);
     if (rc || rs) return fail(rc ? rc : rs, "forward launch");
+    fwd_par_ = par;
+    if (hipEventRecord((hipEvent_t)ev_fend_[par], fs) != hipSuccess) {
+        err_ = "forward: end event";
+        return PSN_LK_ERR_HIP;
+    }
     if (hipEventRecord((hipEvent_t)ev_fread_[src_rb], fs) != hipSuccess) {
         err_ = "forward: read event";
         return PSN_LK_ERR_HIP;
@@ -735,6 +757,7 @@ int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb,
     for (PassCam &p : pc) {
         p.fwd_rb = src_rb;
         p.fwd_n = K * S * cap;
+        p.fwd_par = par;
     }
     return PSN_LK_OK;
 }
@@ -787,14 +810,19 @@ int Tracker2DFlow::PassLaunchForward(std::vector<PassCam> &pc) {
             }
         }
         // counts and points in one copy
+        const int par = fwd_par_ ^ 1;
+        chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_fcopied_[par], 0), "forward block event");
         chk(hipMemcpyAsync(b.d_fiblk, b.h_fiblk, b.fi_off_pts + F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
         if (rc) return rc;
         rc = psn_lk_set_stream(lk_, fs);
         if (!rc)
-            rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_fcnt, b.d_fin, b.d_fout, b.d_fstatus,
-                                             b.d_ferr);
+            rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_fcnt, b.d_fin, b.d_fout[par],
+                                             b.d_fstatus[par], b.d_ferr);
         const int rs = psn_lk_set_stream(lk_, st);
         if (rc || rs) return fail(rc ? rc : rs, "forward launch");
+        fwd_par_ = par;
+        chk(hipEventRecord((hipEvent_t)ev_fend_[par], fs), "forward end event");
+        for (PassCam &p : pc) p.fwd_par = par;
     }
     return rc;
 }
@@ -838,11 +866,16 @@ int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
             "chain results");
     if (!pc.empty() && pc[0].fwd_rb >= 0) F = pc[0].fwd_n;  // the forward launch from the previous frame's chains
     if (F && bp) {
-        // status and points in one copy
-        chk(hipMemcpyAsync(bp->h_foblk, bp->d_foblk, bp->fo_off_pts + F * 8, hipMemcpyDeviceToHost, fs),
+        // status and points in one copy, on the chain stream after the forward
+        // launch (the forward stream goes on with the next frame's launch)
+        const int par = pc[0].fwd_par;
+        chk(hipStreamWaitEvent(st, (hipEvent_t)ev_fend_[par], 0), "forward end wait");
+        chk(hipMemcpyAsync(bp->h_foblk, bp->d_foblk[par], bp->fo_off_pts + F * 8, hipMemcpyDeviceToHost, st),
             "forward results");
+        chk(hipEventRecord((hipEvent_t)ev_fcopied_[par], st), "forward copied event");
     }
-    // everything the pass enqueued on either stream precedes these records
+    // everything the pass enqueued precedes these records (the forward work of
+    // a pass without result copy: the forward stream's record)
     chk(hipEventRecord((hipEvent_t)ev_chain_, st), "chain results event");
     chk(hipEventRecord((hipEvent_t)ev_fwd_, fs), "forward results event");
     wait_chain_ = wait_fwd_ = rc == PSN_LK_OK;

@@ -181,6 +181,7 @@ class Tracker2DFlow {
         int rb = -1;        // the pass's result block
         int fwd_rb = -1;    // the result block its forward calls read (LaunchForwardFromChains), or -1
         size_t fwd_n = 0;   // forward outputs to copy back (that launch's index range)
+        int fwd_par = 0;    // the forward output block its forward launch wrote
     };
     int PassLaunch(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);  // chains, then forward
     int PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uint32_t seed);
@@ -199,6 +200,12 @@ class Tracker2DFlow {
     int trk_rb_ = -1;  // the result block holding the current trackers' set 0 (their next forward call)
     void *ev_set0_[3] = {nullptr, nullptr, nullptr};   // hipEvent_t: a block's set 0 is final (chain stream)
     void *ev_fread_[3] = {nullptr, nullptr, nullptr};  // hipEvent_t: the forward launch reading a block is done
+    // Forward outputs alternate between two device blocks, so that a frame's
+    // result copy (on its chain stream) never sits between two forward launches
+    // on the forward stream: ev_fend_[p] = forward launch into block p done,
+    // ev_fcopied_[p] = block p copied to the host (the next launch into p waits)
+    int fwd_par_ = 0;
+    void *ev_fend_[2] = {nullptr, nullptr}, *ev_fcopied_[2] = {nullptr, nullptr};
     bool fread_rec_[3] = {false, false, false};
     int PassComplete(std::vector<PassCam> &pc, bool gridfast);  // PassWait + PassFeatures + PassUnpack
     int PassWait(std::vector<PassCam> &pc);  // PassCopy + PassSync
