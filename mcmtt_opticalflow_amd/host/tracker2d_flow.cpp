@@ -158,6 +158,11 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
         return PSN_LK_ERR_HIP;
     }
     fwd_stream_ = fs;
+    if (hipStreamCreateWithPriority(&fs, hipStreamNonBlocking, least) != hipSuccess) {
+        err_ = "forward stream";
+        return PSN_LK_ERR_HIP;
+    }
+    fwd_stream2_ = fs;
     for (int i = 0; i < 2; i++) {
         if (hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, greatest) != hipSuccess) {
             err_ = "chain stream";
@@ -227,7 +232,7 @@ struct Tracker2DFlow::DeviceBuffers {
         int *d_cnt = nullptr, *d_tot = nullptr, *d_last = nullptr;
     } sc[2];
     // forward calls: inputs [counts | (256-B aligned) points], outputs [status | (aligned) points] (one copy each)
-    float *d_fin = nullptr, *d_fout[2] = {nullptr, nullptr}, *d_ferr = nullptr;
+    float *d_fin = nullptr, *d_fout[2] = {nullptr, nullptr}, *d_ferr[2] = {nullptr, nullptr};
     uint8_t *d_fstatus[2] = {nullptr, nullptr};
     int *d_fcnt = nullptr;
     char *d_fiblk = nullptr, *d_foblk[2] = {nullptr, nullptr}, *h_fiblk = nullptr, *h_foblk = nullptr;
@@ -305,9 +310,9 @@ struct Tracker2DFlow::DeviceBuffers {
         nchains = 0;
     }
     void release_forward() {
-        free_all({d_fiblk, d_foblk[0], d_foblk[1], d_ferr}, {h_fiblk, h_foblk});
+        free_all({d_fiblk, d_foblk[0], d_foblk[1], d_ferr[0], d_ferr[1]}, {h_fiblk, h_foblk});
         d_fiblk = d_foblk[0] = d_foblk[1] = h_fiblk = h_foblk = nullptr;
-        d_fin = d_fout[0] = d_fout[1] = d_ferr = nullptr;
+        d_fin = d_fout[0] = d_fout[1] = d_ferr[0] = d_ferr[1] = nullptr;
         d_fstatus[0] = d_fstatus[1] = nullptr;
         d_fcnt = nullptr;
         h_fin = h_fwd_out = nullptr;
@@ -326,19 +331,25 @@ void Tracker2DFlow::SyncChains() {
         if (cs) (void)hipStreamSynchronize((hipStream_t)cs);
 }
 
+void Tracker2DFlow::SyncForward() {
+    for (void *fs : {fwd_stream_, fwd_stream2_})
+        if (fs) (void)hipStreamSynchronize((hipStream_t)fs);
+}
+
 void Tracker2DFlow::Finalize() {
     if (dev_) {
         if (lk_) psn_lk_sync(lk_);
-        if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        SyncForward();
         dev_->release();
         delete dev_;
         dev_ = nullptr;
     }
-    if (fwd_stream_) {
-        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
-        (void)hipStreamDestroy((hipStream_t)fwd_stream_);
-        fwd_stream_ = nullptr;
-    }
+    for (void **fs : {&fwd_stream_, &fwd_stream2_})
+        if (*fs) {
+            (void)hipStreamSynchronize((hipStream_t)*fs);
+            (void)hipStreamDestroy((hipStream_t)*fs);
+            *fs = nullptr;
+        }
     if (lk_) psn_lk_destroy(lk_);
     lk_ = nullptr;
     for (void *&cs : chain_streams_)
@@ -366,7 +377,7 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
     if (lk_) psn_lk_sync(lk_);
     SyncChains();
     // a forward launch may still read a result block's set 0
-    if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+    SyncForward();
     b.release_chains();
     for (int r = 0; r < DeviceBuffers::kResBlocks; r++) {
         chain_info_[r].valid = false;
@@ -412,7 +423,7 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     if (!dev_) dev_ = new DeviceBuffers();
     DeviceBuffers &b = *dev_;
     if (b.nfwd_pts >= nfwd_pts && b.nfwd_jobs >= nfwd_jobs && b.d_fin) return PSN_LK_OK;
-    if (fwd_stream_) (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+    SyncForward();
     SyncChains();  // result copies of the forward blocks run on the chain streams
     // results of a pass not unpacked yet (its copy was enqueued) move to the new buffers
     std::vector<uint8_t> keep_st;
@@ -431,7 +442,8 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     dm((void **)&b.d_fiblk, b.fi_off_pts + F * 8);
     dm((void **)&b.d_foblk[0], b.fo_off_pts + F * 8);
     dm((void **)&b.d_foblk[1], b.fo_off_pts + F * 8);
-    dm((void **)&b.d_ferr, F * 4);
+    dm((void **)&b.d_ferr[0], F * 4);
+    dm((void **)&b.d_ferr[1], F * 4);
     hm((void **)&b.h_fiblk, b.fi_off_pts + F * 8);
     hm((void **)&b.h_foblk, b.fo_off_pts + F * 8);
     if (!ok) {
@@ -709,7 +721,8 @@ int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb,
     int rc = EnsureForward(K * S * cap, K);
     if (rc) return rc;
     DeviceBuffers &b = *dev_;
-    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    const int par = fwd_par_ ^ 1;  // the block the last-but-one launch wrote: its copy waited for below
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)FwdStream(par);
     fwd_queries_.assign(K, psn_lk_query{});
     for (PassCam &p : pc) {
         if (p.cam >= ci.k0.size()) continue;
@@ -732,7 +745,6 @@ int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb,
         }
     }
     const DeviceBuffers::ResView rv = b.view(b.d_res[src_rb]);
-    const int par = fwd_par_ ^ 1;  // the block the last-but-one launch wrote: its copy waited for below
     if (hipStreamWaitEvent(fs, (hipEvent_t)ev_set0_[src_rb], 0) != hipSuccess ||
         hipStreamWaitEvent(fs, (hipEvent_t)ev_fcopied_[par], 0) != hipSuccess) {
         err_ = "forward: set-0 / block events";
@@ -741,7 +753,7 @@ int Tracker2DFlow::LaunchForwardFromChains(std::vector<PassCam> &pc, int src_rb,
     rc = psn_lk_set_stream(lk_, fs);
     if (!rc)
         rc = psn_lk_track_device_counted_strided(lk_, fwd_queries_.data(), (int)K, rv.setcnt, (int)S, rv.sets,
-                                                 b.d_fout[par], b.d_fstatus[par], b.d_ferr);
+                                                 b.d_fout[par], b.d_fstatus[par], b.d_ferr[par]);
     const int rs = psn_lk_set_stream(lk_, st);
     if (rc || rs) return fail(rc ? rc : rs, "forward launch");
     fwd_par_ = par;
@@ -779,7 +791,8 @@ int Tracker2DFlow::PassLaunchForward(std::vector<PassCam> &pc) {
     int rc = EnsureForward(F, J);
     if (rc) return rc;
     DeviceBuffers &b = *dev_;
-    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)fwd_stream_;
+    const int par = fwd_par_ ^ 1;
+    hipStream_t st = (hipStream_t)psn_lk_get_stream(lk_), fs = (hipStream_t)FwdStream(par);
     auto chk = [&](hipError_t e, const char *what) {
         if (e != hipSuccess && !rc) {
             err_ = std::string(what) + ": " + hipGetErrorString(e);
@@ -810,14 +823,15 @@ int Tracker2DFlow::PassLaunchForward(std::vector<PassCam> &pc) {
             }
         }
         // counts and points in one copy
-        const int par = fwd_par_ ^ 1;
+        // (one input block: the other stream's last launch has read it)
+        chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_fend_[par ^ 1], 0), "forward input block event");
         chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_fcopied_[par], 0), "forward block event");
         chk(hipMemcpyAsync(b.d_fiblk, b.h_fiblk, b.fi_off_pts + F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
         if (rc) return rc;
         rc = psn_lk_set_stream(lk_, fs);
         if (!rc)
             rc = psn_lk_track_device_counted(lk_, fwd_queries_.data(), (int)J, b.d_fcnt, b.d_fin, b.d_fout[par],
-                                             b.d_fstatus[par], b.d_ferr);
+                                             b.d_fstatus[par], b.d_ferr[par]);
         const int rs = psn_lk_set_stream(lk_, st);
         if (rc || rs) return fail(rc ? rc : rs, "forward launch");
         fwd_par_ = par;
@@ -859,7 +873,7 @@ int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
             for (const Job &jb : *p.fwd) F += jb.in->size();
     }
     hipStream_t st = (hipStream_t)(pc.empty() ? psn_lk_get_stream(lk_) : ChainStream(pc[0].set)),
-                fs = (hipStream_t)fwd_stream_;
+                fs = (hipStream_t)FwdStream(pc.empty() ? fwd_par_ : pc[0].fwd_par);
     const int rb = pc.empty() ? -1 : pc[0].rb;
     if (K && bp && rb >= 0)
         chk(hipMemcpyAsync(bp->h_res[rb], bp->d_res[rb], bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
@@ -1005,7 +1019,7 @@ int Tracker2DFlow::DevicePass(const std::vector<Detection> &dets, std::vector<st
     int rc = PassLaunch(pc, gridfast, seed);
     if (rc) {  // drain what was enqueued before returning the error
         SyncChains();
-        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        SyncForward();
         return rc;
     }
     return PassComplete(pc, gridfast);
@@ -1488,7 +1502,7 @@ int Tracker2DFlow::RunLaunch(unsigned frameIdx, std::vector<CamFrame> &io, bool 
     if (!rc) rc = PassLaunchChains(run_pass_, gridfast, seed);
     if (rc) {  // nothing of the frame stays in flight; the result blocks as before
         SyncChains();
-        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        SyncForward();
         run_pass_.clear();
         next_rb_ = saved_next_rb;
         last_rb_ = saved_last_rb;
@@ -1534,7 +1548,7 @@ int Tracker2DFlow::RunComplete(std::vector<CamFrame> &io, std::vector<CamFrame> 
     // frames staged again (the rings as before), frame t still completed
     auto abandon_next = [&]() {
         SyncChains();
-        (void)hipStreamSynchronize((hipStream_t)fwd_stream_);
+        SyncForward();
         UnadoptFrames();
         next_rb_ = saved_next_rb;
         last_rb_ = saved_last_rb;

@@ -236,6 +236,12 @@ class Tracker2DFlow {
 
     psn_lk_ctx *lk_ = nullptr;
     void *fwd_stream_ = nullptr;    // hipStream_t of the forward launch, beside the chain's launches (lowest priority)
+    // consecutive forward launches alternate between fwd_stream_ (output block 0)
+    // and fwd_stream2_ (block 1): a frame's forward may start while the last
+    // one's slowest workgroups still run
+    void *fwd_stream2_ = nullptr;
+    void *FwdStream(int par) const { return par ? fwd_stream2_ : fwd_stream_; }
+    void SyncForward();
     // the backward chains (highest priority): pass i of the staging set si runs on
     // chain_streams_[si], so the chains of frame t+1 start beside frame t's last steps
     void *ev_gf_ = nullptr;  // after a pass's GridFAST launches (the context's detector scratch)
