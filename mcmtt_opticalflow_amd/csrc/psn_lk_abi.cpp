@@ -40,7 +40,13 @@ struct psn_lk_ctx {
     // the uploads of several frames run back to back while their builds wait on
     // the ingest stream (created at the highest priority: a build gates later
     // LK launches and must not wait behind them for compute-unit slots)
-    hipStream_t copy_stream = nullptr;
+    // Consecutive uploads go round-robin to kCopyStreams copy streams: the cameras
+    // of a frame-set upload in parallel on several DMA engines (one engine moves
+    // a 1080p BGR frame in ~0.3 ms; four in a row were the frame's critical path).
+    static constexpr int kCopyStreams = 4;
+    hipStream_t copy_streams[kCopyStreams] = {};
+    hipStream_t copy_stream = nullptr;  // copy_streams[0]
+    int copy_rr = 0;
     std::vector<hipEvent_t> copy_done;
     int overlap = PSN_LK_OVERLAP_OFF;
     // PSN_LK_OVERLAP_FUSED: the last pushed build is deferred and run inside
@@ -206,7 +212,9 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
             return fail(PSN_LK_ERR_HIP);
         (void)least;
     }
-    if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    for (hipStream_t &cs : c->copy_streams)
+        if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    c->copy_stream = c->copy_streams[0];
     // slot layout: levels back to back, rows padded to 256 B (one HBM burst / 4 x 64-B lines)
     size_t slot_bytes = 0;
     std::vector<size_t> lv_off(c->nlevels);
@@ -267,7 +275,8 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->ingest_stream) (void)hipStreamSynchronize(c->ingest_stream);
-    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    for (hipStream_t cs : c->copy_streams)
+        if (cs) (void)hipStreamSynchronize(cs);
     for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready, &c->copy_done})
         for (auto e : *v)
             if (e) (void)hipEventDestroy(e);
@@ -287,7 +296,8 @@ void psn_lk_destroy(psn_lk_ctx *c) {
         if (p) (void)hipFree(p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->ingest_stream) (void)hipStreamDestroy(c->ingest_stream);
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    for (hipStream_t cs : c->copy_streams)
+        if (cs) (void)hipStreamDestroy(cs);
     delete c;
 }
 
@@ -522,7 +532,7 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
 // The slot's staging buffer, grown to `need` bytes (the old one may still be read by the ingest stream).
 static int ensure_stage(psn_lk_ctx *c, int slot, size_t need) {
     if (c->stage_cap[slot] >= need) return PSN_LK_OK;
-    HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+    for (hipStream_t cs : c->copy_streams) HIPCHK(c, hipStreamSynchronize(cs));
     HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
     if (c->d_stage[slot]) (void)hipFree(c->d_stage[slot]);
     c->d_stage[slot] = nullptr;
@@ -562,7 +572,7 @@ int psn_lk_push_frame_async(psn_lk_ctx *c, int slot, const uint8_t *host, int st
     if (rc) return rc;
     const size_t row = (size_t)c->width * channels, need = row * c->height;
     if ((rc = ensure_stage(c, slot, need))) return rc;
-    hipStream_t s = c->ingest_stream, cs = c->copy_stream;
+    hipStream_t s = c->ingest_stream, cs = c->copy_streams[c->copy_rr++ % psn_lk_ctx::kCopyStreams];
     // the staging buffer is read only by this slot's previous build (its ready
     // event); the build waits for the upload and for every read of the slot
     if (c->ready_rec[slot]) HIPCHK(c, hipStreamWaitEvent(cs, c->slot_ready[slot], 0));
