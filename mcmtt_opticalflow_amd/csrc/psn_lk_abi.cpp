@@ -35,7 +35,12 @@ struct psn_lk_ctx {
     // every launch that reads the slot, on whatever stream it runs), free after
     // the reads (one event per reading stream, all waited for by the next build
     // into the slot)
-    hipStream_t ingest_stream = nullptr;
+    // psn_lk_push_frame_async builds go round-robin to kIngestStreams streams:
+    // consecutive cameras' builds run side by side once their uploads land
+    static constexpr int kIngestStreams = 2;
+    hipStream_t ingest_streams[kIngestStreams] = {};
+    hipStream_t ingest_stream = nullptr;  // ingest_streams[0]
+    int ingest_rr = 0;
     // psn_lk_push_frame_async: host uploads on their own stream (copy engine), so
     // the uploads of several frames run back to back while their builds wait on
     // the ingest stream (created at the highest priority: a build gates later
@@ -208,8 +213,9 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     {
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return fail(PSN_LK_ERR_HIP);
-        if (hipStreamCreateWithPriority(&c->ingest_stream, hipStreamNonBlocking, greatest) != hipSuccess)
-            return fail(PSN_LK_ERR_HIP);
+        for (hipStream_t &is : c->ingest_streams)
+            if (hipStreamCreateWithPriority(&is, hipStreamNonBlocking, greatest) != hipSuccess) return fail(PSN_LK_ERR_HIP);
+        c->ingest_stream = c->ingest_streams[0];
         (void)least;
     }
     for (hipStream_t &cs : c->copy_streams)
@@ -274,7 +280,8 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     if (c->pend && c->stream) (void)flush_pending(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-    if (c->ingest_stream) (void)hipStreamSynchronize(c->ingest_stream);
+    for (hipStream_t is : c->ingest_streams)
+        if (is) (void)hipStreamSynchronize(is);
     for (hipStream_t cs : c->copy_streams)
         if (cs) (void)hipStreamSynchronize(cs);
     for (auto *v : {&c->ev_push, &c->ev_track, &c->slot_ready, &c->copy_done})
@@ -295,7 +302,8 @@ void psn_lk_destroy(psn_lk_ctx *c) {
                     (void *)c->d_gf_oc, (void *)c->d_gf_ot})
         if (p) (void)hipFree(p);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-    if (c->ingest_stream) (void)hipStreamDestroy(c->ingest_stream);
+    for (hipStream_t is : c->ingest_streams)
+        if (is) (void)hipStreamDestroy(is);
     for (hipStream_t cs : c->copy_streams)
         if (cs) (void)hipStreamDestroy(cs);
     delete c;
@@ -319,7 +327,7 @@ int psn_lk_sync(psn_lk_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
     int rc = flush_pending(c);
     if (rc) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
+    for (hipStream_t is : c->ingest_streams) HIPCHK(c, hipStreamSynchronize(is));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return PSN_LK_OK;
 }
@@ -338,7 +346,7 @@ int psn_lk_enable_timing(psn_lk_ctx *c, int capacity, int every) {
     HIPCHK(c, hipSetDevice(c->device));
     int rc = flush_pending(c);
     if (rc) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
+    for (hipStream_t is : c->ingest_streams) HIPCHK(c, hipStreamSynchronize(is));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (auto *v : {&c->ev_push, &c->ev_track}) {
         for (auto e : *v)
@@ -533,7 +541,7 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
 static int ensure_stage(psn_lk_ctx *c, int slot, size_t need) {
     if (c->stage_cap[slot] >= need) return PSN_LK_OK;
     for (hipStream_t cs : c->copy_streams) HIPCHK(c, hipStreamSynchronize(cs));
-    HIPCHK(c, hipStreamSynchronize(c->ingest_stream));
+    for (hipStream_t is : c->ingest_streams) HIPCHK(c, hipStreamSynchronize(is));
     if (c->d_stage[slot]) (void)hipFree(c->d_stage[slot]);
     c->d_stage[slot] = nullptr;
     c->stage_cap[slot] = 0;
@@ -572,7 +580,8 @@ int psn_lk_push_frame_async(psn_lk_ctx *c, int slot, const uint8_t *host, int st
     if (rc) return rc;
     const size_t row = (size_t)c->width * channels, need = row * c->height;
     if ((rc = ensure_stage(c, slot, need))) return rc;
-    hipStream_t s = c->ingest_stream, cs = c->copy_streams[c->copy_rr++ % psn_lk_ctx::kCopyStreams];
+    hipStream_t s = c->ingest_streams[c->ingest_rr++ % psn_lk_ctx::kIngestStreams];
+    hipStream_t cs = c->copy_streams[c->copy_rr++ % psn_lk_ctx::kCopyStreams];
     // the staging buffer is read only by this slot's previous build (its ready
     // event); the build waits for the upload and for every read of the slot
     if (c->ready_rec[slot]) HIPCHK(c, hipStreamWaitEvent(cs, c->slot_ready[slot], 0));

@@ -2,7 +2,7 @@
 # A/B of two builds of the product libraries on the default bench line (no CPU
 # legs): directories A and B each hold libpsn_lk.so + libpsn_tracker2d.so;
 # they are copied over mcmtt_opticalflow_amd/lib on the box in turn (A, B, A, B)
-# -> gpurun_out/$1. The product files are restored from A at the end.
+# -> gpurun_out/$1, $4 rounds (default 2). The product files are restored from A at the end.
 set -o pipefail
 R=${1:-libab}
 DA=$2
@@ -10,7 +10,7 @@ DB=$3
 O=gpurun_out/$R
 mkdir -p $O
 L=mcmtt_opticalflow_amd/lib
-for rep in 1 2; do
+for rep in $(seq ${4:-2}); do
   for which in A B; do
     D=$DA; [ $which = B ] && D=$DB
     cp $D/libpsn_lk.so $D/libpsn_tracker2d.so $L/
