@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PSN_LK_ABI_VERSION 4
+#define PSN_LK_ABI_VERSION 5
 
 #define PSN_LK_OK 0
 #define PSN_LK_ERR_ARG (-1)
@@ -39,7 +39,7 @@ extern "C" {
 #define PSN_LK_ERR_SLOT (-5)        /* ring slot out of range or never filled */
 #define PSN_LK_ERR_LEVEL_CAP (-6)   /* query needs more pyramid levels than the ring holds */
 #define PSN_LK_ERR_COMM (-7)        /* RCCL failure */
-#define PSN_LK_ERR_UNSUPPORTED (-8) /* window larger than the LDS-resident limit */
+#define PSN_LK_ERR_UNSUPPORTED (-8) /* window wider than PSN_LK_MAX_WIN_WIDTH (or a feature this build lacks) */
 
 /* flags: OpenCV 2.4.6 values (video/tracking.hpp) + one accumulation-order bit */
 #define PSN_LK_USE_INITIAL_FLOW 4      /* cv::OPTFLOW_USE_INITIAL_FLOW */
@@ -51,7 +51,11 @@ extern "C" {
 #define PSN_LK_TERM_EPS 2
 
 #define PSN_LK_MAX_LEVELS 8
-#define PSN_LK_MAX_WIN_PIXELS 16384    /* w*h kept LDS-resident per point */
+/* Window limits: any height; widths up to PSN_LK_MAX_WIN_WIDTH (one window row
+ * band of the large-window kernel in LDS). Tracker2D passes box.w x box.h
+ * (PSNWhere_Tracker2D.cpp:871-877) and box.w x box.w (:776-782) uncapped; every
+ * box inside a frame up to 6400 px wide is covered. */
+#define PSN_LK_MAX_WIN_WIDTH 6400
 
 /* Arguments of cv::calcOpticalFlowPyrLK after prevImg/nextImg/points. The
  * reference passes only winSize and leaves the rest at their defaults
@@ -189,8 +193,10 @@ int psn_lk_timing_stats(psn_lk_ctx *ctx, int *n_push, double *push_ms, int *n_tr
 /* Per timed track call since psn_lk_enable_timing (before psn_lk_timing_stats,
  * which resets the counts): its duration in ms (HIP events on the stream it
  * was launched on) and the kernel it ran: tag = 10 * UPT + (no-tail build) for
- * lk_kernel_bx<UPT, no-tail>, 1 = lk_kernel_st, 2 = lk_kernel (row-tiled).
- * *n = the calls written (<= cap). */
+ * lk_kernel_bx<UPT, no-tail>, 1 = lk_kernel_st, 2 = lk_kernel (row-tiled),
+ * 3 = lk_kernel_lg (large windows); a call whose queries went to several
+ * launches (one per window class) gets 1000 + the tag of the launch with the
+ * most window pixels. *n = the calls written (<= cap). */
 int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *n);
 
 /* Kernel-variant selection for tests and experiments (never read from the
@@ -202,17 +208,24 @@ int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *
  *   PSN_LK_VARIANT_ONEWAVE     0 = multi-wave iterations in the single-tile kernel
  *   PSN_LK_VARIANT_BOX         0 = box windows run the row-tiled kernel, not lk_kernel_bx
  *   PSN_LK_VARIANT_TILED_LDS   LDS budget (bytes) of a row-tiled workgroup
- *   PSN_LK_VARIANT_FUSED_HELPERS  tile-only workgroups per fused-ingest launch */
+ *   PSN_LK_VARIANT_FUSED_HELPERS  tile-only workgroups per fused-ingest launch
+ *   PSN_LK_VARIANT_LARGE       1 = every query runs the large-window kernel (lk_kernel_lg)
+ *   PSN_LK_VARIANT_LG_LDS      LDS budget (bytes) of a large-window workgroup (its row bands)
+ * Queries are split into one launch per window class (single-tile / box kernel
+ * per units-per-thread and tail build / row-tiled / large), each sized for its
+ * own windows. */
 #define PSN_LK_VARIANT_THREADS 1
 #define PSN_LK_VARIANT_GENERIC 2
 #define PSN_LK_VARIANT_ONEWAVE 3
 #define PSN_LK_VARIANT_BOX 4
 #define PSN_LK_VARIANT_TILED_LDS 5
 #define PSN_LK_VARIANT_FUSED_HELPERS 6
+#define PSN_LK_VARIANT_LARGE 7
+#define PSN_LK_VARIANT_LG_LDS 8
 int psn_lk_debug_set_variant(psn_lk_ctx *ctx, int key, int value);
 
 /* Window-sample counter (SURVEY 8(d)'s compute figure): while on, every box-
- * window LK launch (lk_kernel_bx) adds, per point, sum over levels of
+ * window LK launch (lk_kernel_bx, lk_kernel_lg) adds, per point, sum over levels of
  * w * h * (1 + iterations) to a device counter. _count_samples(ctx, 1) zeroes
  * and enables it (device-wide sync), 0 disables; _read_samples syncs the
  * device and returns the count. Test / benchmark instrumentation. */

@@ -36,10 +36,11 @@ ACCUM_SCALAR = 0x100
 OVERLAP_OFF, OVERLAP_STREAM, OVERLAP_FUSED = 0, 1, 2  # psn_lk_set_ingest_overlap modes
 TERM_COUNT = 1
 TERM_EPS = 2
-MAX_WIN_PIXELS = 16384
+MAX_WIN_WIDTH = 6400  # PSN_LK_MAX_WIN_WIDTH (any window height)
 COMM_UNIQUE_ID_BYTES = 128
 # psn_lk_debug_set_variant keys (tests / experiments; never read from the environment)
-VARIANTS = {"threads": 1, "generic": 2, "onewave": 3, "box": 4, "tiled_lds": 5, "fused_helpers": 6}
+VARIANTS = {"threads": 1, "generic": 2, "onewave": 3, "box": 4, "tiled_lds": 5, "fused_helpers": 6,
+            "large": 7, "lg_lds": 8}
 
 
 class PsnLkError(RuntimeError):
@@ -107,6 +108,12 @@ def timing_launches(L, ctx, cap: int):
 
 
 def kernel_of_tag(tag: int) -> str:
+    """psn_lk_timing_launches tag -> kernel name (a call split over several
+    window-class launches: "mixed:" + the launch with the most window pixels)."""
+    if tag >= 1000:
+        return "mixed:" + kernel_of_tag(tag - 1000)
+    if tag == 3:
+        return "lk_kernel_lg"
     if tag == 1:
         return "lk_kernel_st"
     if tag == 2:

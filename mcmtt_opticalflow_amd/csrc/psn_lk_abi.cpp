@@ -101,6 +101,18 @@ struct psn_lk_ctx {
     // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
     int tiled_lds = 76 * 1024;
     int num_cus = 256;  // compute units of the device (launch shaping)
+    // large-window kernel (lk_kernel_lg): LARGE forces it for every query;
+    // lg_lds = LDS budget of one of its workgroups (row bands of the window)
+    bool force_large = false;
+    int lg_lds = 40 * 1024;
+    // its window-value slots in HBM, one buffer per stream (launches on one
+    // stream run in order; launches on different streams may overlap)
+    struct LgWs {
+        hipStream_t s = nullptr;
+        void *p = nullptr;
+        size_t bytes = 0;
+    };
+    std::vector<LgWs> lg_ws;
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     unsigned long long *d_samples = nullptr;  // psn_lk_debug_count_samples
     bool count_samples = false;
@@ -297,6 +309,11 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     for (uint8_t *p : c->d_stage)
         if (p) (void)hipFree(p);
     if (c->jpeg) psn_jpeg_destroy(c->jpeg);
+    // (a caller's stream in lg_ws may be gone by now: wait for the whole device)
+    if (!c->lg_ws.empty()) (void)hipDeviceSynchronize();
+    for (auto &ws : c->lg_ws)
+        if (ws.p) (void)hipFree(ws.p);
+    c->lg_ws.clear();
     for (void *p : {(void *)c->d_samples, (void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status, (void *)c->d_gf_kp, (void *)c->d_gf_cnt, (void *)c->d_gf_xy,
                     (void *)c->d_gf_oc, (void *)c->d_gf_ot})
@@ -635,14 +652,42 @@ int psn_lk_push_frame(psn_lk_ctx *c, int slot, const uint8_t *host, int stride, 
     return push_host_impl(c, slot, host, stride, channels);
 }
 
-// Validate and plan one query into its device descriptor.
-static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::LkQueryDev &d, int &lds, bool &single,
-                      bool allow_scratch, int &ow_rows, int &ow_lds, int &bx_upt, int &bx_lds) {
-    single = false;
-    bx_upt = 0;
-    bx_lds = 0;
-    ow_rows = 1 << 30;
-    ow_lds = 0;
+// Kernel classes of the planner: each track call's queries go to one launch per
+// class (and per box-kernel build), each launch sized for its own windows.
+enum LkClass { kClsSt = 0, kClsBx = 1, kClsTiled = 2, kClsLg = 3 };
+
+// One query as planned: its device descriptor and the kernels that can take it.
+struct PlannedQuery {
+    int src = 0;  // index in the caller's query array
+    psn::LkQueryDev d{};
+    bool single = false;        // single-tile kernel (window <= 1024 px, LDS plan fits)
+    int st_lds = 0;             // its LDS
+    int ow_rows = 1 << 30, ow_lds = 0;  // its one-wave mode
+    int bx_upt = 0, bx_lds = 0;  // box kernel units per thread (0: does not fit)
+    int tiled_tr = 0;           // row-tiled kernel: tile rows (0: window not LDS-resident)
+    int lg_tr = 0;              // large-window kernel: band rows
+    int cls = kClsLg, key = 0;  // the launch it goes to
+};
+
+// Row tiles of the row-tiled kernel (window LDS-resident): within the occupancy
+// budget when the window allows, else the LDS limit; 0 if it does not fit.
+static int tiled_rows(const psn_lk_ctx *c, int w, int h) {
+    if ((long)w * h > 16384) return 0;  // Iw + Dw in LDS: 6 B per window pixel
+    int tr = h;
+    const int budget = 160 * 1024 - 1024;
+    while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > c->tiled_lds) tr--;
+    while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
+    return psn::lk_lds_bytes(w, h, tr) <= budget ? tr : 0;
+}
+// Band rows of the large-window kernel within its LDS budget (>= 1 band row).
+static int lg_rows(const psn_lk_ctx *c, int w, int h) {
+    int tr = 1;
+    while (tr < h && psn::lg_lds_bytes(w, tr + 1) <= c->lg_lds) tr++;
+    return tr;
+}
+
+// Validate and plan one query.
+static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, PlannedQuery &pq) {
     const psn_lk_params &p = q.params;
     const int limit = allow_scratch ? c->nslots : c->user_slots;
     if (q.prev_slot < 0 || q.prev_slot >= limit || q.next_slot < 0 || q.next_slot >= limit)
@@ -651,34 +696,33 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
         return set_err(c, PSN_LK_ERR_SLOT, "slot never filled (%d, %d)", q.prev_slot, q.next_slot);
     if (p.win_w <= 2 || p.win_h <= 2) return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", p.win_w, p.win_h);
     if (p.max_level < 0 || q.num_pts < 0 || q.first_pt < 0) return set_err(c, PSN_LK_ERR_ARG, "bad query");
-    if ((long)p.win_w * p.win_h > PSN_LK_MAX_WIN_PIXELS)
-        return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d exceeds %d px", p.win_w, p.win_h, PSN_LK_MAX_WIN_PIXELS);
+    if (p.win_w > PSN_LK_MAX_WIN_WIDTH || (long long)p.win_w * p.win_h > (1LL << 30))
+        return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d wider than %d px", p.win_w, p.win_h, PSN_LK_MAX_WIN_WIDTH);
     const int ml = psn_lk_effective_max_level(c->width, c->height, p.win_w, p.win_h, p.max_level);
     if (ml >= c->nlevels)
         return set_err(c, PSN_LK_ERR_LEVEL_CAP, "query needs %d levels, ring holds %d", ml + 1, c->nlevels);
     int max_count = (p.term_type & PSN_LK_TERM_COUNT) ? std::min(std::max(p.max_count, 0), 100) : 30;
     double eps = (p.term_type & PSN_LK_TERM_EPS) ? std::min(std::max(p.epsilon, 0.), 10.) : 0.01;
     const int w = p.win_w, h = p.win_h;
-    const psn::LkStLayout st(w, h, (p.flags & PSN_LK_ACCUM_SCALAR) == 0, ml + 1);
-    int tr = h;
-    const int budget = 160 * 1024 - 1024;
-    if (w * h <= 256 * psn::kStEPTMax && st.total <= psn::kStMaxLds) {
-        single = true;
-        const psn::LkStLayout so(w, h, (p.flags & PSN_LK_ACCUM_SCALAR) == 0, ml + 1, true);
-        if (psn::ow_rows(w, h) <= psn::kOwMaxRows && so.total <= psn::kStMaxLds) {
-            ow_rows = psn::ow_rows(w, h);
-            ow_lds = so.total;
+    const bool sse = (p.flags & PSN_LK_ACCUM_SCALAR) == 0;
+    psn::LkQueryDev &d = pq.d;
+    d = psn::LkQueryDev{};
+    if ((long)w * h <= 256 * psn::kStEPTMax) {
+        const psn::LkStLayout st(w, h, sse, ml + 1);
+        if (st.total <= psn::kStMaxLds) {
+            pq.single = true;
+            pq.st_lds = st.total;
+            const psn::LkStLayout so(w, h, sse, ml + 1, true);
+            if (psn::ow_rows(w, h) <= psn::kOwMaxRows && so.total <= psn::kStMaxLds) {
+                pq.ow_rows = psn::ow_rows(w, h);
+                pq.ow_lds = so.total;
+            }
         }
-    } else if (psn::lk_lds_bytes(w, h, tr) > std::min(64 * 1024, c->tiled_lds)) {
-        // tile rows: within the occupancy budget when the window allows, else the LDS limit
-        while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > c->tiled_lds) tr--;
-        while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
-        if (psn::lk_lds_bytes(w, h, tr) > budget)
-            return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d does not fit LDS", w, h);
     }
+    pq.tiled_tr = tiled_rows(c, w, h);
+    pq.lg_tr = lg_rows(c, w, h);
     d.prev_slot = q.prev_slot;
     d.next_slot = q.next_slot;
-    d.wg_begin = wg_begin;
     d.pt_begin = q.first_pt;
     d.num_pts = q.num_pts;
     d.win_w = w;
@@ -686,11 +730,11 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     d.max_level = ml;
     d.max_count = max_count;
     d.flags = p.flags;
-    d.tile_rows = tr;
+    d.tile_rows = pq.single ? h : pq.tiled_tr;
     d.min_eig = (float)p.min_eig_threshold;
     d.eps2 = eps * eps;
     const int jrw = psn::st_jreg_w(w);
-    const int nc = (p.flags & PSN_LK_ACCUM_SCALAR) == 0 ? (w / 8) * 2 : 0;  // columns per SSE2 chain class
+    const int nc = sse ? (w / 8) * 2 : 0;  // columns per SSE2 chain class
     d.ow_g = std::max(psn::ow_groups(w), 1);
     d.ow_rg = (h + d.ow_g - 1) / d.ow_g;
     d.dv_w = psn::div_magic(w);
@@ -701,113 +745,114 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, int wg_begin, psn::L
     d.dv_g = psn::div_magic(d.ow_g);
     d.dv_cw = psn::div_magic(nc);
     {  // box-window kernel: units of 4 pixels, <= kBxMaxUPT per thread
-        const int need = (h * psn::bx_qw(w) + psn::kBxNT - 1) / psn::kBxNT;
+        const long need = ((long)h * psn::bx_qw(w) + psn::kBxNT - 1) / psn::kBxNT;
         const int upt = need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : 12;
-        const psn::BxLayout bl(w, h, psn::kBxMaxUPT);  // the launch may run a larger UPT
-        if (need <= psn::kBxMaxUPT && bl.total <= psn::kBxMaxLds) {
-            bx_upt = upt;
-            bx_lds = bl.total;
+        if (need <= psn::kBxMaxUPT && psn::BxLayout(w, h, upt).total <= psn::kBxMaxLds) {
+            pq.bx_upt = upt;
+            pq.bx_lds = psn::BxLayout(w, h, upt).total;
             d.bx_tre = psn::bx_err_rows(w, h, psn::BxLayout(w, h, 4).pb);
             d.dv_bxpm = psn::div_magic(psn::bx_pm(w));
             d.dv_bxjr = psn::div_magic(psn::bx_jrp(w) / 4);
         }
     }
-    lds = single ? st.total : psn::lk_lds_bytes(w, h, tr);
+    // the class: the single-tile kernel for small windows, the box kernel for
+    // Tracker2D boxes it holds in registers, else the large-window kernel (the
+    // row-tiled kernel only when a variant asks for it and the window fits it)
+    const bool forced = c->force_threads != 0;
+    if (c->force_large) {
+        pq.cls = kClsLg;
+    } else if (pq.single && !c->force_generic) {
+        pq.cls = kClsSt;
+    } else if (pq.bx_upt > 0 && c->box && !c->force_generic && !forced) {
+        pq.cls = kClsBx;
+        pq.key = 10 * pq.bx_upt + ((sse && w % 8 == 0) ? 1 : 0);
+    } else if (pq.tiled_tr > 0 && (c->force_generic || !c->box || forced)) {
+        pq.cls = kClsTiled;
+    } else {
+        pq.cls = kClsLg;
+    }
+    if (pq.cls == kClsLg) d.tile_rows = pq.lg_tr;
+    if (pq.cls == kClsTiled) d.tile_rows = pq.tiled_tr;
     return PSN_LK_OK;
 }
 
-static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
-                             uint8_t *d_status, float *d_err, bool allow_scratch, const int *d_counts = nullptr,
-                             int count_stride = 1) {
-    if (d_counts && c->pend) {  // early-exit workgroups cannot take part in a fused build
-        int rc = flush_pending(c);
-        if (rc) return rc;
+// The large-window kernel's slot buffer of the current stream, grown to `bytes`.
+static int ensure_lg_ws(psn_lk_ctx *c, size_t bytes, void **out) {
+    psn_lk_ctx::LgWs *ws = nullptr;
+    for (auto &e : c->lg_ws)
+        if (e.s == c->stream) ws = &e;
+    if (!ws) {
+        c->lg_ws.emplace_back();
+        ws = &c->lg_ws.back();
+        ws->s = c->stream;
     }
-    // slots built on the ingest stream must be complete before the LK reads them;
-    // a deferred build of a slot this call reads runs first, as its own launch
-    std::vector<int> &used = c->used_slots;  // distinct slots this call reads
-    used.clear();
-    for (int i = 0; i < nq; i++)
-        for (int sl : {q[i].prev_slot, q[i].next_slot})
-            if (std::find(used.begin(), used.end(), sl) == used.end()) used.push_back(sl);
-    for (int sl : used) {
-        if (c->pend && sl == c->pend_slot) {
-            int rc = flush_pending(c);
-            if (rc) return rc;
+    if (ws->bytes < bytes) {
+        if (ws->p) {  // earlier launches on this stream may still read the old slots
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            (void)hipFree(ws->p);
+            ws->p = nullptr;
+            ws->bytes = 0;
         }
-        int rc = wait_slot_ready(c, sl);
-        if (rc) return rc;
+        HIPCHK(c, hipMalloc(&ws->p, bytes));
+        ws->bytes = bytes;
     }
-    const bool timed = c->tcap && (c->calls_track++ % c->every) == 0;
-    const long ti = timed ? (c->n_track % c->tcap) : 0;
-    if (timed) HIPCHK(c, hipEventRecord(c->ev_track[2 * ti], c->stream));
-    for (int base = 0; base < nq; base += psn::kMaxQueries) {
-        const int n = std::min(psn::kMaxQueries, nq - base);
-        psn::LkLaunchArgs a{};
-        a.slots = c->d_slots;
-        a.ring = c->ring;
-        a.prev = d_prev;
-        a.next = d_next;
-        a.status = d_status;
-        a.err = d_err;
-        a.stamps = c->d_stamps;
-        a.samples = c->count_samples ? c->d_samples : nullptr;
-        a.counts = d_counts;
-        int wgs = 0, lds = 0, maxpx = 0, nqd = 0, rows_ow = 0, lds_ow = 0, upt_bx = 0, lds_bx = 0;
-        bool all_single = true, all_box = true;
-        bool bx_notail = true;  // every query: SSE2 order with no scalar-tail pixels (width % 8 == 0)
-        for (int i = 0; i < n; i++) {
-            const psn_lk_query &qq = q[base + i];
-            if (qq.num_pts == 0) {
-                if (qq.params.win_w <= 2 || qq.params.win_h <= 2)
-                    return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", qq.params.win_w, qq.params.win_h);
-                continue;
-            }
-            int l = 0, orows = 0, olds = 0, bupt = 0, blds = 0;
-            bool single = false;
-            int rc = plan_query(c, qq, wgs, a.q[nqd], l, single, allow_scratch, orows, olds, bupt, blds);
-            if (rc) return rc;
-            all_box &= bupt > 0;
-            bx_notail &= (qq.params.flags & PSN_LK_ACCUM_SCALAR) == 0 && qq.params.win_w % 8 == 0;
-            upt_bx = std::max(upt_bx, bupt);
-            lds_bx = std::max(lds_bx, blds);
-            a.q[nqd].qidx = (base + i) * count_stride;  // the query's count: d_counts[i * count_stride]
-            all_single &= single;
-            rows_ow = std::max(rows_ow, orows);
-            lds_ow = std::max(lds_ow, olds);
-            wgs += qq.num_pts;
-            lds = std::max(lds, l);
-            maxpx = std::max(maxpx, qq.params.win_w * qq.params.win_h);
-            nqd++;
+    *out = ws->p;
+    return PSN_LK_OK;
+}
+// HBM budget of one stream's large-window slots: one slot per point up to it,
+// beyond it the grid strides (a slot per resident workgroup at the least)
+static constexpr size_t kLgWsBudget = 512ull << 20;
+
+// One launch of a planned group (queries of one class, <= kMaxQueries).
+static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls, int key, const float *d_prev,
+                        float *d_next, uint8_t *d_status, float *d_err, const int *d_counts, int count_stride,
+                        int &fused_slot) {
+    psn::LkLaunchArgs a{};
+    a.slots = c->d_slots;
+    a.ring = c->ring;
+    a.prev = d_prev;
+    a.next = d_next;
+    a.status = d_status;
+    a.err = d_err;
+    a.stamps = c->d_stamps;
+    a.samples = c->count_samples ? c->d_samples : nullptr;
+    a.counts = d_counts;
+    int wgs = 0, maxpx = 0, rows_ow = 0, lds_ow = 0, lds = 0;
+    for (size_t i = 0; i < grp.size(); i++) {
+        PlannedQuery &pq = *grp[i];
+        a.q[i] = pq.d;
+        a.q[i].wg_begin = wgs;
+        a.q[i].qidx = pq.src * count_stride;  // the query's count: d_counts[src * count_stride]
+        wgs += pq.d.num_pts;
+        maxpx = std::max(maxpx, pq.d.win_w * pq.d.win_h);
+        rows_ow = std::max(rows_ow, pq.ow_rows);
+        lds_ow = std::max(lds_ow, pq.ow_lds);
+        lds = std::max(lds, pq.st_lds);
+    }
+    a.nq = (int)grp.size();
+    if (wgs == 0) return PSN_LK_OK;
+    const int forced = c->force_threads;
+    if (cls == kClsSt) {
+        // single-tile kernel: (workgroup size, window pixels per thread)
+        int nt = maxpx <= 128 ? 64 : maxpx <= 256 ? 128 : 256;
+        if (forced == 64 || forced == 128 || forced == 256 || forced == 512) {
+            const int max_ept = forced == 512 ? 2 : psn::kStEPTMax;
+            if (forced * max_ept >= maxpx) nt = forced;
         }
-        a.nq = nqd;
-        if (nqd == 0) continue;
-        int threads = maxpx <= 1024 ? 64 : maxpx <= 4096 ? 128 : 256;
-        const int forced = c->force_threads;
-        if (c->force_generic) all_single = false;
-        if (forced == 64 || forced == 128 || forced == 256) threads = forced;  // tiled kernel sizes
-        if (all_single) {  // single-tile kernel: (workgroup size, window pixels per thread)
-            int nt = maxpx <= 128 ? 64 : maxpx <= 256 ? 128 : 256;
-            if (forced == 64 || forced == 128 || forced == 256 || forced == 512) {
-                const int max_ept = forced == 512 ? 2 : psn::kStEPTMax;
-                if (forced * max_ept >= maxpx) nt = forced;
-            }
-            const int ept = nt == 512 ? (maxpx <= 512 ? 1 : 2) : (maxpx <= 2 * nt ? 2 : 4);
-            threads = nt * 10 + ept;
-            // one-wave iterations (wave 0 iterates, waves 1-3 stage the next level)
-            if (c->onewave && !forced && rows_ow <= psn::kOwMaxRows) {
-                const int oept = maxpx <= 512 ? 2 : 4;
-                int E = rows_ow <= 4 ? 4 : rows_ow <= 7 ? 7 : rows_ow <= 8 ? 8 : 16;
-                if (oept == 4 && E < 8) E = 8;
-                threads = 1000 * E + 2560 + oept;
-                lds = lds_ow;
-                // more points than two workgroups per CU hold, and LDS for three:
-                // the 168-VGPR variant (three per CU; one-camera launches fit at two)
-                if (oept == 2 && E <= 8 && lds_ow <= 53 * 1024 && wgs > 2 * c->num_cus) threads += 200000;
-            }
+        const int ept = nt == 512 ? (maxpx <= 512 ? 1 : 2) : (maxpx <= 2 * nt ? 2 : 4);
+        int threads = nt * 10 + ept;
+        // one-wave iterations (wave 0 iterates, waves 1-3 stage the next level)
+        if (c->onewave && !forced && rows_ow <= psn::kOwMaxRows) {
+            const int oept = maxpx <= 512 ? 2 : 4;
+            int E = rows_ow <= 4 ? 4 : rows_ow <= 7 ? 7 : rows_ow <= 8 ? 8 : 16;
+            if (oept == 4 && E < 8) E = 8;
+            threads = 1000 * E + 2560 + oept;
+            lds = lds_ow;
+            // more points than two workgroups per CU hold, and LDS for three:
+            // the 168-VGPR variant (three per CU; one-camera launches fit at two)
+            if (oept == 2 && E <= 8 && lds_ow <= 53 * 1024 && wgs > 2 * c->num_cus) threads += 200000;
         }
-        int fused_slot = -1;
-        if (c->pend && all_single) {  // fuse the deferred build into this launch's tail
+        if (c->pend && fused_slot < 0 && !d_counts) {  // fuse the deferred build into this launch's tail
             int tx, ty, plds;
             psn::pyramid_grid(c->pend_args, tx, ty, plds);
             a.pyr = c->pend_args;
@@ -823,50 +868,147 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
             lds = std::max(lds, psn::kStScratchBytes + plds);
             c->pend = false;
             fused_slot = c->pend_slot;
-        } else if (c->pend) {
+        }
+        HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, true, c->stream));
+        return PSN_LK_OK;
+    }
+    if (cls == kClsBx) {
+        const int upt = key / 10;
+        const bool notail = key % 10 != 0;
+        // the launch's UPT sizes every query's fallback planes; tiles as large as the
+        // kernel's occupancy (bx_occupancy) allows
+        int lds_bx = 0;
+        for (int i = 0; i < a.nq; i++) {
+            psn::LkQueryDev &d = a.q[i];
+            d.bx_hw = 1;
+            while (d.bx_hw < 8 && psn::BxLayout(d.win_w, d.win_h, upt, d.bx_hw + 1).total <= psn::bx_lds_target(upt))
+                d.bx_hw++;
+            lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt, d.bx_hw).total);
+        }
+        HIPCHK(c, psn::launch_lk_bx(a, wgs, upt, notail, lds_bx, c->stream));
+        return PSN_LK_OK;
+    }
+    if (cls == kClsTiled) {
+        int threads = maxpx <= 1024 ? 64 : maxpx <= 4096 ? 128 : 256;
+        if (forced == 64 || forced == 128 || forced == 256) threads = forced;
+        lds = 0;
+        for (int i = 0; i < a.nq; i++) lds = std::max(lds, psn::lk_lds_bytes(a.q[i].win_w, a.q[i].win_h, a.q[i].tile_rows));
+        HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, false, c->stream));
+        return PSN_LK_OK;
+    }
+    // large windows: one HBM slot per workgroup, the grid strides over the points
+    long long slot = 0;
+    lds = 0;
+    for (int i = 0; i < a.nq; i++) {
+        slot = std::max(slot, psn::lg_slot_int2(a.q[i].win_w, a.q[i].win_h));
+        lds = std::max(lds, psn::lg_lds_bytes(a.q[i].win_w, a.q[i].tile_rows));
+    }
+    const size_t slot_bytes = (size_t)slot * 8;
+    const long long fit = std::max<long long>((long long)(kLgWsBudget / slot_bytes), 64);
+    const int grid = (int)std::min<long long>(wgs, fit);
+    void *ws = nullptr;
+    int rc = ensure_lg_ws(c, slot_bytes * grid, &ws);
+    if (rc) return rc;
+    a.lg_ws = (int2 *)ws;
+    a.lg_slot = slot;
+    a.lk_wgs = wgs;
+    a.total_wgs = wgs;
+    HIPCHK(c, psn::launch_lk_lg(a, grid, lds, c->stream));
+    return PSN_LK_OK;
+}
+
+static int kernel_tag(int cls, int key) { return cls == kClsBx ? key : cls == kClsSt ? 1 : cls == kClsTiled ? 2 : 3; }
+
+static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const float *d_prev, float *d_next,
+                             uint8_t *d_status, float *d_err, bool allow_scratch, const int *d_counts = nullptr,
+                             int count_stride = 1) {
+    if (d_counts && c->pend) {  // early-exit workgroups cannot take part in a fused build
+        int rc = flush_pending(c);
+        if (rc) return rc;
+    }
+    // plan every query first: a bad one fails the call before anything is launched
+    std::vector<PlannedQuery> plan;
+    plan.reserve((size_t)nq);
+    for (int i = 0; i < nq; i++) {
+        if (q[i].num_pts == 0) {
+            if (q[i].params.win_w <= 2 || q[i].params.win_h <= 2)
+                return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", q[i].params.win_w, q[i].params.win_h);
+            continue;
+        }
+        plan.emplace_back();
+        plan.back().src = i;
+        int rc = plan_query(c, q[i], allow_scratch, plan.back());
+        if (rc) return rc;
+    }
+    // slots built on the ingest stream must be complete before the LK reads them;
+    // a deferred build of a slot this call reads runs first, as its own launch
+    std::vector<int> &used = c->used_slots;  // distinct slots this call reads
+    used.clear();
+    for (const PlannedQuery &pq : plan)
+        for (int sl : {pq.d.prev_slot, pq.d.next_slot})
+            if (std::find(used.begin(), used.end(), sl) == used.end()) used.push_back(sl);
+    for (int sl : used) {
+        if (c->pend && sl == c->pend_slot) {
             int rc = flush_pending(c);
             if (rc) return rc;
         }
-        if (!all_single && all_box && c->box && !c->force_generic && !forced) {
-            lds_bx = 0;  // the launch's UPT sizes every query's fallback planes; tiles as large as
-                         // the kernel's occupancy (bx_occupancy) allows
-            for (int i = 0; i < nqd; i++) {
-                psn::LkQueryDev &d = a.q[i];
-                d.bx_hw = 1;
-                while (d.bx_hw < 8 && psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw + 1).total <= psn::bx_lds_target(upt_bx))
-                    d.bx_hw++;
-                lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt_bx, d.bx_hw).total);
-            }
-            HIPCHK(c, psn::launch_lk_bx(a, wgs, upt_bx, bx_notail, lds_bx, c->stream));
-            if (timed) c->track_tag[(size_t)ti] = 10 * upt_bx + (bx_notail ? 1 : 0);
-            continue;
-        }
-        if (!all_single) {  // the generic kernel runs every query of this launch: re-plan its LDS
-            lds = 0;
-            for (int i = 0; i < nqd; i++) {
-                psn::LkQueryDev &d = a.q[i];
-                if (d.tile_rows >= d.win_h) {
-                    int tr = d.win_h;
-                    while (tr > 1 && psn::lk_lds_bytes(d.win_w, d.win_h, tr) > c->tiled_lds) tr--;
-                    while (tr > 1 && psn::lk_lds_bytes(d.win_w, d.win_h, tr) > 160 * 1024 - 1024) tr--;
-                    d.tile_rows = tr;
-                }
-                lds = std::max(lds, psn::lk_lds_bytes(d.win_w, d.win_h, d.tile_rows));
-            }
-        }
-        HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, all_single, c->stream));
-        if (timed) c->track_tag[(size_t)ti] = all_single ? 1 : 2;
-        if (fused_slot >= 0) {  // readers on other streams wait for the launch that built it
-            HIPCHK(c, hipEventRecord(c->slot_ready[fused_slot], c->stream));
-            c->ready_rec[fused_slot] = 1;
-            c->build_gen[fused_slot]++;
-            bool mine = false;  // this stream built it: ordered after the build
-            for (auto &w : c->waited[fused_slot])
-                if (w.first == c->stream) w.second = c->build_gen[fused_slot], mine = true;
-            if (!mine) c->waited[fused_slot].emplace_back(c->stream, c->build_gen[fused_slot]);
+        int rc = wait_slot_ready(c, sl);
+        if (rc) return rc;
+    }
+    // launch groups: (class, key) in a fixed order, queries in call order
+    std::vector<std::pair<int, int>> groups;
+    std::vector<long long> group_px;
+    for (const PlannedQuery &pq : plan) {
+        const std::pair<int, int> g(pq.cls, pq.key);
+        const long long px = (long long)pq.d.win_w * pq.d.win_h * pq.d.num_pts;
+        auto it = std::find(groups.begin(), groups.end(), g);
+        if (it == groups.end()) {
+            groups.push_back(g);
+            group_px.push_back(px);
+        } else {
+            group_px[it - groups.begin()] += px;
         }
     }
-    if (c->pend) {  // no launch took it (no points)
+    const bool timed = c->tcap && (c->calls_track++ % c->every) == 0;
+    const long ti = timed ? (c->n_track % c->tcap) : 0;
+    if (timed) HIPCHK(c, hipEventRecord(c->ev_track[2 * ti], c->stream));
+    int fused_slot = -1;
+    int launches = 0;
+    std::vector<PlannedQuery *> grp;
+    for (const auto &g : groups) {
+        grp.clear();
+        for (PlannedQuery &pq : plan) {
+            if (pq.cls != g.first || pq.key != g.second) continue;
+            grp.push_back(&pq);
+            if ((int)grp.size() == psn::kMaxQueries) {
+                int rc = launch_group(c, grp, g.first, g.second, d_prev, d_next, d_status, d_err, d_counts, count_stride,
+                                      fused_slot);
+                if (rc) return rc;
+                launches++;
+                grp.clear();
+            }
+        }
+        if (!grp.empty()) {
+            int rc = launch_group(c, grp, g.first, g.second, d_prev, d_next, d_status, d_err, d_counts, count_stride,
+                                  fused_slot);
+            if (rc) return rc;
+            launches++;
+        }
+    }
+    if (timed && !groups.empty()) {
+        const size_t dom = (size_t)(std::max_element(group_px.begin(), group_px.end()) - group_px.begin());
+        c->track_tag[(size_t)ti] = kernel_tag(groups[dom].first, groups[dom].second) + (groups.size() > 1 ? 1000 : 0);
+    }
+    if (fused_slot >= 0) {  // readers on other streams wait for the launch that built it
+        HIPCHK(c, hipEventRecord(c->slot_ready[fused_slot], c->stream));
+        c->ready_rec[fused_slot] = 1;
+        c->build_gen[fused_slot]++;
+        bool mine = false;  // this stream built it: ordered after the build
+        for (auto &w : c->waited[fused_slot])
+            if (w.first == c->stream) w.second = c->build_gen[fused_slot], mine = true;
+        if (!mine) c->waited[fused_slot].emplace_back(c->stream, c->build_gen[fused_slot]);
+    }
+    if (c->pend) {  // no launch took it (no single-tile launch)
         int rc = flush_pending(c);
         if (rc) return rc;
     }
@@ -874,6 +1016,7 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         HIPCHK(c, hipEventRecord(c->ev_track[2 * ti + 1], c->stream));
         c->n_track++;
     }
+    (void)launches;
     // the next build into these slots waits for this launch
     if (!used.empty()) {
         int rc = record_slots_free(c, used.data(), (int)used.size());
@@ -990,6 +1133,8 @@ int psn_lk_debug_set_variant(psn_lk_ctx *c, int key, int value) {
     case PSN_LK_VARIANT_BOX: c->box = value != 0; return PSN_LK_OK;
     case PSN_LK_VARIANT_TILED_LDS: c->tiled_lds = std::max(16 * 1024, std::min(value, 160 * 1024 - 1024)); return PSN_LK_OK;
     case PSN_LK_VARIANT_FUSED_HELPERS: c->fused_helpers = std::max(0, value); return PSN_LK_OK;
+    case PSN_LK_VARIANT_LARGE: c->force_large = value != 0; return PSN_LK_OK;
+    case PSN_LK_VARIANT_LG_LDS: c->lg_lds = std::max(4 * 1024, std::min(value, 160 * 1024 - 1024)); return PSN_LK_OK;
     default: return PSN_LK_ERR_ARG;
     }
 }

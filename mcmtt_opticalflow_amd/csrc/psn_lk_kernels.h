@@ -89,6 +89,11 @@ struct LkLaunchArgs {
     int total_wgs, lk_wgs;
     unsigned *pyr_ctr;
     PyrBuildArgs pyr;
+    // Large-window kernel (lk_kernel_lg): per-workgroup HBM slots of the window
+    // values {I*, Ix* | Iy* << 16}, lg_slot int2 apart; the grid strides over
+    // the launch's lk_wgs points
+    int2 *lg_ws;
+    long long lg_slot;
 };
 
 // LDS bytes a query needs for a given tile height (shared by host planner and kernel).
@@ -249,6 +254,18 @@ inline int bx_err_rows(int w, int h, int pb) {
     return 1;
 }
 
+// Large-window kernel (lk_kernel_lg, any window the LDS-resident kernels cannot
+// hold): window values in an HBM slot per workgroup, J read straight from the
+// pyramid, LDS only for one row band of the I patch / Scharr plane / chain
+// product planes (tr rows): reduce scratch | I patch band | Scharr band | 3 planes.
+constexpr int kLgNT = 256;
+__host__ __device__ inline int lg_off_pimg() { return kRedBytes; }
+__host__ __device__ inline int lg_off_dg(int w, int tr) { return lg_off_pimg() + lk_tile_pimg_bytes(w, tr); }
+__host__ __device__ inline int lg_off_prod(int w, int tr) { return lg_off_dg(w, tr) + lk_tile_dg_bytes(w, tr); }
+__host__ __device__ inline int lg_lds_bytes(int w, int tr) { return lg_off_prod(w, tr) + lk_tile_prod_bytes(w, tr); }
+// window-value slot of one workgroup (int2 per pixel, 256-B aligned)
+__host__ __device__ inline long long lg_slot_int2(int w, int h) { return (((long long)w * h + 31) / 32) * 32; }
+
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel
 constexpr int kStMaxLds = 150 * 1024;
 
@@ -262,6 +279,9 @@ hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_
 // notail: every query of the launch sums in the SSE2 order with width % 8 == 0
 // (no scalar-tail chain: a build without its per-pixel bookkeeping)
 hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, bool notail, int lds_bytes, hipStream_t s);
+// Large-window kernel (psn_lk_large.hip): `grid` workgroups over a.lk_wgs points.
+hipError_t launch_lk_lg(const LkLaunchArgs &a, int grid, int lds_bytes, hipStream_t s);
+hipError_t lg_kernels_init();
 hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
 
 }  // namespace psn

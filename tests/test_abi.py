@@ -23,7 +23,7 @@ def test_library_exports_every_header_symbol():
 
 
 def test_abi_version():
-    assert _lib.load().psn_lk_abi_version() == 4
+    assert _lib.load().psn_lk_abi_version() == 5
 
 
 def test_default_params_are_opencv_246_defaults():

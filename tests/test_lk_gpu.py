@@ -12,7 +12,7 @@ import pytest
 
 from mcmtt_opticalflow_amd import lk as glk
 from mcmtt_opticalflow_amd import synth
-from mcmtt_opticalflow_amd._lib import ACCUM_SCALAR, GET_MIN_EIGENVALS, USE_INITIAL_FLOW, PsnLkError
+from mcmtt_opticalflow_amd._lib import ACCUM_SCALAR, GET_MIN_EIGENVALS, MAX_WIN_WIDTH, USE_INITIAL_FLOW, PsnLkError
 
 pytestmark = pytest.mark.gpu
 
@@ -175,8 +175,8 @@ def test_lk_empty_and_errors():
         with pytest.raises(PsnLkError) as e:
             ctx.track([q], np.array([[30, 20]], np.float32))
         assert e.value.code == -5
-        q = glk.make_query(0, 1, 0, 1, glk.make_params((200, 100), 0))
-        with pytest.raises(PsnLkError) as e:
+        q = glk.make_query(0, 1, 0, 1, glk.make_params((MAX_WIN_WIDTH + 1, 100), 0))
+        with pytest.raises(PsnLkError) as e:  # wider than one LDS row band
             ctx.track([q], np.array([[30, 20]], np.float32))
         assert e.value.code == -8
 
@@ -386,3 +386,97 @@ def test_configs3_2048_points(oracle_mod, win):
     ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3)
     gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3)
     assert_same(gpu, ref, f"2048 points win {win}")
+
+
+# ------------------------------------------------------------ large windows
+
+BORDER_PTS_1080 = np.array([[3, 4], [1915.5, 1077.25], [-20, 500], [960, 1079.5], [40, 1060]], np.float32)
+
+
+@pytest.mark.parametrize("win,flags", [((100, 250), 0), ((160, 400), 0), ((200, 200), 0), ((130, 130), 0),
+                                       ((111, 277), 0), ((100, 250), ACCUM_SCALAR), ((150, 375), GET_MIN_EIGENVALS)])
+def test_lk_large_windows_1080p(oracle_mod, win, flags):
+    """Tracker2D box windows above the LDS-resident sizes (PETS-scale pedestrians
+    at 1080p: forward w x h, backward w x w) run lk_kernel_lg, bit for bit the
+    oracle -- SSE2 tails, the scalar build, min-eigenvalue output, border points."""
+    sc, f0, f1 = scene_pair(13, 1920, 1080, 24, box_w=win[0], box_h=win[1])
+    pts = np.concatenate([sc.points_at(0), BORDER_PTS_1080])
+    ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
+    assert_same(gpu, ref, f"win {win} flags {flags}")
+    assert ref[1].sum() >= 12
+
+
+def test_lk_large_window_4k_5level(oracle_mod):
+    """SURVEY 8(d)'s 4K tracker box: 128 x 320 windows, 5-level pyramid."""
+    sc, f0, f1 = scene_pair(14, 3840, 2160, 16, box_w=128, box_h=320)
+    pts = np.concatenate([sc.points_at(0), np.array([[1, 1], [3838.5, 2158.5]], np.float32)])
+    ref = oracle_ref(oracle_mod, f0, f1, pts, (128, 320), 4)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, (128, 320), 4)
+    assert_same(gpu, ref, "4k 128x320")
+
+
+@pytest.mark.parametrize("lg_lds", [0, 4096])
+@pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
+def test_lk_large_kernel_all_shapes(oracle_mod, lg_lds, flags):
+    """The large-window kernel forced for every window (variant large=1), with
+    its default row bands and with 4 KB bands (many bands per window: the
+    ordered chains continue band to band)."""
+    sc, f0, f1 = scene_pair(15, 640, 480, 40)
+    pts = np.concatenate([sc.points_at(0), np.array([[0, 0], [639.5, 479.5], [-8, 200], [320, 485]], np.float32)])
+    env = {"large": 1}
+    if lg_lds:
+        env["lg_lds"] = lg_lds
+    for win in [(21, 21), (3, 3), (9, 15), (33, 33), (64, 64), (45, 120), (37, 50), (100, 60)]:
+        ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
+        gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags, variants=env)
+        assert_same(gpu, ref, f"{env} {win}")
+
+
+def test_lk_large_err_sequential_path(oracle_mod):
+    """Uncorrelated frames and a 160 x 160 window: sum|diff| > 2^24, so err takes
+    the ordered chain of the large-window kernel; b and A chains as well."""
+    rng = np.random.default_rng(19)
+    f0 = rng.integers(0, 256, (480, 480), dtype=np.uint8)
+    f1 = rng.integers(0, 256, (480, 480), dtype=np.uint8)
+    pts = rng.uniform(100, 380, (12, 2)).astype(np.float32)
+    ref = oracle_ref(oracle_mod, f0, f1, pts, (160, 160), 1, criteria=(1, 2, 0.0))
+    assert np.any(ref[2] * 32 * 160 * 160 > 2 ** 24)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, (160, 160), 1, criteria=(1, 2, 0.0))
+    assert_same(gpu, ref, "large err chain")
+
+
+def test_lk_mixed_window_classes_one_call(oracle_mod):
+    """One track call whose queries need four kernel classes (single-tile 21x21,
+    box kernel no-tail 64x64 and tail 45x120, large 100x250 and 130x130): each
+    class is its own launch; every query matches the oracle, also counted."""
+    import hiprt
+
+    W, H = 1920, 1080
+    sc = synth.make_scene(16, W, H, 240)
+    f0, f1 = sc.frame(0), sc.frame(1)
+    pts = sc.points_at(0)
+    specs = [(0, 40, (100, 250)), (40, 40, (21, 21)), (80, 40, (64, 64)), (120, 40, (45, 120)),
+             (160, 40, (130, 130)), (200, 40, (21, 21))]
+    with glk.LKContext(W, H, ring_slots=2, max_level_cap=3) as ctx:
+        ctx.push_frame(0, f0)
+        ctx.push_frame(1, f1)
+        qs = [glk.make_query(0, 1, first, n, glk.make_params(win, 3)) for first, n, win in specs]
+        gn, gs, ge = ctx.track(qs, pts)
+        counts = np.array([40, 0, 17, 40, 5, 40], np.int32)
+        d_p = hiprt.DeviceBuffer.from_array(pts)
+        sentinel = np.full(pts.shape, -7.0, np.float32)
+        d_n = hiprt.DeviceBuffer.from_array(sentinel)
+        d_s, d_e = hiprt.DeviceBuffer.from_array(np.full(len(pts), 9, np.uint8)), hiprt.DeviceBuffer(4 * len(pts))
+        d_c = hiprt.DeviceBuffer.from_array(counts)
+        ctx.track_device_counted(qs, d_c.addr, d_p.addr, d_n.addr, d_s.addr, d_e.addr)
+        ctx.sync()
+        cn, cs_ = d_n.to_array(pts.shape, np.float32), d_s.to_array(len(pts), np.uint8)
+        ce = d_e.to_array(len(pts), np.float32)
+    for (first, n, win), c in zip(specs, counts):
+        sl = slice(first, first + n)
+        ref = oracle_ref(oracle_mod, f0, f1, pts[sl], win, 3)
+        assert_same((gn[sl], gs[sl], ge[sl]), ref, f"query {win}")
+        assert_same((cn[first:first + c], cs_[first:first + c], ce[first:first + c]),
+                    tuple(r[:c] if r is not None else None for r in ref), f"counted {win}")
+        np.testing.assert_array_equal(cn[first + c:first + n], sentinel[first + c:first + n])

@@ -234,3 +234,45 @@ def test_group_failed_frame_after_regrow_matches_oracle(oracle_mod):
             objs, _, r_res = ref.run(*args)
             _check_result(g_res, r_res, f"frame {t}")
             assert len([d for d in g_out if d.valid]) == len(objs), f"frame {t}"
+
+
+@pytest.mark.parametrize("gridfast", [False, True])
+def test_group_large_boxes_match_oracle(oracle_mod, gridfast):
+    """PETS-scale boxes at 1280x720: forward windows 100x250 and 140x300 and the
+    140x140 backward window run the large-window kernel, 100x100 the box
+    kernel, in the same group launches -- bit for bit the reference schedule."""
+    W, H, T = 1280, 720, 5
+    sizes = [(100, 250), (140, 300)]
+    C = len(sizes)
+    scenes = [synth.make_scene(60 + c, W, H, 120, nboxes=2, box_w=bw, box_h=bh, max_speed=3.0)
+              for c, (bw, bh) in enumerate(sizes)]
+    refs = [ORC.CameraTracker(cam_id=c) for c in range(C)]
+    rngs = [np.random.default_rng(700 + c) for c in range(C)]
+    grays = [[sc.frame(t) for t in range(T)] for sc in scenes]
+    per_frame = [[_camera_dets(scenes[c], t, rngs[c]) for c in range(C)] for t in range(T)]
+    n_obj = 0
+    with t2d.Group(W, H, list(range(C))) as g:
+        for t in range(T):
+            for c in range(C):
+                g.push_frame(c, grays[c][t])
+            frames = [[t2d.make_detection(b, np.zeros((0, 2), np.float32) if gridfast else f, head=e[0],
+                                          location=e[1], height=e[2]) for b, e, f in zip(*per_frame[t][c])]
+                      for c in range(C)]
+            out = g.run(t, frames, gridfast=gridfast, seed=t)
+            for c in range(C):
+                boxes, extra, feats = per_frame[t][c]
+                if gridfast:
+                    feats, _ = oracle_mod.gridfast_detect(grays[c][t], _rois(boxes, W, H), seed=t)
+                objs, _, r_res = refs[c].run(grays[c][t], [ORC.Rect(*b) for b in boxes], feats, t,
+                                             [(ORC.Rect(*e[0]), e[1], e[2]) for e in extra])
+                what = f"frame {t} camera {c}"
+                g_out, g_res = out[c]
+                valid = [d for d in g_out if d.valid]
+                assert len(valid) == len(objs), what
+                for d, o in zip(valid, objs):
+                    assert [d.boxes[i].tuple() for i in range(d.num_boxes)] == [b.tuple() for b in o.boxes], what
+                    for k in range(d.num_sets):
+                        np.testing.assert_array_equal(t2d.points(d.sets[k], d.set_count[k]), o.sets[k], err_msg=what)
+                _check_result(g_res, r_res, what)
+                n_obj += len(g_res["objects"])
+    assert n_obj >= 6
