@@ -369,6 +369,10 @@ struct Parsed {
     psn::JpegArgs a{};
     std::vector<int> seg;
     size_t ent0 = 0, ent1 = 0;  // entropy bytes [ent0, ent1) of the file
+    // per Huffman slot (class tc, index th): 0 never defined, 1 valid, -1 the last
+    // definition is one jpeg_make_d_derived_tbl rejects -- an error only for a table
+    // the scan uses (libjpeg builds the derived tables of the scan's components)
+    int hstate[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 };
 
 int parse(const uint8_t *d, size_t n, Parsed &P, std::string &why) {
@@ -403,8 +407,7 @@ int parse(const uint8_t *d, size_t n, Parsed &P, std::string &why) {
                 int cnt = 0;
                 for (int l = 0; l < 16; l++) cnt += s[o + 1 + l];
                 if (cnt > 256 || o + 17 + cnt > sl) return why = "bad DHT", PSN_LK_ERR_ARG;
-                if (!psn::build_huff(s + o + 1, s + o + 17, cnt, tc == 0, tc ? P.tab.ac[th] : P.tab.dc[th]))
-                    return why = "bad DHT (code lengths or DC symbols)", PSN_LK_ERR_ARG;
+                P.hstate[tc][th] = psn::build_huff(s + o + 1, s + o + 17, cnt, tc == 0, tc ? P.tab.ac[th] : P.tab.dc[th]) ? 1 : -1;
                 o += 17 + cnt;
             }
         } else if (m == 0xC0 || m == 0xC1) {
@@ -435,6 +438,14 @@ int parse(const uint8_t *d, size_t n, Parsed &P, std::string &why) {
                         P.a.c[c].td = (s[2 + 2 * i] >> 4) & 3;
                         P.a.c[c].ta = s[2 + 2 * i] & 3;
                     }
+            // the scan's tables (jdhuff.c start_pass_huff_decoder -> jpeg_make_d_derived_tbl:
+            // JERR_NO_HUFF_TABLE, JERR_BAD_HUFF_TABLE)
+            for (int c = 0; c < P.a.nc; c++)
+                for (int tc = 0; tc < 2; tc++) {
+                    const int st = P.hstate[tc][tc ? P.a.c[c].ta : P.a.c[c].td];
+                    if (st == 0) return why = "Huffman table not defined", PSN_LK_ERR_ARG;
+                    if (st < 0) return why = "bad DHT (code lengths or DC symbols)", PSN_LK_ERR_ARG;
+                }
             P.ent0 = p + 2 + (size_t)len;
             break;
         }

@@ -523,6 +523,13 @@ static int wait_slot_free(psn_lk_ctx *c, int slot, hipStream_t s) {
     return PSN_LK_OK;
 }
 
+// Make stream s wait for the slot's last recorded build (it may run on another
+// ingest stream and still read the slot's staging buffer or write its pyramid).
+static int wait_prev_build(psn_lk_ctx *c, int slot, hipStream_t s) {
+    if (c->ready_rec[slot]) HIPCHK(c, hipStreamWaitEvent(s, c->slot_ready[slot], 0));
+    return PSN_LK_OK;
+}
+
 // Pyramid-build arguments of `slot` from a device source frame.
 static psn::PyrBuildArgs build_args(const psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
     psn::PyrBuildArgs a{};
@@ -550,6 +557,8 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
     hipStream_t s = c->stream;
     if (c->overlap == PSN_LK_OVERLAP_STREAM) s = c->ingest_stream;  // once the slot's last readers are done
     rc = wait_slot_free(c, slot, s);
+    if (rc) return rc;
+    rc = wait_prev_build(c, slot, s);
     if (rc) return rc;
     return launch_build(c, a, s, slot);
 }
@@ -583,6 +592,9 @@ int psn_lk_push_frame_jpeg(psn_lk_ctx *c, int slot, const uint8_t *jpeg, size_t 
     const size_t row = (size_t)c->width * 3;
     if ((rc = ensure_stage(c, slot, row * c->height))) return rc;
     if ((rc = wait_slot_free(c, slot, c->ingest_stream))) return rc;
+    // the slot's previous build may still read d_stage[slot] (an async push builds
+    // on either ingest stream): the decode overwrites it only after that build
+    if ((rc = wait_prev_build(c, slot, c->ingest_stream))) return rc;
     rc = psn_jpeg_decode_device(c->jpeg, jpeg, len, c->d_stage[slot], (int)row);
     if (rc) return set_err(c, rc, "JPEG decode: %s", psn_jpeg_last_error(c->jpeg));
     c->filled[slot] = 1;

@@ -2357,9 +2357,11 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
     int *X = (int *)smem;                      // chain-check records, two parities
     float *RS = (float *)(X + kBxXInts);       // serial-chain results (wave 0 -> all)
     int *EP = (int *)(RS + 16);                // err partial sums per wave
-    // b-fallback tile hand-off flags (PSN_BX_FLAGS): ready[3], consumed[3]
+    // b-fallback tile hand-off flags (PSN_BX_FLAGS): ready[3], consumed[3], and
+    // FLG[6] = a hand-off wait ran out of its bound (never expected: the point is
+    // then reported failed, see the result writes)
     volatile int *FLG = (volatile int *)(RS + 24);
-    if (threadIdx.x < 6) FLG[threadIdx.x] = -1;  // ordered by the first level barrier
+    if (threadIdx.x < 7) FLG[threadIdx.x] = threadIdx.x < 6 ? -1 : 0;  // ordered by the first level barrier
     int fb_epoch = 0;
     uint8_t *JR = smem + lay.jr;
     const uint32_t *JR32 = (const uint32_t *)JR;
@@ -3084,10 +3086,12 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     const int ep = ++fb_epoch, wv = ftid >> 6, fl = ftid & 63;
                     auto tag = [&](int g) { return ep * 16 + g; };
                     auto spin = [&](int idx, int want) {
-                        for (int n = 0; n < (1 << 22); n++) {  // (a bound: never a hang)
+                        int n = 0;
+                        for (; n < (1 << 22); n++) {  // (a bound: never a hang)
                             if (__builtin_amdgcn_readfirstlane(FLG[idx]) == want) break;
                             __builtin_amdgcn_s_sleep(1);
                         }
+                        if (n == (1 << 22)) FLG[6] = 1;  // the tile may be half written: fail the point
                         asm volatile("" ::: "memory");
                     };
                     for (int g = max(h0, 2 * wv); g <= min(2 * wv + 1, g_last); g++) {
@@ -3290,6 +3294,10 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
     }
 #endif
     if (tid == 0) {
+        if (FLG[6]) {  // a fallback hand-off timed out: the sums may be wrong -- say so
+            NPx = NPy = errv = __builtin_nanf("");
+            status = 0;
+        }
         A.next[2 * pi] = NPx;
         A.next[2 * pi + 1] = NPy;
         A.status[pi] = (uint8_t)status;

@@ -338,7 +338,11 @@ void Tracker2DFlow::SyncForward() {
 
 void Tracker2DFlow::Finalize() {
     if (dev_) {
+        // every stream that may still use the device buffers: the LK context's,
+        // both chain streams (a frame launched ahead runs on the other one) and
+        // both forward streams
         if (lk_) psn_lk_sync(lk_);
+        SyncChains();
         SyncForward();
         dev_->release();
         delete dev_;

@@ -185,8 +185,8 @@ class Munkres {
 };
 }  // namespace
 
-// CPSNWhere_Hungarian Initialize(float*, rows, cols) + Match()
-// (helpers/PSNWhere_Hungarian.cpp:124-155, :212-359): infinity pre-processing
+// CPSNWhere_Hungarian Initialize(std::vector<float>, rows, cols) + Match()
+// (helpers/PSNWhere_Hungarian.cpp:67-89, :212-359; called at PSNWhere_Tracker2D.cpp:1059): infinity pre-processing
 // (:711-735), condensed matrix padded by the minimum line cover of its finite
 // entries (:241-289), Munkres, then the starred pairs of the first rows x cols
 // entries whose cost is finite after the post-processing (:737-747, :339-354).

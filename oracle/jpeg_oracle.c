@@ -316,18 +316,20 @@ int oracle_jpeg_decode_bgr(const uint8_t *d, size_t n, uint8_t *out, int out_str
                     cnt += s[o + l];
                 }
                 if (cnt > 256) return -2;
-                /* jpeg_make_d_derived_tbl's JERR_BAD_HUFF_TABLE: code overflow, DC symbol > 15 */
+                /* jpeg_make_d_derived_tbl's JERR_BAD_HUFF_TABLE (code overflow, DC symbol
+                 * > 15) is raised when a scan uses the table: remember it (defined = -1) */
+                int bad = 0;
                 for (int l = 1, code = 0; l <= 16; l++) {
                     code += hh->bits[l];
-                    if (code >= (1 << l)) return -2;
+                    if (code >= (1 << l)) bad = 1;
                     code <<= 1;
                 }
                 for (int i = 0; i < cnt; i++)
-                    if (tc == 0 && s[o + 17 + i] > 15) return -2;
+                    if (tc == 0 && s[o + 17 + i] > 15) bad = 1;
                 for (int i = 0; i < cnt && i < 256; i++) hh->vals[i] = s[o + 17 + i];
                 hh->nvals = cnt;
-                hh->defined = 1;
-                huff_build(hh);
+                hh->defined = bad ? -1 : 1;
+                if (!bad) huff_build(hh);
                 o += 17 + cnt;
             }
         } else if (m == 0xC0 || m == 0xC1) {  /* SOF0 / SOF1 (8-bit Huffman sequential) */
@@ -357,6 +359,9 @@ int oracle_jpeg_decode_bgr(const uint8_t *d, size_t n, uint8_t *out, int out_str
                         cp[c].ta = s[2 + 2 * i] & 15;
                     }
             }
+            /* the scan's tables: JERR_NO_HUFF_TABLE / JERR_BAD_HUFF_TABLE */
+            for (int c = 0; c < nc; c++)
+                if (hdc[cp[c].td & 3].defined != 1 || hac[cp[c].ta & 3].defined != 1) return -2;
             p += 2 + (size_t)len;
             rc = 0;
             break;

@@ -3,7 +3,7 @@
 Plain-Python restatement of the reference's Hungarian matcher,
 CPSNWhere_Hungarian (psn_where/helpers/PSNWhere_Hungarian.cpp), as
 Track2D_MatchingAndUpdating drives it (psn_where/PSNWhere_Tracker2D.cpp
-:1040-1064): Initialize (:124-155) + Match (:212-359) with its infinity
+:1040-1064): Initialize (the std::vector<float> overload Tracker2D calls, :67-89, from PSNWhere_Tracker2D.cpp:1059) + Match (:212-359) with its infinity
 pre/post-processing (:711-747), the minimum line cover that sizes the padding
 (:677-709) and Munkres steps 1-6 (:405-675). Every cost operation is float32
 as in the reference (numpy float32 scalars/arrays, IEEE single rounding per
@@ -120,7 +120,7 @@ def _min_line_cover(E):
 
 
 def hungarian_match(cost):
-    """CPSNWhere_Hungarian Initialize(float*, rows, cols) + Match() -> (rows, cols,
+    """CPSNWhere_Hungarian Initialize(std::vector<float>, rows, cols) (:67-89) + Match() -> (rows, cols,
     match costs) of the matched pairs in row-major order, as stMatchInfo holds them.
     An empty matrix, or one holding a NaN (:78-81), matches nothing."""
     C = np.array(cost, np.float32, copy=True)

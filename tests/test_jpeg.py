@@ -71,36 +71,48 @@ def test_jpeg_info_and_rejects():
         lk.JpegDecoder.info(prog)
 
 
-def _with_dht(data: bytes, tc_th: int, bits, vals) -> bytes:
-    """data with one more DHT segment right after SOI (parsed before the file's own)."""
+def _with_dht(data: bytes, tc_th: int, bits, vals, before_sos: bool = False) -> bytes:
+    """data with one more DHT segment: right after SOI (parsed before the file's
+    own tables, which redefine its slot) or right before SOS (after them: the
+    scan uses it)."""
     body = bytes([tc_th]) + bytes(bits) + bytes(vals)
     seg = b"\xff\xc4" + (len(body) + 2).to_bytes(2, "big") + body
-    return data[:2] + seg + data[2:]
+    at = data.find(b"\xff\xda") if before_sos else 2
+    return data[:at] + seg + data[at:]
 
 
-@pytest.mark.parametrize("case", ["two_1bit_codes", "overfull_1bit", "all_ones_3bit", "dc_symbol_200", "ac_overflow"])
+_BAD_TABLES = {
+    "two_1bit_codes": (0x00, [2] + [0] * 15, [0, 1]),
+    "overfull_1bit": (0x00, [200] + [0] * 15, [0] * 200),  # the advisor's bits[0] = 200
+    "all_ones_3bit": (0x10, [0, 0, 8] + [0] * 13, list(range(8))),
+    "dc_symbol_200": (0x01, [0, 1] + [0] * 14, [200]),
+    "ac_overflow": (0x11, [0, 3, 3] + [0] * 13, [1, 2, 3, 4, 5, 6]),
+}
+
+
+@pytest.mark.parametrize("case", sorted(_BAD_TABLES))
 def test_jpeg_rejects_bad_huffman_tables(oracle_mod, case):
     """jdhuff.c jpeg_make_d_derived_tbl's JERR_BAD_HUFF_TABLE cases: a canonical
     code that overflows its length (would index past the 9-bit lookahead table),
-    and DC symbols above 15 (shifts of >= 16 bits in extend). Both the device
-    decoder's parser and the oracle refuse them (PSN_LK_ERR_ARG)."""
+    and DC symbols above 15 (shifts of >= 16 bits in extend). libjpeg checks the
+    tables a scan uses, when the scan starts: a bad table the scan uses is
+    refused by the device decoder's parser and the oracle (PSN_LK_ERR_ARG); the
+    same table redefined by the file's own DHT before the scan, or put in a slot
+    no component uses, is accepted and the frame decodes as before."""
     from mcmtt_opticalflow_amd import lk
 
-    _, data, _ = fixtures()[0]
-    z = [0] * 16
-    bad = {
-        "two_1bit_codes": (0x00, [2] + z[1:], [0, 1]),
-        "overfull_1bit": (0x00, [200] + z[1:], [0] * 200),  # the advisor's bits[0] = 200
-        "all_ones_3bit": (0x10, [0, 0, 8] + z[3:], list(range(8))),
-        "dc_symbol_200": (0x01, [0, 1] + z[2:], [200]),
-        "ac_overflow": (0x11, [0, 3, 3] + z[3:], [1, 2, 3, 4, 5, 6]),
-    }[case]
-    crafted = _with_dht(data, *bad)
+    _, data, bgr = fixtures()[0]
+    tc_th, bits, vals = _BAD_TABLES[case]
+    used = _with_dht(data, tc_th, bits, vals, before_sos=True)
     with pytest.raises(lk.PsnLkError) as e:
-        lk.JpegDecoder.info(crafted)
+        lk.JpegDecoder.info(used)
     assert e.value.code == -1  # PSN_LK_ERR_ARG
     with pytest.raises(ValueError):
-        oracle_mod.jpeg_decode_bgr(crafted)
+        oracle_mod.jpeg_decode_bgr(used)
+    for ok in (_with_dht(data, tc_th, bits, vals),  # redefined by the file's own table
+               _with_dht(data, (tc_th & 0xF0) | 3, bits, vals, before_sos=True)):  # slot 3: unused
+        assert lk.JpegDecoder.info(ok)[:2] == lk.JpegDecoder.info(data)[:2]
+        np.testing.assert_array_equal(oracle_mod.jpeg_decode_bgr(ok), bgr)
     # a valid extra table (the JPEG standard's luminance DC table) is accepted
     ok = _with_dht(data, 0x03, [0, 1, 5, 1, 1, 1, 1, 1, 1] + [0] * 7, list(range(12)))
     assert lk.JpegDecoder.info(ok)[:2] == lk.JpegDecoder.info(data)[:2]
