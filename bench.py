@@ -40,8 +40,12 @@ Modes and legs:
   --mode config4      BASELINE.json configs[4]: 8 cameras sharded over the
                       ranks, 3840x2160, 4096 points/camera, 21x21, 5 levels,
                       SG(9, 1) post-filter of every point's trajectory.
+  --box-dist pets     per-detection box sizes from a seeded PETS-like
+                      distribution (synth.pets_box_sizes): windows of every
+                      kernel class in one frame.
   At N = 1 the default line also carries `legs`: configs[3] on one GPU,
-  configs[4] on one GPU and the GridFAST Run (--no-legs skips them).
+  configs[4] on one GPU, the GridFAST Run and the PETS-like mixed-box Run
+  (--no-legs skips them).
 
 Multi-GPU: `python bench.py --gpus N` starts N ranks itself (one process per
 GPU, RANK/LOCAL_RANK/WORLD_SIZE set before anything touches a GPU); under
@@ -230,7 +234,7 @@ class CameraFeed:
         from mcmtt_opticalflow_amd import synth
 
         W, H = args.width, args.height
-        self.scene = synth.make_scene(cam, W, H, args.points, nboxes=args.boxes)
+        self.scene = synth.make_scene(cam, W, H, args.points, nboxes=args.boxes, box_dist=args.box_dist)
         self.period = args.period
         self.gridfast = args.features == "gridfast"
         self.jpeg = None
@@ -278,7 +282,8 @@ class CameraFeed:
 
 
 def detection_boxes(scene, f):
-    return [(float(int(x)), float(int(y)), float(scene.box_w), float(scene.box_h)) for x, y in scene.box_at(f)]
+    return [(float(int(x)), float(int(y)), float(scene.box_ws[k]), float(scene.box_hs[k]))
+            for k, (x, y) in enumerate(scene.box_at(f))]
 
 
 def detection_extra(b):
@@ -433,7 +438,9 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     group.close()
     if exch:
         exch.close()
+    box_sizes = [[[int(fd.scene.box_ws[k]), int(fd.scene.box_hs[k])] for k in range(args.boxes)] for fd in feeds]
     return {"elapsed": elapsed, "steps": steps, "warmup": warmup, "cams_per_rank": C, "world": world,
+            "box_sizes": box_sizes,
             "measure_steps": measure,
             "per_kernel": per_kernel, "ts": ts, "samples": samples, "objs_last": objs_last,
             "points_per_camera": pts_last, "recorded": recorded, "slot_bytes": slot_bytes, "max_obj": max_obj}
@@ -457,7 +464,7 @@ def verify_tracker(args, r):
     W, H = args.width, args.height
     mism, checked, objects, first = 0, 0, 0, None
     for cam in range(ncam):
-        sc = synth.make_scene(cam, W, H, args.points, nboxes=args.boxes)
+        sc = synth.make_scene(cam, W, H, args.points, nboxes=args.boxes, box_dist=args.box_dist)
         ref = T2.CameraTracker(cam_id=cam)
         jpeg = {}
         for t in range(frames):
@@ -519,7 +526,7 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
     from mcmtt_opticalflow_amd import synth
 
     W, H, C = args.width, args.height, args.cameras
-    scenes = [synth.make_scene(c, W, H, args.points, nboxes=args.boxes) for c in range(C)]
+    scenes = [synth.make_scene(c, W, H, args.points, nboxes=args.boxes, box_dist=args.box_dist) for c in range(C)]
     grays = [[oracle.bgr2gray(synth.to_bgr(sc.frame(t))) for t in range(args.period)] for sc in scenes]
 
     def leg(threads, shared, budget, ncams=C):
@@ -670,23 +677,28 @@ def tracker_line(args, r, world, C, scaling, profile):
     what = ("BASELINE.json configs[3]" if cfg3 else "BASELINE.json configs[2] per GPU"
             if (args.width, args.height, args.cameras, args.points, args.boxes) == (1920, 1080, 4, 512, 8)
             and not args.total_cameras else "Tracker2D Run")
+    pets = args.box_dist == "pets"
+    box_txt = ("PETS-like boxes, synth.pets_box_sizes" if pets else "64x160 boxes")
+    win_txt = ("box-derived windows (backward w x w, forward w x h, mixed kernel classes)" if pets else
+               "64x64 windows")
     out = {
         "metric": METRIC, "value": round(fps_all, 2), "unit": "frames/s", "n_gpus": world, "steps": r["steps"],
         "warmup": r["warmup"], "ms_per_step": round(1e3 * r["elapsed"] / r["steps"], 5), "higher_is_better": True,
         "scaling": scaling, "vs_baseline": None, "dtype": "u8+f32", "data": "synthetic",
         "config": {
             "workload": (f"{what}: {world * C} cameras ({C} per GPU) x {args.width}x{args.height} "
-                         f"{'JPEG' if args.ingest == 'jpeg' else 'BGR'}, {args.boxes} detections/camera (64x160 "
-                         f"boxes) x " + ("GridFAST features (<= 100 each)" if args.features == "gridfast" else
-                                         f"{args.points // args.boxes} points = {args.points} tracked points/camera")
-                         + ", CPSNWhere_Tracker2D::Run: async H2D ingest + BGR->gray + pyramid, 3-step backward "
-                         "chains (64x64 windows, LocalSearchKLT on device), forward LK (64x160) + matching cost, "
+                         f"{'JPEG' if args.ingest == 'jpeg' else 'BGR'}, {args.boxes} detections/camera ({box_txt}"
+                         f") x " + ("GridFAST features (<= 100 each)" if args.features == "gridfast" else
+                                    f"{args.points // args.boxes} points = {args.points} tracked points/camera")
+                         + f", CPSNWhere_Tracker2D::Run: async H2D ingest + BGR->gray + pyramid, 3-step backward "
+                         f"chains ({win_txt}, LocalSearchKLT on device), forward LK + matching cost, "
                          "Munkres + tracker update + ResultWithTracker, packed result slots in host memory"
                          + (", RCCL all-gather of the slots (psn_comm)" if world > 1 else "")),
             "cameras": world * C, "cameras_per_gpu": C, "width": args.width, "height": args.height,
             "points_per_camera": args.points if args.features == "given" else round(r["points_per_camera"], 1),
-            "features": args.features, "detections_per_camera": args.boxes, "box": [64, 160], "levels": 4,
-            "win_backward": [64, 64], "win_forward": [64, 160],
+            "features": args.features, "detections_per_camera": args.boxes, "levels": 4,
+            **({"box_dist": "pets", "boxes_per_camera": r.get("box_sizes")} if pets else
+               {"box": [64, 160], "win_backward": [64, 64], "win_forward": [64, 160]}),
             "ingest": ("baseline JPEG files in host memory (q90 4:2:0, restart per MCU row), decoded on the device"
                        if args.ingest == "jpeg" else "BGR frames in pinned host memory"),
             "parallelism": f"camera-sharded x{world} ({C} cameras per GPU), RCCL all-gather of result slots"},
@@ -756,6 +768,11 @@ def tracker_legs(args, profile):
     rg = tracker_run(ag, steps=args.leg_steps, warmup=3)
     lg = tracker_line(ag, rg, 1, args.cameras, "weak", None)
     legs["gridfast"] = {k: lg[k] for k in ("value", "unit", "ms_per_step", "steps", "config")}
+    am = argparse.Namespace(**{**vars(args), "box_dist": "pets", "verify": False})
+    rm = tracker_run(am, steps=args.leg_steps, warmup=3)
+    lm = tracker_line(am, rm, 1, args.cameras, "weak", None)
+    legs["mixed_boxes"] = {k: lm[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
+    legs["mixed_boxes"]["lk_launches"] = {k: lm["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
     legs["config4"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3)["line"]
     return legs
 
@@ -1018,6 +1035,9 @@ def parse_args(argv=None):
     ap.add_argument("--boxes", type=int, default=8, help="tracker mode: detections per camera")
     ap.add_argument("--features", choices=["given", "gridfast"], default="given",
                     help="tracker mode: points given (SURVEY 8(d) recipe) or GridFAST on the device")
+    ap.add_argument("--box-dist", choices=["uniform", "pets"], default="uniform",
+                    help="tracker mode: every detection 64x160 (SURVEY 8(d), default) or per-detection sizes from "
+                         "a seeded PETS-like distribution scaled to the frame (synth.pets_box_sizes)")
     ap.add_argument("--ingest", choices=["bgr", "jpeg"], default="bgr",
                     help="tracker mode: frames arrive as BGR arrays (default) or as JPEG files (device decode)")
     ap.add_argument("--verify", action="store_true", help="check every frame's results against the oracle")

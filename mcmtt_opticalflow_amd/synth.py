@@ -49,7 +49,7 @@ class CameraScene:
     cam: int
     width: int
     height: int
-    box_w: int
+    box_w: int              # uniform box size (the largest box under a size distribution)
     box_h: int
     boxes0: np.ndarray      # (K, 2) top-left at t=0
     vel: np.ndarray         # (K, 2) px/frame
@@ -57,6 +57,18 @@ class CameraScene:
     pt_box: np.ndarray      # (N,) box index of each point
     bg: np.ndarray          # (H, W) float64 background intensity (before clamp)
     box_params: list
+    box_ws: np.ndarray = None  # (K,) per-box width / height (int)
+    box_hs: np.ndarray = None
+
+    def __post_init__(self):
+        k = len(self.boxes0)
+        if self.box_ws is None:
+            self.box_ws = np.full(k, self.box_w, np.int64)
+        if self.box_hs is None:
+            self.box_hs = np.full(k, self.box_h, np.int64)
+
+    def box_size(self, k: int) -> tuple[int, int]:
+        return int(self.box_ws[k]), int(self.box_hs[k])
 
     def box_at(self, t: float) -> np.ndarray:
         return self.boxes0 + self.vel * t
@@ -69,8 +81,9 @@ class CameraScene:
         ys = np.arange(self.height, dtype=np.float64)
         xs = np.arange(self.width, dtype=np.float64)
         for k, (bx, by) in enumerate(self.box_at(t)):
-            x0, x1 = int(np.ceil(bx)), int(np.ceil(bx + self.box_w))
-            y0, y1 = int(np.ceil(by)), int(np.ceil(by + self.box_h))
+            bw, bh = self.box_size(k)
+            x0, x1 = int(np.ceil(bx)), int(np.ceil(bx + bw))
+            y0, y1 = int(np.ceil(by)), int(np.ceil(by + bh))
             x0, y0 = max(x0, 0), max(y0, 0)
             x1, y1 = min(x1, self.width), min(y1, self.height)
             if x1 <= x0 or y1 <= y0:
@@ -79,31 +92,51 @@ class CameraScene:
         return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
 
+def pets_box_sizes(cam: int, nboxes: int, height: int) -> tuple[np.ndarray, np.ndarray]:
+    """Seeded PETS2009-like pedestrian boxes (seed 4000+cam): heights U[0.14,
+    0.35] of the frame height (150..375 px at 1080p; PETS S2.L1 people span
+    roughly 80..200 of its 576 rows), width/height U[0.35, 0.45] -- widths of
+    any residue mod 8, as real detections have."""
+    rng = np.random.default_rng(4000 + cam)
+    hs = np.floor(rng.uniform(0.14, 0.35, nboxes) * height).astype(np.int64)
+    ws = np.floor(hs * rng.uniform(0.35, 0.45, nboxes)).astype(np.int64)
+    return np.maximum(ws, 8), np.maximum(hs, 8)
+
+
 def make_scene(cam: int, width: int, height: int, npts: int, nboxes: int | None = None,
-               box_w: int | None = None, box_h: int | None = None, max_speed: float = 4.0) -> CameraScene:
-    """Box sizes per BASELINE.md: 32x80 at 640x480, 64x160 at 1080p, 128x320 at 4K."""
+               box_w: int | None = None, box_h: int | None = None, max_speed: float = 4.0,
+               box_dist: str = "uniform") -> CameraScene:
+    """Box sizes per BASELINE.md: 32x80 at 640x480, 64x160 at 1080p, 128x320 at 4K
+    (box_dist "uniform"), or per box from pets_box_sizes (box_dist "pets")."""
     if box_w is None:
         box_w = 32 if width <= 640 else 64 if width <= 1920 else 128
     if box_h is None:
         box_h = int(box_w * 2.5)
     if nboxes is None:
         nboxes = max(1, min(16, npts // 32))
+    if box_dist == "pets":
+        bws, bhs = pets_box_sizes(cam, nboxes, height)
+        box_w, box_h = int(bws.max()), int(bhs.max())
+    elif box_dist == "uniform":
+        bws, bhs = np.full(nboxes, box_w, np.int64), np.full(nboxes, box_h, np.int64)
+    else:
+        raise ValueError(f"box_dist {box_dist!r}")
     bgp = _texture_params(1000 + cam)
     xs = np.arange(width, dtype=np.float64)
     ys = np.arange(height, dtype=np.float64)
     bg = 128.0 + _render(bgp, xs, ys)
     rng = np.random.default_rng(2000 + cam)
-    mx = min(8 * max_speed + 8, max(0.0, (width - box_w) / 2 - 1))
-    my = min(8 * max_speed + 8, max(0.0, (height - box_h) / 2 - 1))
-    boxes0 = np.stack([rng.uniform(mx, max(mx, width - box_w - mx), nboxes),
-                       rng.uniform(my, max(my, height - box_h - my), nboxes)], axis=1)
+    mx = np.minimum(8 * max_speed + 8, np.maximum(0.0, (width - bws) / 2 - 1))
+    my = np.minimum(8 * max_speed + 8, np.maximum(0.0, (height - bhs) / 2 - 1))
+    boxes0 = np.stack([rng.uniform(mx, np.maximum(mx, width - bws - mx), nboxes),
+                       rng.uniform(my, np.maximum(my, height - bhs - my), nboxes)], axis=1)
     vel = rng.uniform(-max_speed, max_speed, (nboxes, 2))
     box_params = [_texture_params(2000 + cam * 1000 + 17 * k + 1) for k in range(nboxes)]
     prng = np.random.default_rng(3000 + cam)
     pt_box = np.arange(npts) % nboxes
-    inner = np.stack([prng.uniform(4, box_w - 4, npts), prng.uniform(4, box_h - 4, npts)], axis=1)
+    inner = np.stack([prng.uniform(4, bws[pt_box] - 4, npts), prng.uniform(4, bhs[pt_box] - 4, npts)], axis=1)
     pts0 = (boxes0[pt_box] + inner).astype(np.float32)
-    return CameraScene(cam, width, height, box_w, box_h, boxes0, vel, pts0, pt_box, bg, box_params)
+    return CameraScene(cam, width, height, box_w, box_h, boxes0, vel, pts0, pt_box, bg, box_params, bws, bhs)
 
 
 def to_bgr(gray: np.ndarray) -> np.ndarray:

@@ -52,3 +52,12 @@ def test_configs3_shape_matches_oracle(oracle_mod):
     v = _verify("--cameras", "2", "--points", "2048", "--boxes", "32", steps=2, warmup=1)
     assert v["mismatches"] == 0, v["first_mismatch"]
     assert v["objects_checked"] >= 2 * 32 * 2
+
+
+def test_headline_mixed_boxes_matches_oracle(oracle_mod):
+    """bench.py --box-dist pets (the mixed_boxes leg): PETS-like per-detection
+    boxes, so every frame's LK launches span the box-kernel builds and the
+    large-window kernel."""
+    v = _verify("--box-dist", "pets", "--cameras", "2", steps=2, warmup=2)
+    assert v["mismatches"] == 0, v["first_mismatch"]
+    assert v["objects_checked"] >= 2 * 8 * 3
