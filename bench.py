@@ -281,6 +281,13 @@ class CameraFeed:
             group.push_frame(k, self.frames[f])
 
 
+def uniform_box(width):
+    """synth.make_scene's uniform box at a frame width (32x80 at 640x480,
+    64x160 at 1080p, 128x320 at 4K)."""
+    bw = 32 if width <= 640 else 64 if width <= 1920 else 128
+    return bw, int(bw * 2.5)
+
+
 def detection_boxes(scene, f):
     return [(float(int(x)), float(int(y)), float(scene.box_ws[k]), float(scene.box_hs[k]))
             for k, (x, y) in enumerate(scene.box_at(f))]
@@ -678,9 +685,10 @@ def tracker_line(args, r, world, C, scaling, profile):
             if (args.width, args.height, args.cameras, args.points, args.boxes) == (1920, 1080, 4, 512, 8)
             and not args.total_cameras else "Tracker2D Run")
     pets = args.box_dist == "pets"
-    box_txt = ("PETS-like boxes, synth.pets_box_sizes" if pets else "64x160 boxes")
+    bw, bh = uniform_box(args.width)
+    box_txt = ("PETS-like boxes, synth.pets_box_sizes" if pets else f"{bw}x{bh} boxes")
     win_txt = ("box-derived windows (backward w x w, forward w x h, mixed kernel classes)" if pets else
-               "64x64 windows")
+               f"{bw}x{bw} backward, {bw}x{bh} forward windows")
     out = {
         "metric": METRIC, "value": round(fps_all, 2), "unit": "frames/s", "n_gpus": world, "steps": r["steps"],
         "warmup": r["warmup"], "ms_per_step": round(1e3 * r["elapsed"] / r["steps"], 5), "higher_is_better": True,
@@ -691,14 +699,14 @@ def tracker_line(args, r, world, C, scaling, profile):
                          f") x " + ("GridFAST features (<= 100 each)" if args.features == "gridfast" else
                                     f"{args.points // args.boxes} points = {args.points} tracked points/camera")
                          + f", CPSNWhere_Tracker2D::Run: async H2D ingest + BGR->gray + pyramid, 3-step backward "
-                         f"chains ({win_txt}, LocalSearchKLT on device), forward LK + matching cost, "
+                         f"chains + forward LK ({win_txt}; LocalSearchKLT on device) + matching cost, "
                          "Munkres + tracker update + ResultWithTracker, packed result slots in host memory"
                          + (", RCCL all-gather of the slots (psn_comm)" if world > 1 else "")),
             "cameras": world * C, "cameras_per_gpu": C, "width": args.width, "height": args.height,
             "points_per_camera": args.points if args.features == "given" else round(r["points_per_camera"], 1),
-            "features": args.features, "detections_per_camera": args.boxes, "levels": 4,
+            "features": args.features, "detections_per_camera": args.boxes, "levels": 4 if args.width <= 1920 else "maxLevel 3, truncated per window (buildOpticalFlowPyramid)",
             **({"box_dist": "pets", "boxes_per_camera": r.get("box_sizes")} if pets else
-               {"box": [64, 160], "win_backward": [64, 64], "win_forward": [64, 160]}),
+               {"box": [bw, bh], "win_backward": [bw, bw], "win_forward": [bw, bh]}),
             "ingest": ("baseline JPEG files in host memory (q90 4:2:0, restart per MCU row), decoded on the device"
                        if args.ingest == "jpeg" else "BGR frames in pinned host memory"),
             "parallelism": f"camera-sharded x{world} ({C} cameras per GPU), RCCL all-gather of result slots"},
@@ -774,6 +782,18 @@ def tracker_legs(args, profile):
     legs["mixed_boxes"] = {k: lm[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["mixed_boxes"]["lk_launches"] = {k: lm["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
     legs["config4"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3)["line"]
+    legs["config4_frames_in_hbm"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3,
+                                                ingest="hbm")["line"]
+    # configs[4] through the whole Tracker2D Run: 8 x 4K BGR cameras, 4096 points per camera
+    # (64 detections x 64), 128 x 320 boxes: 128 x 128 backward and 128 x 320
+    # forward windows -- the large-window kernel
+    a4 = argparse.Namespace(**{**vars(args), "width": 3840, "height": 2160, "cameras": 8, "points": 4096,
+                               "boxes": 64, "verify": False, "box_dist": "uniform"})
+    r4 = tracker_run(a4, steps=max(args.leg_steps // 8, 5), warmup=2)
+    l4 = tracker_line(a4, r4, 1, 8, "weak", None)
+    legs["config4_tracker"] = {k: l4[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
+    legs["config4_tracker"]["lk_launches"] = {k: l4["roofline"].get(k) for k in ("kernel", "avg_launch_us",
+                                                                               "per_kernel_us")}
     return legs
 
 
@@ -807,10 +827,13 @@ def kernel_cpu_baseline(scene, period, npts, win, max_level, budget_s, max_frame
 
 
 def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, H=1080, N=512, levels=4,
-               sg=False):
-    """LK step over frames resident in HBM: C cameras per GPU, 21x21, `levels`
-    pyramid levels; sg: SG(9, 1) Insert of every tracked point's position per
-    frame (status as the active mask), on the same stream."""
+               sg=False, ingest="hbm"):
+    """LK step over C cameras per GPU, 21x21, `levels` pyramid levels; frames
+    resident in HBM (ingest "hbm": gray, pushed from device memory) or BGR in
+    pinned host memory uploaded every frame (ingest "host":
+    psn_lk_push_frame_async, copy engines, as the Tracker2D headline does);
+    sg: SG(9, 1) Insert of every tracked point's position per frame (status as
+    the active mask), on the same stream."""
     import torch
 
     from mcmtt_opticalflow_amd import dist as pdist
@@ -821,11 +844,22 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     win, R = 21, 4
     scenes = [synth.make_scene(c, W, H, N) for c in cams]
     frames = []
-    for sc in scenes:
-        f = torch.empty((args.period, H, W), dtype=torch.uint8, device=device)
-        for t in range(args.period):
-            f[t].copy_(torch.from_numpy(sc.frame(t)))
-        frames.append(f)
+    period = args.period if ingest == "hbm" else min(args.period, 4)  # pinned 4K BGR: 25 MB a frame
+    if ingest == "host":
+        pinned = pinned_allocator()
+        for sc in scenes:
+            fr = []
+            for t in range(period):
+                b = pinned((H, W, 3))
+                b[...] = synth.to_bgr(sc.frame(t))
+                fr.append(b)
+            frames.append(fr)
+    else:
+        for sc in scenes:
+            f = torch.empty((period, H, W), dtype=torch.uint8, device=device)
+            for t in range(period):
+                f[t].copy_(torch.from_numpy(sc.frame(t)))
+            frames.append(f)
     stream = torch.cuda.Stream(device)
     torch.cuda.set_stream(stream)
     ctx = lk.LKContext(W, H, ring_slots=R * C, max_level_cap=levels - 1, device=local_rank)
@@ -849,7 +883,10 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
 
     def push(t):
         for k in range(C):
-            ctx.push_frame_device(k * R + t % R, frames[k][ping_pong(t, args.period)].data_ptr(), W, 1)
+            if ingest == "host":
+                ctx.push_frame_async(k * R + t % R, frames[k][ping_pong(t, period)])
+            else:
+                ctx.push_frame_device(k * R + t % R, frames[k][ping_pong(t, period)].data_ptr(), W, 1)
 
     push(0)
     push(1)
@@ -895,7 +932,7 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     launch_b = C * lk_b + (pyr_b if mode == 2 else 0)
     return {"fps": C * steps / elapsed, "ms_per_step": 1e3 * elapsed / steps, "lk_us": lk_us,
             "launch_bytes": launch_b, "frame_bytes": pyr_b + lk_b, "scene": scenes[0], "elapsed": elapsed,
-            "mode": mode}
+            "mode": mode if ingest == "hbm" else "async-host"}
 
 
 def kernel_secondary(args):
@@ -909,16 +946,19 @@ def kernel_secondary(args):
                          "bytes_per_launch": r["launch_bytes"], "avg_launch_us": round(r["lk_us"], 3)}}
 
 
-def config4_run(args, world, rank, local_rank, steps, warmup):
+def config4_run(args, world, rank, local_rank, steps, warmup, ingest="host"):
     """BASELINE.json configs[4]: 8 cameras sharded over the ranks (strong), 3840x2160,
     4096 points/camera, 21x21, 5 levels (maxLevel 4), SG(9, 1) post-filter of every
-    tracked point's trajectory (CPSNWhere_SGSmooth, PSNWhere_SGSmooth.cpp:198-274)."""
+    tracked point's trajectory (CPSNWhere_SGSmooth, PSNWhere_SGSmooth.cpp:198-274).
+    ingest "host": BGR frames in pinned host memory uploaded every frame (8 x 24.9 MB
+    per frame-set over PCIe); "hbm": gray frames resident in HBM (no upload)."""
     total = 8
     if total % world:
         raise SystemExit(f"configs[4] shards 8 cameras: {world} ranks do not divide them")
     C = total // world
     W, H, N, levels = 3840, 2160, 4096, 5
-    r = kernel_run(args, steps, warmup, world, rank, local_rank, C=C, W=W, H=H, N=N, levels=levels, sg=True)
+    r = kernel_run(args, steps, warmup, world, rank, local_rank, C=C, W=W, H=H, N=N, levels=levels, sg=True,
+                   ingest=ingest)
     import torch
 
     from mcmtt_opticalflow_amd import dist as pdist
@@ -926,8 +966,11 @@ def config4_run(args, world, rank, local_rank, steps, warmup):
     elapsed = pdist.max_over_ranks(r["elapsed"], torch.device("cuda", local_rank))
     fps_all = total * steps / elapsed
     ach = r["launch_bytes"] / (r["lk_us"] * 1e-6) / 1e9
-    line = {"workload": f"BASELINE.json configs[4]: {total} cameras ({C} per GPU) x 3840x2160 gray resident in HBM, "
+    src = ("BGR in pinned host memory, uploaded every frame (psn_lk_push_frame_async)" if ingest == "host"
+           else "gray resident in HBM (no upload)")
+    line = {"workload": f"BASELINE.json configs[4]: {total} cameras ({C} per GPU) x 3840x2160 {src}, "
                         f"{N} points/camera, 21x21, 5 levels, SG(9,1) post-filter of every point trajectory",
+            "ingest": ingest,
             "value": round(fps_all, 2), "unit": "frames/s", "n_gpus": world, "steps": steps,
             "ms_per_step": round(1e3 * elapsed / steps, 5), "scaling": "strong",
             "roofline": {"kernel": "lk_kernel_st (all cameras in one launch) + sg_insert_kernel", "bound": "latency",
