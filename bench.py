@@ -11,8 +11,9 @@ recipe: uniform inside the boxes, seed 3000+cam), box-derived LK windows
 
 One step = one frame of every camera through CPSNWhere_Tracker2D::Run
 (psn_where/PSNWhere_Tracker2D.cpp:251-373) as psn_t2d_group runs it:
-  1. upload of frame t+1 of every camera from pinned host memory (copy engine)
-     + BGR->gray + pyramid build, overlapping frame t's work (:256-263);
+  1. upload of frame t+2 of every camera from pinned host memory (copy engine)
+     + BGR->gray + pyramid build, overlapping frame t's work (:256-263; two
+     frames staged ahead, --stage-ahead);
   2. features of every detection: given (SURVEY 8(d) point recipe) or GridFAST
      on the device (--features gridfast, :735-758);
   3. backward chains of every detection: 3 LK steps (64x64) with LocalSearchKLT
@@ -379,10 +380,12 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     T = t2d.load()
     recorded = [] if args.verify else None
 
+    ahead = args.stage_ahead
+
     def step(t, dets, next_dets):
         group.launch(t, dets, gridfast=gridfast, seed=t)  # after complete_next(t-1): a confirmation
-        for k, fd in enumerate(feeds):  # frame t+1 uploads while frame t runs
-            fd.push(group, k, t + 1)
+        for k, fd in enumerate(feeds):  # frame t+ahead uploads (and builds) while frame t runs
+            fd.push(group, k, t + ahead)
         group.complete_next(t + 1, next_dets, gridfast=gridfast, seed=t + 1, raw=True)
         for k in range(C):  # the hand-off slots (psn_t2d_pack_result) in host memory
             rc = T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
@@ -396,8 +399,9 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     def all_dets(t):
         return [fd.detections(t2d, t) for fd in feeds]
 
-    for k, fd in enumerate(feeds):
-        fd.push(group, k, 0)
+    for f in range(ahead):  # frames 0 .. ahead-1 staged before the first launch
+        for k, fd in enumerate(feeds):
+            fd.push(group, k, f)
     # ctypes records of every frame, built outside the timed region; one more
     # frame than completed: the last step launches its successor ahead, as the
     # warm-up's last step did for the first timed frame
@@ -1083,6 +1087,9 @@ def parse_args(argv=None):
                          "a seeded PETS-like distribution scaled to the frame (synth.pets_box_sizes)")
     ap.add_argument("--ingest", choices=["bgr", "jpeg"], default="bgr",
                     help="tracker mode: frames arrive as BGR arrays (default) or as JPEG files (device decode)")
+    ap.add_argument("--stage-ahead", type=int, choices=[1, 2], default=2,
+                    help="tracker mode: frames uploaded ahead of the running one (2: frame t+2 uploads and builds "
+                         "while frame t runs; 1: frame t+1 only)")
     ap.add_argument("--verify", action="store_true", help="check every frame's results against the oracle")
     ap.add_argument("--kcameras", type=int, default=1, help="kernel mode: cameras per GPU")
     ap.add_argument("--kpoints", type=int, default=512, help="kernel mode: points per camera")

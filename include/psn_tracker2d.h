@@ -188,8 +188,8 @@ int psn_t2d_track_frame_detect(psn_t2d *t, psn_t2d_detection *dets, int ndet, ui
  * as the reference's row-major Munkres breaks them. */
 int psn_t2d_assign(const float *cost, int rows, int cols, int *match);
 
-/* CPSNWhere_Hungarian Initialize(float*, rows, cols) + Match()
- * (helpers/PSNWhere_Hungarian.cpp:124-155, :212-359) on [rows x cols] float
+/* CPSNWhere_Hungarian Initialize(std::vector<float>, rows, cols) + Match()
+ * (helpers/PSNWhere_Hungarian.cpp:67-89, :212-359) on [rows x cols] float
  * costs: non-finite entries become FLT_MAX - (sum of the finite ones), rows and
  * columns without a finite entry are condensed out, the square is padded to its
  * minimum line cover, Munkres steps 1-6 in float32 (row-major scans), and the
@@ -232,7 +232,9 @@ int psn_t2d_read_result_txt(const char *dir, unsigned cam_id, unsigned frame_idx
 /* ---- CPSNWhere_Tracker2D::Run over several cameras, batched ----
  * One group = C cameras on one device (camera c = index c, cam_ids[c] its
  * camID). Per frame:
- *   psn_t2d_group_push_frame(g, c, frame t)    for every camera (async upload)
+ *   psn_t2d_group_push_frame(g, c, frame t)    for every camera (async upload;
+ *                                              up to 2 frames per camera may be
+ *                                              staged, adopted in push order)
  *   psn_t2d_group_launch(g, t, dets, ...)      enqueue the frame's device work
  *   [psn_t2d_group_push_frame(g, c, frame t+1) may overlap it here]
  *   psn_t2d_group_complete(g, dets, results)   wait; matching, update, results
@@ -270,8 +272,9 @@ int psn_t2d_group_run(psn_t2d_group *g, unsigned frame_idx, psn_t2d_detection *c
  * every camera must be staged (push_frame) before this call; the next call must
  * be psn_t2d_group_launch(g, next_frame_idx, next_dets, next_ndet, feature_mode,
  * .), which then only confirms the frame, and next_dets must stay valid until
- * that frame's complete. A pipelined driver:
- *   launch(0); push(1); complete_next(0 -> 1); launch(1); push(2); complete_next(1 -> 2); ...
+ * that frame's complete. A pipelined driver (frames uploaded two ahead: frame
+ * t+2 moves while frame t runs):
+ *   push(0); push(1); launch(0); push(2); complete_next(0 -> 1); launch(1); push(3); complete_next(1 -> 2); ...
  * If only the next frame cannot be launched (e.g. a detection whose window the
  * LK cannot run), this frame's results are still written to dets / results and
  * that error is returned; the next frame is not in flight, its images stay

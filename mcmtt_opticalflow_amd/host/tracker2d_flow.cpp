@@ -143,7 +143,8 @@ int Tracker2DFlow::InitializeCameras(const std::vector<unsigned> &camIDs, int wi
     for (size_t c = 0; c < camIDs.size(); c++) {
         cams_[c].camID = camIDs[c];
         for (int i = 0; i < kT2dInterval; i++) cams_[c].ring[i] = (int)c * kSlotsPerCam + i;
-        cams_[c].spare = (int)c * kSlotsPerCam + kT2dInterval;
+        for (int i = 0; i < kT2dStaging; i++) cams_[c].spares[i] = (int)c * kSlotsPerCam + kT2dInterval + i;
+        cams_[c].nstaged = 0;
     }
     filled_.assign((size_t)nslots, 0);
     // stream priorities: the backward chains (three dependent launches per frame)
@@ -1047,24 +1048,39 @@ int Tracker2DFlow::PushFrameDevice(const uint8_t *dev, int stride, int channels)
     return PSN_LK_OK;
 }
 
+// The next free staging slot of a camera (frames are adopted in push order).
+int Tracker2DFlow::NextStagingSlot(size_t cam, int *slot) {
+    Cam &c = cams_[cam];
+    if (c.nstaged >= kT2dStaging) {
+        err_ = "camera " + std::to_string(cam) + ": " + std::to_string(kT2dStaging) + " frames staged already";
+        return PSN_LK_ERR_ARG;
+    }
+    *slot = c.spares[c.nstaged];
+    return PSN_LK_OK;
+}
+
 int Tracker2DFlow::StageFrame(size_t cam, const uint8_t *frame, int stride, int channels, bool on_device) {
     if (!lk_ || cam >= cams_.size() || !frame) return PSN_LK_ERR_ARG;
     Cam &c = cams_[cam];
-    const int rc = on_device ? psn_lk_push_frame_device(lk_, c.spare, frame, stride, channels)
-                             : psn_lk_push_frame_async(lk_, c.spare, frame, stride, channels);
+    int slot = -1, rc = NextStagingSlot(cam, &slot);
+    if (rc) return rc;
+    rc = on_device ? psn_lk_push_frame_device(lk_, slot, frame, stride, channels)
+                   : psn_lk_push_frame_async(lk_, slot, frame, stride, channels);
     if (rc) return fail(rc, "stage frame");
-    filled_[(size_t)c.spare] = 1;
-    c.staged = true;
+    filled_[(size_t)slot] = 1;
+    c.nstaged++;
     return PSN_LK_OK;
 }
 
 int Tracker2DFlow::StageFrameJpeg(size_t cam, const uint8_t *jpeg, size_t len) {
     if (!lk_ || cam >= cams_.size() || !jpeg) return PSN_LK_ERR_ARG;
     Cam &c = cams_[cam];
-    const int rc = psn_lk_push_frame_jpeg(lk_, c.spare, jpeg, len);
+    int slot = -1, rc = NextStagingSlot(cam, &slot);
+    if (rc) return rc;
+    rc = psn_lk_push_frame_jpeg(lk_, slot, jpeg, len);
     if (rc) return fail(rc, "stage JPEG frame");
-    filled_[(size_t)c.spare] = 1;
-    c.staged = true;
+    filled_[(size_t)slot] = 1;
+    c.nstaged++;
     return PSN_LK_OK;
 }
 
@@ -1442,7 +1458,7 @@ int Tracker2DFlow::TrackFrame(const std::vector<Detection> &dets, const std::vec
 int Tracker2DFlow::AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::vector<PassCam> &pass) {
     if (io.size() != cams_.size()) return PSN_LK_ERR_ARG;
     for (size_t c = 0; c < cams_.size(); c++) {
-        if (!cams_[c].staged) {
+        if (cams_[c].nstaged == 0) {
             err_ = "camera " + std::to_string(c) + ": no frame staged";
             return PSN_LK_ERR_SLOT;
         }
@@ -1451,11 +1467,14 @@ int Tracker2DFlow::AdoptFrames(std::vector<CamFrame> &io, bool gridfast, std::ve
     pass.assign(cams_.size(), PassCam());
     for (size_t c = 0; c < cams_.size(); c++) {
         Cam &cam = cams_[c];
+        // the first staged frame joins the ring as frame t; the oldest ring slot
+        // becomes the last staging slot (a later push into it waits for its readers)
         const int oldest = cam.ring[0];
         std::rotate(cam.ring, cam.ring + 1, cam.ring + kT2dInterval);
-        cam.ring[kT2dInterval - 1] = cam.spare;
-        cam.spare = oldest;
-        cam.staged = false;
+        cam.ring[kT2dInterval - 1] = cam.spares[0];
+        std::rotate(cam.spares, cam.spares + 1, cam.spares + kT2dStaging);
+        cam.spares[kT2dStaging - 1] = oldest;
+        cam.nstaged--;
         PassCam &p = pass[c];
         p.cam = c;
         p.dets = &io[c].dets;
@@ -1471,9 +1490,10 @@ void Tracker2DFlow::UnadoptFrames() {
     for (Cam &cam : cams_) {
         const int newest = cam.ring[kT2dInterval - 1];
         std::rotate(cam.ring, cam.ring + kT2dInterval - 1, cam.ring + kT2dInterval);
-        cam.ring[0] = cam.spare;
-        cam.spare = newest;
-        cam.staged = true;
+        cam.ring[0] = cam.spares[kT2dStaging - 1];
+        std::rotate(cam.spares, cam.spares + kT2dStaging - 1, cam.spares + kT2dStaging);
+        cam.spares[0] = newest;
+        cam.nstaged++;
     }
 }
 

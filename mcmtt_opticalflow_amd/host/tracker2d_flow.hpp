@@ -25,7 +25,10 @@
 namespace psn {
 
 constexpr int kT2dInterval = 4;          // PSN_2D_BACKTRACKING_INTERVAL (:16)
-constexpr int kSlotsPerCam = kT2dInterval + 1;  // the ring + one slot the next frame is staged in
+// the ring + two staging slots: frame t+2 uploads (and its pyramid builds) while
+// frame t+1 waits staged and frame t runs
+constexpr int kT2dStaging = 2;
+constexpr int kSlotsPerCam = kT2dInterval + kT2dStaging;
 constexpr size_t kT2dMinFeatures = 4;    // PSN_2D_FEATURE_MIN_NUM_TRACK (:12)
 constexpr size_t kT2dMaxFeatures = 100;  // PSN_2D_FEATURE_MAX_NUM_TRACK (:13)
 constexpr int kT2dResBlocks = 3;         // chain result blocks used in turn by consecutive passes
@@ -91,10 +94,13 @@ class Tracker2DFlow {
     // ---- multi-camera Run (CPSNWhere_Tracker2D::Run of every camera) ----
     // StageFrame: frame t of camera `cam` is uploaded (host frames: async, a copy
     // engine for pinned memory) and its pyramid built on the ingest stream, into
-    // the camera's staging slot; the next RunLaunch adopts it as frame t. May be
-    // called for frame t+1 between RunLaunch(t) and RunComplete(t).
+    // the camera's next staging slot; launches adopt staged frames in push order
+    // (up to kT2dStaging staged at once). May be called for frame t+1 between
+    // RunLaunch(t) and RunComplete(t), and for frame t+2 as well once frame t+1
+    // is staged (a pipelined driver uploads two frames ahead).
     int StageFrame(size_t cam, const uint8_t *frame, int stride, int channels, bool on_device);
     int StageFrameJpeg(size_t cam, const uint8_t *jpeg, size_t len);  // a baseline JPEG, decoded on the device
+    int NextStagingSlot(size_t cam, int *slot);
     struct CamFrame {  // one camera's inputs and outputs of Run
         std::vector<Detection> dets;                      // height-validated detections of frame t
         std::vector<std::vector<Point2f>> features;       // in (given mode) / out (GridFAST mode)
@@ -157,8 +163,10 @@ class Tracker2DFlow {
     struct Cam {  // per-camera state
         unsigned camID = 0;
         int ring[kT2dInterval];  // slot ids, oldest first; ring[kT2dInterval - 1] = frame t
-        int spare = -1;          // staging slot of the next frame (multi-camera Run)
-        bool staged = false;
+        // slots outside the ring (multi-camera Run), FIFO: spares[0 .. nstaged) hold
+        // staged frames in push order, the rest are free
+        int spares[kT2dStaging];
+        int nstaged = 0;
         // Run state: m_listTracker2D, m_queueActiveTracker2D, m_nNewTrackerID
         std::list<Tracker2D> storage;
         std::deque<Tracker2D *> active;

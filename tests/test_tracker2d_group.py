@@ -68,12 +68,14 @@ def _check_result(g_res, r_res, what):
     assert g_res["detection_rects"] == [] and g_res["tracker_rects"] == []
 
 
-@pytest.mark.parametrize("ahead", [False, True])
+@pytest.mark.parametrize("ahead", [False, True, "two"])
 @pytest.mark.parametrize("gridfast", [False, True])
 @pytest.mark.parametrize("W,H,bw,bh", [(640, 480, 32, 80), (960, 540, 64, 160)])
 def test_group_run_matches_oracle(oracle_mod, gridfast, W, H, bw, bh, ahead):
     """ahead: frame t+1's chains are launched by complete_next(t) before the host
-    matches frame t (the pipelined driver of the bench)."""
+    matches frame t (the pipelined driver of the bench); "two": besides, frames
+    are staged two ahead (frame t+2 pushed while frame t runs, the bench's
+    default driver)."""
     C, T = 3, 7
     scenes = [synth.make_scene(40 + c, W, H, 120, nboxes=3, box_w=bw, box_h=bh, max_speed=3.0) for c in range(C)]
     refs = [ORC.CameraTracker(cam_id=10 + c) for c in range(C)]
@@ -85,15 +87,17 @@ def test_group_run_matches_oracle(oracle_mod, gridfast, W, H, bw, bh, ahead):
                                      location=e[1], height=e[2]) for b, e, f in zip(*per_frame[t][c])]
                  for c in range(C)] for t in range(T)]
     n_obj = n_matched = 0
+    stage = 2 if ahead == "two" else 1
     with t2d.Group(W, H, [10 + c for c in range(C)]) as g:
-        for c in range(C):  # camera 1 ingests BGR, the others gray
-            g.push_frame(c, bgrs[c][0] if c == 1 else grays[c][0])
+        for f in range(stage):
+            for c in range(C):  # camera 1 ingests BGR, the others gray
+                g.push_frame(c, bgrs[c][f] if c == 1 else grays[c][f])
         for t in range(T):
             per_cam = per_frame[t]
             g.launch(t, g_frames[t], gridfast=gridfast, seed=t)
-            if t + 1 < T:  # frame t+1 is uploaded while frame t runs
+            if t + stage < T:  # frame t+stage is uploaded while frame t runs
                 for c in range(C):
-                    g.push_frame(c, bgrs[c][t + 1] if c == 1 else grays[c][t + 1])
+                    g.push_frame(c, bgrs[c][t + stage] if c == 1 else grays[c][t + stage])
             if ahead and t + 1 < T:
                 out = g.complete_next(t + 1, g_frames[t + 1], gridfast=gridfast, seed=t + 1)
             else:
@@ -139,6 +143,14 @@ def test_group_ahead_protocol():
             g.launch(2, d)  # not the announced frame
         g.launch(1, d)
         g.complete()
+        g.push_frame(0, img)
+        g.push_frame(0, img)  # two frames staged
+        with pytest.raises(t2d.T2dError):
+            g.push_frame(0, img)  # a third one has no slot
+        g.run(2, d)
+        g.run(3, d)
+        with pytest.raises(t2d.T2dError):
+            g.launch(4, d)  # nothing staged
 
 
 def test_group_next_frame_failure_keeps_frame():
