@@ -449,9 +449,12 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     group.close()
     if exch:
         exch.close()
+    isolated = None
+    if args.isolated and world == 1:
+        isolated = isolated_launches(args, C)
     box_sizes = [[[int(fd.scene.box_ws[k]), int(fd.scene.box_hs[k])] for k in range(args.boxes)] for fd in feeds]
     return {"elapsed": elapsed, "steps": steps, "warmup": warmup, "cams_per_rank": C, "world": world,
-            "box_sizes": box_sizes,
+            "box_sizes": box_sizes, "isolated": isolated,
             "measure_steps": measure,
             "per_kernel": per_kernel, "ts": ts, "samples": samples, "objs_last": objs_last,
             "points_per_camera": pts_last, "recorded": recorded, "slot_bytes": slot_bytes, "max_obj": max_obj}
@@ -600,6 +603,41 @@ def load_profile(path):
         return None
 
 
+def isolated_launches(args, C, reps=20):
+    """The frame-set's LK launches alone on the GPU (nothing else in flight):
+    C cameras' pyramids (frames 0 -> 1 of each camera's synthetic scene) and one
+    query per camera over its `points` given features, with the forward (w x h)
+    and the backward (w x w) box windows; per shape the median HIP-event duration
+    of `reps` launches. Outside the timed region."""
+    from mcmtt_opticalflow_amd import _lib, lk, synth
+
+    L = _lib.load()
+    W, H = args.width, args.height
+    bw, bh = uniform_box(W)
+    out = {}
+    scenes = [synth.make_scene(c, W, H, args.points, nboxes=args.boxes) for c in range(C)]
+    with lk.LKContext(W, H, ring_slots=2 * C, max_level_cap=3) as ctx:
+        for c, sc in enumerate(scenes):
+            ctx.push_frame(2 * c, synth.to_bgr(sc.frame(0)))
+            ctx.push_frame(2 * c + 1, synth.to_bgr(sc.frame(1)))
+        pts = np.concatenate([sc.points_at(0) for sc in scenes])
+        for name, win in (("forward", (bw, bh)), ("backward", (bw, bw))):
+            qs = [lk.make_query(2 * c, 2 * c + 1, c * args.points, args.points, lk.make_params(win, 3))
+                  for c in range(C)]
+            for _ in range(3):
+                ctx.track(qs, pts)
+            L.psn_lk_enable_timing(ctx.handle, reps + 1, 1)
+            for _ in range(reps):
+                ctx.track(qs, pts)
+            ms = np.array([m for m, _ in _lib.timing_launches(L, ctx.handle, reps + 1)])
+            tags = {t for _, t in _lib.timing_launches(L, ctx.handle, reps + 1)}
+            L.psn_lk_enable_timing(ctx.handle, 0, 1)
+            out[name] = {"window": list(win), "median_us": round(1e3 * float(np.median(ms)), 2),
+                         "min_us": round(1e3 * float(ms.min()), 2), "launches": int(ms.size),
+                         "kernel": ",".join(sorted(_lib.kernel_of_tag(t) for t in tags))}
+    return out
+
+
 def tracker_roofline(args, r, C, profile):
     """Roofline of the dominant LK kernel (largest share of the timed LK time),
     per launch: SURVEY 8(d) LK bytes per camera-frame (2*S_pyr + 21*N) x the C
@@ -622,7 +660,20 @@ def tracker_roofline(args, r, C, profile):
            "bytes_note": f"SURVEY 8(d) LK bytes 2*S_pyr + 21*N = {lk_b} per camera-frame x {C} camera-frames per "
                          "launch; achieved/peak/frac are the HBM roofline of this kernel (contract fields)",
            "per_kernel_us": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
-                                 "ms_per_step": round(v[1] / max(r["measure_steps"], 1), 4)} for k, v in sorted(per.items())}}
+                                 "ms_per_step": round(v[1] / max(r["measure_steps"], 1), 4)} for k, v in sorted(per.items())},
+           "avg_launch_note": "avg_launch_us = the launch's wall time in the running pipeline (HIP events on its "
+                              "stream; consecutive launches overlap on their streams); isolated = the same launch "
+                              "alone on the GPU"}
+    iso = r.get("isolated")
+    if iso:
+        fw = iso["forward"] if "forward" in iso else None
+        if fw and fw.get("median_us"):
+            a_iso = launch_b / (fw["median_us"] * 1e-6) / 1e9
+            out["isolated"] = {**fw, "achieved": round(a_iso, 3), "frac": round(a_iso / HBM_PEAK_GBPS, 6),
+                               "bytes_per_launch": launch_b,
+                               "workload": f"the forward launch of one frame-set alone on the GPU: {C} cameras x "
+                                           f"{args.points} points, median of {fw['launches']} launches"}
+        out["isolated_backward"] = iso.get("backward")
     lib_sha = file_sha16(_lib.LIB_PATH)
     if profile:
         pk = profile.get("kernels", {}).get(name, {})
@@ -661,6 +712,10 @@ def tracker_roofline(args, r, C, profile):
                     v[key + "_per_launch"] = int(pk[key])
             if pk.get("SQ_WAVE_CYCLES") and pk.get("SQ_WAIT_INST_ANY"):
                 v["wait_frac"] = round(pk["SQ_WAIT_INST_ANY"] / pk["SQ_WAVE_CYCLES"], 4)
+            cyc2 = pk.get("SQ_WAVE_CYCLES_sq2") or pk.get("SQ_WAVE_CYCLES")
+            if cyc2 and pk.get("SQ_WAIT_ANY"):
+                v["SQ_WAIT_ANY_per_launch"] = int(pk["SQ_WAIT_ANY"])
+                v["wait_any_frac"] = round(pk["SQ_WAIT_ANY"] / cyc2, 4)
             out["valu"] = v
             # what bounds it, from the counters: VALU issue when either issue fraction
             # nears the peak; the HBM roofline when the PMC traffic rate does; else the
@@ -673,7 +728,9 @@ def tracker_roofline(args, r, C, profile):
                 out["bound"] = "hbm"
             out["bound_note"] = (f"VALU issue {v['frac']:.0%} of peak over the launch, "
                                  f"{v.get('frame_set_frac', 0):.0%} over the frame-set; PMC HBM "
-                                 f"{hbm_rate:.0f} GB/s; below 60 % of either peak the kernel is latency-bound")
+                                 f"{hbm_rate:.0f} GB/s; below 60 % of either peak the kernel is latency-bound"
+                                 + (f"; waves wait {v['wait_any_frac']:.0%} of their cycles (SQ_WAIT_ANY)"
+                                    if "wait_any_frac" in v else ""))
     return out
 
 
@@ -770,17 +827,18 @@ def tracker_legs(args, profile):
     """Extra single-GPU lines of the default run: configs[3] on one GPU (8 cameras
     x 2048 points, the strong-scaling run's N=1), the GridFAST Run, configs[4]."""
     legs = {}
-    a3 = argparse.Namespace(**{**vars(args), "total_cameras": 8, "points": 2048, "boxes": 32, "verify": False})
+    a3 = argparse.Namespace(**{**vars(args), "total_cameras": 8, "points": 2048, "boxes": 32, "verify": False,
+                               "isolated": False})
     r3 = tracker_run(a3, steps=args.leg_steps, warmup=3)
     l3 = tracker_line(a3, r3, 1, 8, "strong", None)
     legs["configs3_1gpu"] = {k: l3[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["configs3_1gpu"]["roofline"] = {k: l3["roofline"].get(k) for k in ("kernel", "achieved", "frac",
                                                                             "avg_launch_us", "per_kernel_us")}
-    ag = argparse.Namespace(**{**vars(args), "features": "gridfast", "verify": False})
+    ag = argparse.Namespace(**{**vars(args), "features": "gridfast", "verify": False, "isolated": False})
     rg = tracker_run(ag, steps=args.leg_steps, warmup=3)
     lg = tracker_line(ag, rg, 1, args.cameras, "weak", None)
     legs["gridfast"] = {k: lg[k] for k in ("value", "unit", "ms_per_step", "steps", "config")}
-    am = argparse.Namespace(**{**vars(args), "box_dist": "pets", "verify": False})
+    am = argparse.Namespace(**{**vars(args), "box_dist": "pets", "verify": False, "isolated": False})
     rm = tracker_run(am, steps=args.leg_steps, warmup=3)
     lm = tracker_line(am, rm, 1, args.cameras, "weak", None)
     legs["mixed_boxes"] = {k: lm[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
@@ -792,7 +850,7 @@ def tracker_legs(args, profile):
     # (64 detections x 64), 128 x 320 boxes: 128 x 128 backward and 128 x 320
     # forward windows -- the large-window kernel
     a4 = argparse.Namespace(**{**vars(args), "width": 3840, "height": 2160, "cameras": 8, "points": 4096,
-                               "boxes": 64, "verify": False, "box_dist": "uniform"})
+                               "boxes": 64, "verify": False, "box_dist": "uniform", "isolated": False})
     r4 = tracker_run(a4, steps=max(args.leg_steps // 8, 5), warmup=2)
     l4 = tracker_line(a4, r4, 1, 8, "weak", None)
     legs["config4_tracker"] = {k: l4[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
@@ -1098,6 +1156,8 @@ def parse_args(argv=None):
     ap.add_argument("--leg-steps", type=int, default=40)
     ap.add_argument("--measure-steps", type=int, default=20,
                     help="frames after the timed region with per-launch HIP-event timing (roofline)")
+    ap.add_argument("--no-isolated", dest="isolated", action="store_false",
+                    help="skip the isolated-launch timing of the frame-set's LK launches (roofline.isolated)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-legs", action="store_true")

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 def _verify(*argv, steps, warmup):
     import bench
 
-    args = bench.parse_args(["--verify", "--no-legs", "--no-secondary", "--no-cpu-baseline", *argv])
+    args = bench.parse_args(["--verify", "--no-legs", "--no-secondary", "--no-cpu-baseline", "--no-isolated", *argv])
     r = bench.tracker_run(args, steps=steps, warmup=warmup)
     v = bench.verify_tracker(args, r)
     assert v["frames"] == steps + warmup

@@ -13,12 +13,13 @@ OUT=$ROOT/gpurun_out/prof_$R
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 B="$ROOT/bench.py"
-Q="--no-cpu-baseline --no-secondary --no-legs"
+Q="--no-cpu-baseline --no-secondary --no-legs --no-isolated"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$B" --steps 100 --warmup 5 $Q > "$OUT/trace_bench.json" 2> "$OUT/trace.log"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace" -o run --output-format csv -- python3 "$B" --mode kernel --steps 200 --warmup 10 $Q > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.log"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/fetch.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/write.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY -d "$OUT/sq" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/sq.log" 2>&1
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY -d "$OUT/sq2" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/sq2.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/cfetch" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cfetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/cwrite" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cwrite.log" 2>&1
 python3 "$ROOT/tools/profile_summary.py" "$OUT" "$ROOT/mcmtt_opticalflow_amd/lib/libpsn_lk.so" "$OUT/profile.json" > "$OUT/profile_summary.log"

@@ -9,7 +9,7 @@ factors), SQ counters per launch (SQ_INSTS_VALU, SQ_WAVES, SQ_BUSY_CYCLES,
 the profiled libpsn_lk.so (bench.py checks it against the binary it runs).
 
 usage: profile_summary.py OUTDIR LIB OUT.json
-  OUTDIR holds trace/ fetch/ write/ cfetch/ cwrite/ sq/ (rocprofv3 -d dirs)
+  OUTDIR holds trace/ fetch/ write/ cfetch/ cwrite/ sq/ sq2/ (rocprofv3 -d dirs)
 """
 import csv
 import glob
@@ -62,6 +62,13 @@ def main():
     fetch, res_f = counters(os.path.join(d, "fetch"))
     write, _ = counters(os.path.join(d, "write"))
     sq, res_s = counters(os.path.join(d, "sq"))
+    # the SQ_WAIT_ANY pass, with its own SQ_WAVE_CYCLES (the wait fraction comes from one pass)
+    sq2, _ = counters(os.path.join(d, "sq2"))
+    for k, cs in sq2.items():
+        if "SQ_WAIT_ANY" in cs:
+            sq[k]["SQ_WAIT_ANY"] = cs["SQ_WAIT_ANY"]
+        if "SQ_WAVE_CYCLES" in cs:
+            sq[k]["SQ_WAVE_CYCLES_sq2"] = cs["SQ_WAVE_CYCLES"]
     stats = {}
     for r in rows(os.path.join(d, "trace"), "*kernel_stats.csv"):
         stats[short(r["Name"])] = {"launches": int(r["Calls"]), "avg_us": round(float(r["AverageNs"]) / 1e3, 2),
