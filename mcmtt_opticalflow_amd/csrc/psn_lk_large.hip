@@ -63,6 +63,27 @@ __device__ __forceinline__ LgIter lg_iter(const LevelDev &J, int inx, int iny, i
 __device__ __forceinline__ int lg_gx(int v) { return (int)(short)(v & 0xffff); }
 __device__ __forceinline__ int lg_gy(int v) { return v >> 16; }
 
+// Diagnostic phase clocks (PSN_LK_STAMPS build, tools/lg_stamps.py): accumulated
+// s_memtime ticks per phase of each point, thread 0's view, stamps[point][0..15].
+#ifdef PSN_LK_STAMPS
+#define LG_CLK(t) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory")
+#define LG_MARK(i)                    \
+    do {                              \
+        unsigned long long t_;        \
+        LG_CLK(t_);                   \
+        lg_acc[i] += t_ - lg_t;       \
+        lg_t = t_;                    \
+    } while (0)
+#define LG_COUNT(i) lg_acc[i]++
+#else
+#define LG_MARK(i) \
+    do {           \
+    } while (0)
+#define LG_COUNT(i) \
+    do {            \
+    } while (0)
+#endif
+
 template <int NT>
 __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -97,6 +118,11 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
         int status = 1;
         float errv = 0.f;
         unsigned nwin = 0;  // window passes (A phase + iterations): the sample count / (w*h)
+#ifdef PSN_LK_STAMPS
+        unsigned long long lg_acc[16] = {}, lg_t = 0, lg_t0 = 0;
+        LG_CLK(lg_t0);
+        lg_t = lg_t0;
+#endif
 
         for (int level = maxL; level >= 0; level--) {
             const LevelDev I = ring_level_u(A.ring, Q.prev_slot, level);
@@ -186,6 +212,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
             }
             // (the reduce's barrier also publishes the slot's window values to the workgroup)
             block_reduce4<NT, true>(sA11, sA12, aA12, sA22, REDI);
+            LG_MARK(0);  // A phase: I bands, Scharr, window values, integer sums
             const bool ex11 = sA11 <= kExact, ex12 = aA12 <= (unsigned)kExact, ex22 = sA22 <= (unsigned)kExact;
             float A11 = (float)sA11, A12 = (float)sA12, A22 = (float)sA22;
             if (!(ex11 && ex12 && ex22)) {
@@ -230,6 +257,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
                 if (!ex22) A22 = s3[2];
                 __syncthreads();  // RED read by all before any later write
             }
+            LG_MARK(1);  // A ordered chains
             A11 = __fmul_rn(A11, FLT_SCALE);
             A12 = __fmul_rn(A12, FLT_SCALE);
             A22 = __fmul_rn(A22, FLT_SCALE);
@@ -273,12 +301,16 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
                         a2 = sat_add(a2, (unsigned)abs(t2));
                     }
                 }
+                LG_MARK(2);  // main pass
+                LG_COUNT(10);
                 block_reduce4<NT, false>(s1, s2, a1, a2, REDI);
+                LG_MARK(3);  // reduce
                 float b1, b2;
                 if (sums_exact(a1, s1) && sums_exact(a2, s2)) {  // subset-sum bound (see sums_exact)
                     b1 = (float)s1;
                     b2 = (float)s2;
                 } else {
+                    LG_COUNT(11);
                     float bacc = 0.f;
                     for (int r0 = 0; r0 < h; r0 += TR) {
                         const int th = min(TR, h - r0);
@@ -294,12 +326,14 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
                             Prod[C.P + pos] = (float)(diff * lg_gy(v.y));
                         }
                         __syncthreads();
+                        LG_MARK(4);  // fallback: band products
                         if (tid < 10) {
                             const int ch = tid % 5, s = tid / 5;
                             const int base = ch < 4 ? ch * C.SB : 4 * C.SB;
                             const int len = ch < 4 ? th * 2 * C.nB : th * C.tB;
                             bacc = chain_sum(Prod + s * C.P + base, len, bacc);
                         }
+                        LG_MARK(5);  // fallback: chain sums
                     }
                     if (tid < 10) RED[16 + tid] = bacc;
                     __syncthreads();
@@ -316,6 +350,7 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
                     }
                     __syncthreads();  // RED read by all before any later write
                 }
+                LG_MARK(6);  // results
                 b1 = __fmul_rn(b1, FLT_SCALE);
                 b2 = __fmul_rn(b2, FLT_SCALE);
                 const float dx = __fmul_rn(__fsub_rn(__fmul_rn(A12, b2), __fmul_rn(A22, b1)), D);
@@ -379,6 +414,15 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
             }
         }
 
+#ifdef PSN_LK_STAMPS
+        {
+            unsigned long long t_end;
+            LG_CLK(t_end);
+            lg_acc[15] = t_end - lg_t0;
+            if (tid == 0 && A.stamps)
+                for (int i = 0; i < 16; i++) A.stamps[(size_t)g * 64 + i] = lg_acc[i];
+        }
+#endif
         if (tid == 0) {
             A.next[2 * pi] = NPx;
             A.next[2 * pi + 1] = NPy;
