@@ -104,7 +104,7 @@ struct psn_lk_ctx {
     // large-window kernel (lk_kernel_lg): LARGE forces it for every query;
     // lg_lds = LDS budget of one of its workgroups (row bands of the window)
     bool force_large = false;
-    int lg_lds = 40 * 1024;
+    int lg_lds = 24 * 1024;
     // its window-value slots in HBM, one buffer per stream (launches on one
     // stream run in order; launches on different streams may overlap)
     struct LgWs {
@@ -691,10 +691,12 @@ static int tiled_rows(const psn_lk_ctx *c, int w, int h) {
     while (tr > 1 && psn::lk_lds_bytes(w, h, tr) > budget) tr--;
     return psn::lk_lds_bytes(w, h, tr) <= budget ? tr : 0;
 }
-// Band rows of the large-window kernel within its LDS budget (>= 1 band row).
+// Band rows of the large-window kernel's A phase within its LDS budget (>= 1 row;
+// the tile planes of the fallbacks set the floor of the budget).
 static int lg_rows(const psn_lk_ctx *c, int w, int h) {
     int tr = 1;
-    while (tr < h && psn::lg_lds_bytes(w, tr + 1) <= c->lg_lds) tr++;
+    const int budget = std::max(c->lg_lds, psn::lg_lds_bytes(w, 1));
+    while (tr < h && psn::lg_lds_bytes(w, tr + 1) <= budget) tr++;
     return tr;
 }
 

@@ -254,17 +254,31 @@ inline int bx_err_rows(int w, int h, int pb) {
     return 1;
 }
 
-// Large-window kernel (lk_kernel_lg, any window the LDS-resident kernels cannot
-// hold): window values in an HBM slot per workgroup, J read straight from the
-// pyramid, LDS only for one row band of the I patch / Scharr plane / chain
-// product planes (tr rows): reduce scratch | I patch band | Scharr band | 3 planes.
+// Large-window kernel (lk_kernel_lg, psn_lk_large.hip: box windows the box kernel
+// cannot hold in registers). Per workgroup an HBM slot of the window values
+// (3 x 256 x K uint2: I*, Ix*, Iy* of every quad as packed pairs, K quads per
+// thread) and LDS: the chain-check records | a union of one row band of the I
+// patch + Scharr plane (A phase) and the double-buffered tile planes of the
+// ordered-chain fallbacks (A: 3 planes of kLgTQA quads, b: 2 of kLgTQB).
 constexpr int kLgNT = 256;
-__host__ __device__ inline int lg_off_pimg() { return kRedBytes; }
-__host__ __device__ inline int lg_off_dg(int w, int tr) { return lg_off_pimg() + lk_tile_pimg_bytes(w, tr); }
-__host__ __device__ inline int lg_off_prod(int w, int tr) { return lg_off_dg(w, tr) + lk_tile_dg_bytes(w, tr); }
-__host__ __device__ inline int lg_lds_bytes(int w, int tr) { return lg_off_prod(w, tr) + lk_tile_prod_bytes(w, tr); }
-// window-value slot of one workgroup (int2 per pixel, 256-B aligned)
-__host__ __device__ inline long long lg_slot_int2(int w, int h) { return (((long long)w * h + 31) / 32) * 32; }
+constexpr int kLgTQA = 64;   // quads per A fallback tile
+constexpr int kLgTQB = 128;  // quads per b fallback tile
+constexpr int kLgTQE = 128;  // quads per err fallback tile (one row-major chain)
+__host__ __device__ constexpr int lg_sreg(int tq) { return ((tq + 15) & ~15) + 4; }  // SSE chain region (floats)
+__host__ __device__ constexpr int lg_plane(int tq) { return 4 * lg_sreg(tq) + ((4 * tq + 15) & ~15) + 4; }
+__host__ __device__ inline int lg_scr_bytes() { return align16((kBxXInts + 32) * 4); }
+__host__ __device__ inline int lg_tiles_bytes() {
+    const int a = 2 * 3 * lg_plane(kLgTQA) * 4, b = 2 * 2 * lg_plane(kLgTQB) * 4;
+    return (a > b ? a : b) + 1024;  // + slack: the chain sums read up to 5 blocks past a chain (discarded)
+}
+__host__ __device__ inline int lg_band_bytes(int w, int tr) { return lk_tile_pimg_bytes(w, tr) + lk_tile_dg_bytes(w, tr); }
+__host__ __device__ inline int lg_lds_bytes(int w, int tr) {
+    const int u = lg_band_bytes(w, tr), t = lg_tiles_bytes();
+    return lg_scr_bytes() + (u > t ? u : t);
+}
+__host__ __device__ inline int lg_quads_per_thread(int w, int h) { return (h * ((w + 3) >> 2) + kLgNT - 1) / kLgNT; }
+// window-value slot of one workgroup, in 8-byte units
+__host__ __device__ inline long long lg_slot_int2(int w, int h) { return 3LL * kLgNT * lg_quads_per_thread(w, h); }
 
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel
 constexpr int kStMaxLds = 150 * 1024;

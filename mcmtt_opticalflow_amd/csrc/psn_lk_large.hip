@@ -1,31 +1,38 @@
 // lk_kernel_lg: LKTrackerInvoker (OpenCV 2.4.6, reached from
-// PSNWhere_Tracker2D.cpp:776-782 backward and :871-877 forward) for windows the
-// LDS-resident kernels cannot hold -- Tracker2D box windows of any size
-// (forward w x h, backward w x w; e.g. 100x250 at 1080p, 128x320 at 4K).
+// PSNWhere_Tracker2D.cpp:776-782 backward and :871-877 forward) for the box
+// windows the box kernel cannot hold in registers -- Tracker2D windows of any
+// size (forward w x h, backward w x w; PETS-scale 100x250 at 1080p, 128x320 at
+// 4K).
 //
-// One workgroup per point, the grid striding over the launch's points; each
-// workgroup owns an HBM slot for the window values of the current level
-// ({I*, Ix* | Iy* << 16}, 8 B per window pixel, written once per level by the A
-// phase and streamed by every iteration -- L2 / MALL resident for Tracker2D box
-// sizes). LDS holds only one row band of the I patch, its Scharr plane and the
-// chain-major product planes of the ordered-sum fallbacks, so several
-// workgroups share a CU and hide each other's serial chains. J is read straight
-// from the pyramid level (reflect-101 addressing off the image interior).
+// The structure of lk_kernel_bx (psn_lk_kernels.hip) with the window values
+// streamed instead of register-resident. One workgroup (4 waves) per point, the
+// grid striding over the launch's points. The window is cut into quads (row y,
+// 4 pixels) in row-major order; thread t owns the CONTIGUOUS quads [t*K, t*K+K),
+// so for every SSE2 lane chain and the scalar tail chain its terms form one
+// contiguous run of the chain. Per level the A phase writes every quad's window
+// values -- (I*, Ix*, Iy*) of 4 pixels as packed 16-bit pairs, 24 B -- into the
+// workgroup's HBM slot (laid out [j][t], so thread t's j-th quads are one
+// coalesced load), and every iteration streams them back (L2 / MALL resident)
+// with the quad's J rows as two aligned dwords per row (packed-dot bilinear as
+// in lk_kernel_bx). Exactness of each float sum per chain by the run records
+// (total, maximum / minimum prefix) through one block scan; otherwise the
+// ordered chains from the first inexact half wave on, over tiles of consecutive
+// quads whose products are written chain-major into double-buffered LDS planes
+// while wave 0's chain lanes sum the previous tile. LDS holds only the tiles
+// (and, in the A phase, one row band of the I patch and its Scharr plane), so
+// several workgroups share a CU and hide each other's serial chains.
 //
-// Arithmetic and summation order are those of lk_kernel (psn_lk_kernels.hip):
-// integer window sums with the subset-sum exactness bound, otherwise the SSE2
-// chains summed in order, one lane per chain, band by band. Bit-identical to
-// oracle/lk_oracle.c.
-#include "psn_lk_device.h"
+// Bit-identical to oracle/lk_oracle.c (the SSE2 build's summation order, or the
+// scalar build's with PSN_LK_ACCUM_SCALAR).
+#include "psn_lk_bx.h"
 
 namespace psn {
 
-// bilinear J (DESCALE 9) at a window pixel whose 2x2 taps are inside the level
-__device__ __forceinline__ int lg_j_in(const uint8_t *p, int pitch, int w00, int w01, int w10, int w11) {
-    return PSN_DESCALE(p[0] * w00 + p[1] * w01 + p[pitch] * w10 + p[pitch + 1] * w11, 9);
-}
-// the same at level coordinates (gy, gx) with reflect-101 taps (the padded J
-// buffer of calcOpticalFlowPyrLK: copyMakeBorder(..., BORDER_REFLECT_101))
+// pair selector: bytes (s, s + 1) of a row's 8-byte window -> J[x] | J[x+1] << 16
+__device__ __forceinline__ unsigned lg_sel(int s) { return 0x0c000c00u | ((unsigned)(s + 1) << 16) | (unsigned)s; }
+
+// bilinear J (DESCALE 9) at level coordinates (gy, gx) with reflect-101 taps (the
+// padded J buffer of calcOpticalFlowPyrLK: copyMakeBorder(..., BORDER_REFLECT_101))
 __device__ __forceinline__ int lg_j_refl(const LevelDev &J, int gy, int gx, int w00, int w01, int w10, int w11) {
     const uint8_t *r0 = J.p + (long long)refl101(gy, J.h) * J.pitch;
     const uint8_t *r1 = J.p + (long long)refl101(gy + 1, J.h) * J.pitch;
@@ -33,35 +40,129 @@ __device__ __forceinline__ int lg_j_refl(const LevelDev &J, int gy, int gx, int 
     return PSN_DESCALE(r0[x0] * w00 + r0[x1] * w01 + r1[x0] * w10 + r1[x1] * w11, 9);
 }
 
-// J - I* and the gradients of window pixel (y, x), idx = y * w + x
-struct LgIter {
-    const uint8_t *jb;  // J at the window origin (interior only)
-    LevelDev J;
-    int pitch, iny, inx, w00, w01, w10, w11;
-    bool in;
-    __device__ __forceinline__ int jval(int y, int x) const {
-        return in ? lg_j_in(jb + (long long)y * pitch + x, pitch, w00, w01, w10, w11)
-                  : lg_j_refl(J, iny + y, inx + x, w00, w01, w10, w11);
-    }
+// Window geometry: quads per row, quads, quads per thread; the SSE2 chain split
+// of the b sums (8-pixel steps: nB2 quads per row, n8 pixels, tB tail pixels)
+// and of the A sums (4-pixel steps: nA quads, tA tail pixels).
+struct LgGeo {
+    int w, h, QW, NQ, K;
+    int nB2, n8, tB, nA, tA;
 };
-__device__ __forceinline__ LgIter lg_iter(const LevelDev &J, int inx, int iny, int w, int h, int w00, int w01, int w10,
-                                          int w11) {
-    LgIter it;
-    it.J = J;
-    it.pitch = J.pitch;
-    it.inx = inx;
-    it.iny = iny;
-    it.w00 = w00;
-    it.w01 = w01;
-    it.w10 = w10;
-    it.w11 = w11;
-    // the taps of every window pixel: columns inx .. inx + w, rows iny .. iny + h
-    it.in = inx >= 0 && iny >= 0 && inx + w + 1 <= J.w && iny + h + 1 <= J.h;
-    it.jb = it.in ? J.p + (long long)iny * J.pitch + inx : J.p;
-    return it;
+__device__ __forceinline__ LgGeo lg_geo(int w, int h, bool sse) {
+    LgGeo g;
+    g.w = w;
+    g.h = h;
+    g.QW = (w + 3) >> 2;
+    g.NQ = h * g.QW;
+    g.K = (g.NQ + kLgNT - 1) / kLgNT;
+    g.nB2 = sse ? 2 * (w / 8) : 0;
+    g.n8 = 4 * g.nB2;
+    g.tB = w - g.n8;
+    g.nA = sse ? w / 4 : 0;
+    g.tA = w - 4 * g.nA;
+    return g;
 }
-__device__ __forceinline__ int lg_gx(int v) { return (int)(short)(v & 0xffff); }
-__device__ __forceinline__ int lg_gy(int v) { return v >> 16; }
+// terms of the SSE chains (one per SSE quad) and of the tail chain before quad q
+__device__ __forceinline__ int lg_sse_before(const LgGeo &g, int q, int nS) {
+    const int y = q / g.QW;
+    return y * nS + min(q - y * g.QW, nS);
+}
+__device__ __forceinline__ int lg_tail_before(const LgGeo &g, int q, int nS, int t) {
+    const int y = q / g.QW;
+    return y * t + min(max(4 * (q - y * g.QW - nS), 0), t);
+}
+
+// One quad's J - I* (4 pixels) at window row y, quad column qx.
+struct LgJ {
+    const uint8_t *jb;  // interior: J at the window origin aligned down to a dword
+    LevelDev J;
+    int inx, iny, pitch;
+    unsigned W0, W1, s[4];
+    int w00, w01, w10, w11;
+    bool in;
+};
+__device__ __forceinline__ LgJ lg_j(const LevelDev &J, int inx, int iny, int w, int h, int w00, int w01, int w10,
+                                    int w11) {
+    LgJ r;
+    r.J = J;
+    r.inx = inx;
+    r.iny = iny;
+    r.pitch = J.pitch;
+    r.w00 = w00;
+    r.w01 = w01;
+    r.w10 = w10;
+    r.w11 = w11;
+    r.W0 = pack_w(w00, w01);
+    r.W1 = pack_w(w10, w11);
+    // every tap of the window (columns inx .. inx + w, rows iny .. iny + h) inside the level
+    r.in = inx >= 0 && iny >= 0 && inx + w + 1 <= J.w && iny + h + 1 <= J.h;
+    const int sh = r.in ? (inx & 3) : 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) r.s[i] = lg_sel(sh + i);
+    r.jb = r.in ? J.p + (long long)iny * J.pitch + (inx - sh) : J.p;
+    return r;
+}
+// d[i] = DESCALE(bilinear J, 9) - I of the quad's pixels (ip: I* as packed pairs);
+// the diff is folded into the dot product's accumulator: (v + 256 - 512 I) >> 9
+__device__ __forceinline__ void lg_diffs(const LgJ &J, int y, int qx, const uint2 &ip, int (&d)[4]) {
+    const int I[4] = {lo16(ip.x), hi16(ip.x), lo16(ip.y), hi16(ip.y)};
+    if (J.in) {
+        const uint32_t *r0 = (const uint32_t *)(J.jb + (long long)y * J.pitch + 4 * qx);
+        const uint32_t *r1 = (const uint32_t *)((const uint8_t *)r0 + J.pitch);
+        const uint32_t a0 = r0[0], a1 = r0[1], b0 = r1[0], b1 = r1[1];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            d[i] = sdot2(__builtin_amdgcn_perm(b1, b0, J.s[i]), J.W1,
+                         sdot2(__builtin_amdgcn_perm(a1, a0, J.s[i]), J.W0, 256 - 512 * I[i])) >> 9;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            d[i] = lg_j_refl(J.J, J.iny + y, J.inx + 4 * qx + i, J.w00, J.w01, J.w10, J.w11) - I[i];
+    }
+}
+
+// LDS tile planes of the ordered-chain fallbacks (psn_lk_kernels.h): per plane 4
+// SSE chain regions of up to TQ terms and a tail region of up to 4*TQ terms
+// (16-float blocks + 4: conflict-free across the chain lanes' 16-B reads)
+
+// Ordered chains from quad qs on, tile by tile: `write(tile quad range, buffer)`
+// writes the tile's products (every thread at most one quad), chain lanes
+// (wave 0, lanes < NCH) zero their regions' pads and sum; double-buffered, one
+// barrier per tile. Returns acc (chain lanes: their chain's sum onto its base).
+template <int NPL, int TQ, typename Write, typename Geo>
+__device__ __forceinline__ float lg_tiles(int qs, int NQ, float *buf, int nch, float acc, Write write, Geo geo) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int PL = lg_plane(TQ), SR = lg_sreg(TQ);
+    const bool chl = tid < nch;
+    const int cs = lane / 5, cc = lane - 5 * cs;
+    const int ntiles = (NQ - qs + TQ - 1) / TQ;
+    auto region = [&](float *b) { return b + cs * PL + (cc < 4 ? cc * SR : 4 * SR); };
+    auto pad = [&](int g, float *b) {
+        if (!chl) return;
+        int nsse, ntail;
+        geo(qs + g * TQ, min(qs + (g + 1) * TQ, NQ), nsse, ntail);
+        const int len = cc < 4 ? nsse : ntail;
+        float *rg = region(b);
+        for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
+    };
+    if (ntiles <= 0) return acc;
+    write(qs, min(qs + TQ, NQ), buf);
+    pad(0, buf);
+    __syncthreads();
+    for (int g = 0; g < ntiles; g++) {
+        float *cur = buf + (g & 1) * NPL * PL, *nxt = buf + ((g + 1) & 1) * NPL * PL;
+        if (g + 1 < ntiles) write(qs + (g + 1) * TQ, min(qs + (g + 2) * TQ, NQ), nxt);
+        if (tid < 64) {
+            int nsse, ntail;
+            geo(qs + g * TQ, min(qs + (g + 1) * TQ, NQ), nsse, ntail);
+            const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
+            const int nbmax = __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
+            if (chl) acc = chain_sum_pl<false>(region(cur), len, nbmax, acc);
+            if (g + 1 < ntiles) pad(g + 1, nxt);
+        }
+        __syncthreads();
+    }
+    return acc;
+}
 
 // Diagnostic phase clocks (PSN_LK_STAMPS build, tools/lg_stamps.py): accumulated
 // s_memtime ticks per phase of each point, thread 0's view, stamps[point][0..15].
@@ -84,29 +185,37 @@ __device__ __forceinline__ int lg_gy(int v) { return v >> 16; }
     } while (0)
 #endif
 
-template <int NT>
-__global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
+__global__ __launch_bounds__(kLgNT, 4) void lk_kernel_lg(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int tid = threadIdx.x;
-    float *RED = (float *)smem;
-    int *REDI = (int *)(RED + 48);  // 16 ints of block-reduce scratch
-    int2 *WV = A.lg_ws + (long long)blockIdx.x * A.lg_slot;
+    constexpr int NT = kLgNT;
+    const int tid = threadIdx.x, lane = tid & 63;
+    int *X = (int *)smem;                 // chain-check records, two parities
+    float *RS = (float *)(X + kBxXInts);  // results (wave 0 -> all), err partials
+    int *EP = (int *)(RS + 16);
+    uint8_t *U = smem + lg_scr_bytes();   // band staging | tile planes
+    float *PL = (float *)U;
+    uint8_t *const slot = (uint8_t *)A.lg_ws + (long long)blockIdx.x * A.lg_slot * 8;
     const float FLT_SCALE = 1.f / (1 << 20);
+    int par = 0;
 
-    for (int g = blockIdx.x; g < A.lk_wgs; g += gridDim.x) {
+    for (int gi = blockIdx.x; gi < A.lk_wgs; gi += gridDim.x) {
+        const int g = gi;
         int qi = 0;
         while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
         const LkQueryDev &Q = A.q[qi];
         if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) continue;  // past the query's device count
         const int pi = Q.pt_begin + (g - Q.wg_begin);
-        const int w = Q.win_w, h = Q.win_h, wh = w * h;
-        const int TR = Q.tile_rows;
+        const int w = Q.win_w, h = Q.win_h, TR = Q.tile_rows;
         const int maxL = Q.max_level, flags = Q.flags;
         const bool sse = (flags & PSN_LK_ACCUM_SCALAR) == 0;
+        const LgGeo G = lg_geo(w, h, sse);
+        const int K = G.K, QW = G.QW, NQ = G.NQ;
+        uint2 *IPs = (uint2 *)slot, *XPs = IPs + NT * K, *YPs = XPs + NT * K;
+        const int q0 = min(tid * K, NQ), cnt = min(NQ - q0, K);  // this thread's quads [q0, q0 + cnt)
+        const int y0 = q0 / QW, x0 = q0 - y0 * QW;
         const int PW = w + 3, DW = w + 1;
-        uint8_t *Pimg = smem + lg_off_pimg();
-        short2 *Dg = (short2 *)(smem + lg_off_dg(w, TR));
-        float *Prod = (float *)(smem + lg_off_prod(w, TR));
+        uint8_t *Pimg = U;
+        short2 *Dg = (short2 *)(U + lk_tile_pimg_bytes(w, TR));
 
         const float hwx = __fmul_rn((float)(w - 1), 0.5f), hwy = __fmul_rn((float)(h - 1), 0.5f);
         const float px0 = A.prev[2 * pi], py0 = A.prev[2 * pi + 1];
@@ -159,15 +268,13 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
             bilin_weights(__fsub_rn(px, (float)ipx), __fsub_rn(py, (float)ipy), iw00, iw01, iw10, iw11);
             nx = __fsub_rn(nx, hwx);
             ny = __fsub_rn(ny, hwy);
-
-            // ---- A phase, band by band: I patch rows -> Scharr -> window values
-            // into the HBM slot, integer structure-tensor sums ----
             nwin++;
-            int sA11 = 0, sA12 = 0;
-            unsigned aA12 = 0, sA22 = 0;
+
+            // ---- A phase (1): window values, band by band (every thread on the
+            // band's quads): I patch rows -> Scharr -> bilinear I*, Ix*, Iy* ----
             for (int r0 = 0; r0 < h; r0 += TR) {
                 const int th = min(TR, h - r0);
-                __syncthreads();  // the previous band's (level's, point's) LDS readers are done
+                __syncthreads();  // the previous band's (tile's, level's, point's) LDS readers are done
                 stage_one<NT>(Pimg, I, ipy + r0 - 1, ipx - 1, PW, th + 3);
                 __syncthreads();
                 {  // Scharr on (th+1) x (w+1) positions; zero outside the image
@@ -193,74 +300,160 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
                 __syncthreads();
                 {
                     Walk wk;
-                    wk.init(tid, NT, w);
-                    for (int idx = tid; idx < th * w; idx += NT, wk.step()) {
-                        const int yl = wk.y, x = wk.x;
-                        const uint8_t *p = Pimg + (yl + 1) * PW + x + 1;
-                        const int ival = PSN_DESCALE(p[0] * iw00 + p[1] * iw01 + p[PW] * iw10 + p[PW + 1] * iw11, 9);
-                        const short2 *d = Dg + yl * DW + x;
-                        const int ixv = PSN_DESCALE(d[0].x * iw00 + d[1].x * iw01 + d[DW].x * iw10 + d[DW + 1].x * iw11, 14);
-                        const int iyv = PSN_DESCALE(d[0].y * iw00 + d[1].y * iw01 + d[DW].y * iw10 + d[DW + 1].y * iw11, 14);
-                        WV[r0 * w + idx] = make_int2(ival, (ixv & 0xffff) | (iyv << 16));
-                        const int xy = ixv * iyv;
-                        sA11 = (int)sat_add((unsigned)sA11, (unsigned)(ixv * ixv));
-                        sA12 += xy;
-                        aA12 = sat_add(aA12, (unsigned)abs(xy));
-                        sA22 = sat_add(sA22, (unsigned)(iyv * iyv));
+                    wk.init(tid, NT, QW);
+                    for (int qb = tid; qb < th * QW; qb += NT, wk.step()) {
+                        const int yl = wk.y, qx = wk.x;
+                        int iv[4], gxv[4], gyv[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int x = 4 * qx + i;
+                            iv[i] = gxv[i] = gyv[i] = 0;
+                            if (x < w) {
+                                const uint8_t *p = Pimg + (yl + 1) * PW + x + 1;
+                                iv[i] = PSN_DESCALE(p[0] * iw00 + p[1] * iw01 + p[PW] * iw10 + p[PW + 1] * iw11, 9);
+                                const short2 *d = Dg + yl * DW + x;
+                                gxv[i] = PSN_DESCALE(d[0].x * iw00 + d[1].x * iw01 + d[DW].x * iw10 + d[DW + 1].x * iw11, 14);
+                                gyv[i] = PSN_DESCALE(d[0].y * iw00 + d[1].y * iw01 + d[DW].y * iw10 + d[DW + 1].y * iw11, 14);
+                            }
+                        }
+                        const int q = (r0 + yl) * QW + qx, t = q / K, idx = (q - t * K) * NT + t;
+                        IPs[idx] = make_uint2(pack_w(iv[0], iv[1]), pack_w(iv[2], iv[3]));
+                        XPs[idx] = make_uint2(pack_w(gxv[0], gxv[1]), pack_w(gxv[2], gxv[3]));
+                        YPs[idx] = make_uint2(pack_w(gyv[0], gyv[1]), pack_w(gyv[2], gyv[3]));
                     }
                 }
             }
-            // (the reduce's barrier also publishes the slot's window values to the workgroup)
-            block_reduce4<NT, true>(sA11, sA12, aA12, sA22, REDI);
-            LG_MARK(0);  // A phase: I bands, Scharr, window values, integer sums
-            const bool ex11 = sA11 <= kExact, ex12 = aA12 <= (unsigned)kExact, ex22 = sA22 <= (unsigned)kExact;
-            float A11 = (float)sA11, A12 = (float)sA12, A22 = (float)sA22;
-            if (!(ex11 && ex12 && ex22)) {
-                // ordered float chains over (float)(Ix*Ix), (float)(Ix*Iy), (float)(Iy*Iy)
-                float acc = 0.f;
-                for (int r0 = 0; r0 < h; r0 += TR) {
-                    const int th = min(TR, h - r0);
-                    const ChainA C(w, th, sse);
-                    __syncthreads();  // chain lanes done with the previous band
-                    Walk wk;
-                    wk.init(tid, NT, w);
-                    for (int idx = tid; idx < th * w; idx += NT, wk.step()) {
-                        const int v = WV[r0 * w + idx].y;
-                        const int gx = lg_gx(v), gy = lg_gy(v);
-                        const int pos = C.pos(wk.y, wk.x);
-                        Prod[pos] = (float)(gx * gx);
-                        Prod[C.P + pos] = (float)(gx * gy);
-                        Prod[2 * C.P + pos] = (float)(gy * gy);
+            __syncthreads();  // the window values of every band for every thread
+            LG_MARK(0);  // A phase: window values
+
+            // ---- A phase (2): the 15 A chains (sum x class) as runs over the
+            // thread's quads, the block check, ordered chains if inexact ----
+            float A11, A12, A22;
+            int gmax = 0;  // max |Ix|, |Iy| of the thread's pixels (exactness of the b terms)
+            {
+                int T11[5] = {0, 0, 0, 0, 0}, T22[5] = {0, 0, 0, 0, 0}, T12[5] = {0, 0, 0, 0, 0};
+                int M12[5] = {0, 0, 0, 0, 0}, m12[5] = {0, 0, 0, 0, 0};
+                int qx = x0;
+                for (int j = 0; j < cnt; j++) {
+                    const uint2 xp = XPs[j * NT + tid], yp = YPs[j * NT + tid];
+                    const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
+                    const int gy[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
+                    // (A11 / A22 runs saturate at 2^30: a long run never wraps; a run past 2^25
+                    // fails the check below, as it must)
+                    if (qx < G.nA) {  // SSE2 quad: pixel i feeds lane chain i
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            T11[i] = (int)sat_add((unsigned)T11[i], (unsigned)(gx[i] * gx[i]));
+                            T22[i] = (int)sat_add((unsigned)T22[i], (unsigned)(gy[i] * gy[i]));
+                            run_add(T12[i], M12[i], m12[i], gx[i] * gy[i]);
+                        }
+                    } else {  // the tail chain, in order (pixels past w carry zero gradients)
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            T11[4] = (int)sat_add((unsigned)T11[4], (unsigned)(gx[i] * gx[i]));
+                            T22[4] = (int)sat_add((unsigned)T22[4], (unsigned)(gy[i] * gy[i]));
+                            run_add(T12[4], M12[4], m12[4], gx[i] * gy[i]);
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++) gmax = max(gmax, max(abs(gx[i]), abs(gy[i])));
+                    if (++qx == QW) qx = 0;
+                }
+                // A11 / A22 terms are >= 0: the maximum prefix is the total
+                int T[15], M[15], m[15];
+#pragma unroll
+                for (int c = 0; c < 5; c++) {
+                    T[c] = T11[c], M[c] = T11[c], m[c] = 0;
+                    T[5 + c] = T12[c], M[5 + c] = M12[c], m[5 + c] = m12[c];
+                    T[10 + c] = T22[c], M[10 + c] = T22[c], m[10 + c] = 0;
+                }
+                // a run whose own prefix leaves [-2^25, 2^25] cannot stay exact after any
+                // exact start (|start| <= 2^24): flag it (long runs never wrap unseen)
+                bool badA = false;
+#pragma unroll
+                for (int c = 0; c < 15; c++) badA |= M[c] > (1 << 25) || m[c] < -(1 << 25);
+                int *rec = X + par * 4 * kBxRecInts;
+                par ^= 1;
+                bx_publish<15>(T, rec, G.tA == 0);
+                __syncthreads();
+                bx_check<15>(T, M, m, badA, rec, G.tA == 0);
+                __syncthreads();
+                int tot, h0, base0;
+                const bool exact = bx_eval<15>(rec, tot, h0, base0);
+                float s3[3];
+                if (exact) {
+#pragma unroll
+                    for (int s = 0; s < 3; s++) {
+                        float t = rl_f(tot, 5 * s + 4);
+                        if (sse)
+                            t = __fadd_rn(t, __fadd_rn(__fadd_rn(__fadd_rn(rl_f(tot, 5 * s), rl_f(tot, 5 * s + 1)),
+                                                                 rl_f(tot, 5 * s + 2)), rl_f(tot, 5 * s + 3)));
+                        s3[s] = t;
+                    }
+                } else {
+                    // ordered chains from half wave h0 on (every earlier prefix is an exact
+                    // integer: the chain lanes start from base0)
+                    const int qs = min(h0 * 32 * K, NQ);
+                    auto geoA = [&](int a, int b, int &nsse, int &ntail) {
+                        nsse = lg_sse_before(G, b, G.nA) - lg_sse_before(G, a, G.nA);
+                        ntail = lg_tail_before(G, b, G.nA, G.tA) - lg_tail_before(G, a, G.nA, G.tA);
+                    };
+                    auto writeA = [&](int a, int b, float *buf) {
+                        const int q = a + tid;
+                        if (q >= b) return;
+                        const int t = q / K, idx = (q - t * K) * NT + t;
+                        const uint2 xp = XPs[idx], yp = YPs[idx];
+                        const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
+                        const int gy[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
+                        const int PLA = lg_plane(kLgTQA), SR = lg_sreg(kLgTQA);
+                        const int y = q / QW, qx = q - y * QW;
+                        if (qx < G.nA) {
+                            const int pos = lg_sse_before(G, q, G.nA) - lg_sse_before(G, a, G.nA);
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                float *p = buf + i * SR + pos;
+                                p[0] = (float)(gx[i] * gx[i]);
+                                p[PLA] = (float)(gx[i] * gy[i]);
+                                p[2 * PLA] = (float)(gy[i] * gy[i]);
+                            }
+                        } else {
+                            const int pos = lg_tail_before(G, q, G.nA, G.tA) - lg_tail_before(G, a, G.nA, G.tA);
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                if (4 * qx + i >= w) break;
+                                float *p = buf + 4 * SR + pos + i;
+                                p[0] = (float)(gx[i] * gx[i]);
+                                p[PLA] = (float)(gx[i] * gy[i]);
+                                p[2 * PLA] = (float)(gy[i] * gy[i]);
+                            }
+                        }
+                    };
+                    float acc = lg_tiles<3, kLgTQA>(qs, NQ, PL, 15, (float)base0, writeA, geoA);
+                    if (tid < 64) {  // wave 0 combines in the SSE2 build's order
+                        const int av = __float_as_int(acc);
+#pragma unroll
+                        for (int s = 0; s < 3; s++) {
+                            float t = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 4));
+                            if (sse) {
+                                const float c0 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s));
+                                const float c1 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 1));
+                                const float c2 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 2));
+                                const float c3 = __int_as_float(__builtin_amdgcn_readlane(av, 5 * s + 3));
+                                t = __fadd_rn(t, __fadd_rn(__fadd_rn(__fadd_rn(c0, c1), c2), c3));
+                            }
+                            if (tid == 0) RS[s] = t;
+                        }
                     }
                     __syncthreads();
-                    if (tid < 15) {
-                        const int ch = tid % 5, s = tid / 5;
-                        const int base = ch < 4 ? ch * C.SA : 4 * C.SA;
-                        const int len = ch < 4 ? th * C.nA : th * C.tA;
-                        acc = chain_sum(Prod + s * C.P + base, len, acc);
-                    }
+                    s3[0] = RS[0];
+                    s3[1] = RS[1];
+                    s3[2] = RS[2];
                 }
-                if (tid < 15) RED[tid] = acc;
-                __syncthreads();
-                float s3[3];
-#pragma unroll
-                for (int s = 0; s < 3; s++) {
-                    float tail = RED[s * 5 + 4];
-                    if (sse) {
-                        const float q = __fadd_rn(__fadd_rn(__fadd_rn(RED[s * 5 + 0], RED[s * 5 + 1]), RED[s * 5 + 2]), RED[s * 5 + 3]);
-                        tail = __fadd_rn(tail, q);
-                    }
-                    s3[s] = tail;
-                }
-                if (!ex11) A11 = s3[0];
-                if (!ex12) A12 = s3[1];
-                if (!ex22) A22 = s3[2];
-                __syncthreads();  // RED read by all before any later write
+                A11 = __fmul_rn(s3[0], FLT_SCALE);
+                A12 = __fmul_rn(s3[1], FLT_SCALE);
+                A22 = __fmul_rn(s3[2], FLT_SCALE);
             }
-            LG_MARK(1);  // A ordered chains
-            A11 = __fmul_rn(A11, FLT_SCALE);
-            A12 = __fmul_rn(A12, FLT_SCALE);
-            A22 = __fmul_rn(A22, FLT_SCALE);
+            LG_MARK(1);  // A chains
             float D = __fsub_rn(__fmul_rn(A11, A22), __fmul_rn(A12, A12));
             {
                 const float dd = __fsub_rn(A11, A22);
@@ -273,8 +466,8 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
                 }
             }
             D = __fdiv_rn(1.f, D);
-            float pdx = 0.f, pdy = 0.f;
 
+            float pdx = 0.f, pdy = 0.f;
             for (int j = 0; j < Q.max_count; j++) {
                 const int inx = cv_floor(nx), iny = cv_floor(ny);
                 if (inx < -w || inx >= cols || iny < -h || iny >= rows) {
@@ -284,71 +477,138 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
                 nwin++;
                 int w00, w01, w10, w11;
                 bilin_weights(__fsub_rn(nx, (float)inx), __fsub_rn(ny, (float)iny), w00, w01, w10, w11);
-                const LgIter it = lg_iter(J, inx, iny, w, h, w00, w01, w10, w11);
-                int s1 = 0, s2 = 0;
-                unsigned a1 = 0, a2 = 0;
+                const LgJ JJ = lg_j(J, inx, iny, w, h, w00, w01, w10, w11);
+                // ---- main pass: the thread's quads in order, the 10 b chains as runs ----
+                int T1[5] = {0, 0, 0, 0, 0}, M1[5] = {0, 0, 0, 0, 0}, m1[5] = {0, 0, 0, 0, 0};
+                int T2[5] = {0, 0, 0, 0, 0}, M2[5] = {0, 0, 0, 0, 0}, m2[5] = {0, 0, 0, 0, 0};
+                int dmax = 0;
                 {
-                    Walk wk;
-                    wk.init(tid, NT, w);
-#pragma unroll 2
-                    for (int idx = tid; idx < wh; idx += NT, wk.step()) {
-                        const int2 v = WV[idx];
-                        const int diff = it.jval(wk.y, wk.x) - v.x;
-                        const int t1 = diff * lg_gx(v.y), t2 = diff * lg_gy(v.y);
-                        s1 += t1;
-                        s2 += t2;
-                        a1 = sat_add(a1, (unsigned)abs(t1));
-                        a2 = sat_add(a2, (unsigned)abs(t2));
+                    int y = y0, qx = x0;
+                    for (int k = 0; k < cnt; k++) {
+                        const int ix = k * NT + tid;
+                        const uint2 ip = IPs[ix], xp = XPs[ix], yp = YPs[ix];
+                        int d[4];
+                        lg_diffs(JJ, y, qx, ip, d);
+                        const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
+                        const int gy[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
+                        if (qx < G.nB2) {  // SSE2 quad: pixel i feeds lane chain i
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                run_add(T1[i], M1[i], m1[i], __mul24(d[i], gx[i]));
+                                run_add(T2[i], M2[i], m2[i], __mul24(d[i], gy[i]));
+                            }
+                        } else {  // the tail chain, in order (pixels past w: zero gradients)
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                run_add(T1[4], M1[4], m1[4], __mul24(d[i], gx[i]));
+                                run_add(T2[4], M2[4], m2[4], __mul24(d[i], gy[i]));
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (4 * qx + i < w) dmax = max(dmax, abs(d[i]));
+                        if (++qx == QW) {
+                            qx = 0;
+                            y++;
+                        }
                     }
                 }
                 LG_MARK(2);  // main pass
                 LG_COUNT(10);
-                block_reduce4<NT, false>(s1, s2, a1, a2, REDI);
-                LG_MARK(3);  // reduce
+                // every term is an exact float unless |d| * |g| > 2^24; a run past
+                // [-2^25, 2^25] (terms < 2^26: seen before any wrap) cannot be exact
+                bool bad = (long long)dmax * gmax > (long long)kExact;
+                int T[10], M[10], m[10];
+#pragma unroll
+                for (int c = 0; c < 5; c++) {
+                    T[c] = T1[c], M[c] = M1[c], m[c] = m1[c];
+                    T[5 + c] = T2[c], M[5 + c] = M2[c], m[5 + c] = m2[c];
+                }
+#pragma unroll
+                for (int c = 0; c < 10; c++) bad |= M[c] > (1 << 25) || m[c] < -(1 << 25);
+                int *rec = X + par * 4 * kBxRecInts;
+                par ^= 1;
+                bx_publish<10>(T, rec, G.tB == 0);
+                __syncthreads();
+                bx_check<10>(T, M, m, bad, rec, G.tB == 0);
+                __syncthreads();
+                int tot, h0, base0;
+                const bool bex = bx_eval<10>(rec, tot, h0, base0);
+                LG_MARK(3);  // publish / check / eval
                 float b1, b2;
-                if (sums_exact(a1, s1) && sums_exact(a2, s2)) {  // subset-sum bound (see sums_exact)
-                    b1 = (float)s1;
-                    b2 = (float)s2;
+                if (bex) {
+                    b1 = rl_f(tot, 4);
+                    b2 = rl_f(tot, 9);
+                    if (sse) {
+                        b1 = __fadd_rn(b1, __fadd_rn(__fadd_rn(rl_f(tot, 0), rl_f(tot, 2)), __fadd_rn(rl_f(tot, 1), rl_f(tot, 3))));
+                        b2 = __fadd_rn(b2, __fadd_rn(__fadd_rn(rl_f(tot, 5), rl_f(tot, 7)), __fadd_rn(rl_f(tot, 6), rl_f(tot, 8))));
+                    }
                 } else {
                     LG_COUNT(11);
-                    float bacc = 0.f;
-                    for (int r0 = 0; r0 < h; r0 += TR) {
-                        const int th = min(TR, h - r0);
-                        const ChainB C(w, th, sse);
-                        __syncthreads();  // chain lanes done with the previous band / reduce scratch
-                        Walk wk;
-                        wk.init(tid, NT, w);
-                        for (int idx = tid; idx < th * w; idx += NT, wk.step()) {
-                            const int2 v = WV[r0 * w + idx];
-                            const int diff = it.jval(r0 + wk.y, wk.x) - v.x;
-                            const int pos = C.pos(wk.y, wk.x);
-                            Prod[pos] = (float)(diff * lg_gx(v.y));
-                            Prod[C.P + pos] = (float)(diff * lg_gy(v.y));
+                    // ordered float chains from half wave h0 on (chain lanes: wave 0, lanes
+                    // 0-9, from their exact prefixes base0), tiles of kLgTQB quads
+                    const int qs = min(h0 * 32 * K, NQ);
+                    auto geoB = [&](int a, int b, int &nsse, int &ntail) {
+                        nsse = lg_sse_before(G, b, G.nB2) - lg_sse_before(G, a, G.nB2);
+                        ntail = lg_tail_before(G, b, G.nB2, G.tB) - lg_tail_before(G, a, G.nB2, G.tB);
+                    };
+                    auto writeB = [&](int a, int b, float *buf) {
+                        const int q = a + tid;
+                        if (q >= b) return;
+                        const int t = q / K, idx = (q - t * K) * NT + t;
+                        const int y = q / QW, qx = q - y * QW;
+                        const uint2 ip = IPs[idx], xp = XPs[idx], yp = YPs[idx];
+                        int d[4];
+                        lg_diffs(JJ, y, qx, ip, d);
+                        const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
+                        const int gy[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
+                        const int PLB = lg_plane(kLgTQB), SR = lg_sreg(kLgTQB);
+                        if (qx < G.nB2) {
+                            const int pos = lg_sse_before(G, q, G.nB2) - lg_sse_before(G, a, G.nB2);
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                float *p = buf + i * SR + pos;
+                                p[0] = (float)__mul24(d[i], gx[i]);
+                                p[PLB] = (float)__mul24(d[i], gy[i]);
+                            }
+                        } else {
+                            const int pos = lg_tail_before(G, q, G.nB2, G.tB) - lg_tail_before(G, a, G.nB2, G.tB);
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                if (4 * qx + i >= w) break;
+                                float *p = buf + 4 * SR + pos + i;
+                                p[0] = (float)__mul24(d[i], gx[i]);
+                                p[PLB] = (float)__mul24(d[i], gy[i]);
+                            }
                         }
-                        __syncthreads();
-                        LG_MARK(4);  // fallback: band products
-                        if (tid < 10) {
-                            const int ch = tid % 5, s = tid / 5;
-                            const int base = ch < 4 ? ch * C.SB : 4 * C.SB;
-                            const int len = ch < 4 ? th * 2 * C.nB : th * C.tB;
-                            bacc = chain_sum(Prod + s * C.P + base, len, bacc);
+                    };
+                    LG_MARK(4);
+                    const float acc = lg_tiles<2, kLgTQB>(qs, NQ, PL, 10, (float)base0, writeB, geoB);
+                    LG_MARK(5);  // ordered b chains
+                    if (tid < 64) {  // wave 0 combines in the SSE2 build's order
+                        const int a = __float_as_int(acc);
+                        float r1 = __int_as_float(__builtin_amdgcn_readlane(a, 4));
+                        float r2 = __int_as_float(__builtin_amdgcn_readlane(a, 9));
+                        if (sse) {
+                            const float bb0 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 0)),
+                                                        __int_as_float(__builtin_amdgcn_readlane(a, 2)));
+                            const float bb2 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 1)),
+                                                        __int_as_float(__builtin_amdgcn_readlane(a, 3)));
+                            const float bb1 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 5)),
+                                                        __int_as_float(__builtin_amdgcn_readlane(a, 7)));
+                            const float bb3 = __fadd_rn(__int_as_float(__builtin_amdgcn_readlane(a, 6)),
+                                                        __int_as_float(__builtin_amdgcn_readlane(a, 8)));
+                            r1 = __fadd_rn(r1, __fadd_rn(bb0, bb2));
+                            r2 = __fadd_rn(r2, __fadd_rn(bb1, bb3));
                         }
-                        LG_MARK(5);  // fallback: chain sums
+                        if (tid == 0) {
+                            RS[4] = r1;
+                            RS[5] = r2;
+                        }
                     }
-                    if (tid < 10) RED[16 + tid] = bacc;
                     __syncthreads();
-                    b1 = RED[16 + 4];
-                    b2 = RED[16 + 9];
-                    if (sse) {
-                        // bbuf = qb0 + qb1; b1 += bbuf[0] + bbuf[2]; b2 += bbuf[1] + bbuf[3]
-                        const float bb0 = __fadd_rn(RED[16 + 0], RED[16 + 2]);
-                        const float bb2 = __fadd_rn(RED[16 + 1], RED[16 + 3]);
-                        const float bb1 = __fadd_rn(RED[16 + 5], RED[16 + 7]);
-                        const float bb3 = __fadd_rn(RED[16 + 6], RED[16 + 8]);
-                        b1 = __fadd_rn(b1, __fadd_rn(bb0, bb2));
-                        b2 = __fadd_rn(b2, __fadd_rn(bb1, bb3));
-                    }
-                    __syncthreads();  // RED read by all before any later write
+                    b1 = RS[4];
+                    b2 = RS[5];
                 }
                 LG_MARK(6);  // results
                 b1 = __fmul_rn(b1, FLT_SCALE);
@@ -371,44 +631,60 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
             }
 
             if (level == 0 && status && A.err && (flags & PSN_LK_GET_MIN_EIGENVALS) == 0) {
-                const float qx = __fsub_rn(NPx, hwx), qy = __fsub_rn(NPy, hwy);
-                const int iqx = cv_floor(qx), iqy = cv_floor(qy);
+                const float qxf = __fsub_rn(NPx, hwx), qyf = __fsub_rn(NPy, hwy);
+                const int iqx = cv_floor(qxf), iqy = cv_floor(qyf);
                 if (iqx < -w || iqx >= cols || iqy < -h || iqy >= rows) {
                     status = 0;
                     continue;
                 }
                 int w00, w01, w10, w11;
-                bilin_weights(__fsub_rn(qx, (float)iqx), __fsub_rn(qy, (float)iqy), w00, w01, w10, w11);
-                const LgIter it = lg_iter(J, iqx, iqy, w, h, w00, w01, w10, w11);
-                int e0 = 0, e1 = 0;
-                unsigned e2 = 0, e3 = 0;
+                bilin_weights(__fsub_rn(qxf, (float)iqx), __fsub_rn(qyf, (float)iqy), w00, w01, w10, w11);
+                const LgJ JJ = lg_j(J, iqx, iqy, w, h, w00, w01, w10, w11);
+                unsigned e = 0;
                 {
-                    Walk wk;
-                    wk.init(tid, NT, w);
-                    for (int idx = tid; idx < wh; idx += NT, wk.step())
-                        e2 = sat_add(e2, (unsigned)abs(it.jval(wk.y, wk.x) - WV[idx].x));
-                }
-                block_reduce4<NT, false>(e0, e1, e2, e3, REDI);
-                float errval;
-                if (e2 <= (unsigned)kExact) {
-                    // every partial sum of errval += |diff| is an integer <= 2^24: exact
-                    errval = (float)e2;
-                } else {  // row-major order, one lane, band by band
-                    float eacc = 0.f;
-                    for (int r0 = 0; r0 < h; r0 += TR) {
-                        const int th = min(TR, h - r0);
-                        __syncthreads();
-                        Walk wk;
-                        wk.init(tid, NT, w);
-                        for (int idx = tid; idx < th * w; idx += NT, wk.step())
-                            Prod[idx] = (float)abs(it.jval(r0 + wk.y, wk.x) - WV[r0 * w + idx].x);
-                        __syncthreads();
-                        if (tid == 0) eacc = chain_sum(Prod, th * w, eacc);
+                    int y = y0, qx = x0;
+                    for (int k = 0; k < cnt; k++) {
+                        int d[4];
+                        lg_diffs(JJ, y, qx, IPs[k * NT + tid], d);
+#pragma unroll
+                        for (int i = 0; i < 4; i++)
+                            if (4 * qx + i < w) e = sat_add(e, (unsigned)abs(d[i]));
+                        if (++qx == QW) {
+                            qx = 0;
+                            y++;
+                        }
                     }
-                    if (tid == 0) RED[32] = eacc;
+                }
+                e = wave_sum_sat(e);
+                if (lane == 0) EP[tid >> 6] = (int)e;
+                __syncthreads();
+                const unsigned et = sat_add(sat_add((unsigned)EP[0], (unsigned)EP[1]), sat_add((unsigned)EP[2], (unsigned)EP[3]));
+                float errval;
+                if (et <= (unsigned)kExact) {
+                    errval = (float)et;  // every partial sum of errval += |diff| is an exact integer
+                } else {  // row-major order, one lane, tiles of kLgTQE quads
+                    float acc = 0.f;
+                    for (int a = 0; a < NQ; a += kLgTQE) {
+                        const int b = min(a + kLgTQE, NQ);
+                        const int pa = (a / QW) * w + 4 * (a % QW);  // row-major pixel index of quad a
+                        __syncthreads();
+                        const int q = a + tid;
+                        if (q < b) {
+                            const int t = q / K, idx = (q - t * K) * NT + t;
+                            const int y = q / QW, qx = q - y * QW;
+                            int d[4];
+                            lg_diffs(JJ, y, qx, IPs[idx], d);
+#pragma unroll
+                            for (int i = 0; i < 4; i++)
+                                if (4 * qx + i < w) PL[y * w + 4 * qx + i - pa] = (float)abs(d[i]);
+                        }
+                        __syncthreads();
+                        const int pb = b < NQ ? (b / QW) * w + 4 * (b % QW) : w * h;
+                        if (tid == 0) acc = chain_sum(PL, pb - pa, acc);
+                    }
+                    if (tid == 0) RS[8] = acc;
                     __syncthreads();
-                    errval = RED[32];
-                    __syncthreads();  // RED read by all before any later write
+                    errval = RS[8];
                 }
                 errv = __fdiv_rn(__fmul_rn(errval, 1.f), (float)(32 * w * h));
             }
@@ -428,21 +704,21 @@ __global__ __launch_bounds__(NT) void lk_kernel_lg(LkLaunchArgs A) {
             A.next[2 * pi + 1] = NPy;
             A.status[pi] = (uint8_t)status;
             if (A.err) A.err[pi] = errv;
-            if (A.samples) atomicAdd(A.samples, (unsigned long long)nwin * (unsigned)wh);
+            if (A.samples) atomicAdd(A.samples, (unsigned long long)nwin * (unsigned)(w * h));
         }
-        __syncthreads();  // the next point reuses the slot, the bands and the reduce scratch
+        __syncthreads();  // the next point reuses the slot, the LDS and the records
     }
 }
 
 hipError_t launch_lk_lg(const LkLaunchArgs &a, int grid, int lds_bytes, hipStream_t s) {
     if (grid <= 0 || a.lk_wgs <= 0) return hipSuccess;
     if (!a.lg_ws || a.lg_slot <= 0 || lds_bytes > 160 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lk_kernel_lg<kLgNT>, dim3(grid), dim3(kLgNT), lds_bytes, s, a);
+    hipLaunchKernelGGL(lk_kernel_lg, dim3(grid), dim3(kLgNT), lds_bytes, s, a);
     return hipGetLastError();
 }
 
 hipError_t lg_kernels_init() {
-    return hipFuncSetAttribute((const void *)lk_kernel_lg<kLgNT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return hipFuncSetAttribute((const void *)lk_kernel_lg, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
 }  // namespace psn
