@@ -31,6 +31,15 @@ namespace psn {
 // pair selector: bytes (s, s + 1) of a row's 8-byte window -> J[x] | J[x+1] << 16
 __device__ __forceinline__ unsigned lg_sel(int s) { return 0x0c000c00u | ((unsigned)(s + 1) << 16) | (unsigned)s; }
 
+// bilinear J (DESCALE 9) at level coordinates (gy, gx) with reflect-101 taps (the
+// padded J buffer of calcOpticalFlowPyrLK: copyMakeBorder(..., BORDER_REFLECT_101))
+__device__ __forceinline__ int lg_j_refl(const LevelDev &J, int gy, int gx, int w00, int w01, int w10, int w11) {
+    const uint8_t *r0 = J.p + (long long)refl101(gy, J.h) * J.pitch;
+    const uint8_t *r1 = J.p + (long long)refl101(gy + 1, J.h) * J.pitch;
+    const int x0 = refl101(gx, J.w), x1 = refl101(gx + 1, J.w);
+    return PSN_DESCALE(r0[x0] * w00 + r0[x1] * w01 + r1[x0] * w10 + r1[x1] * w11, 9);
+}
+
 // Window geometry: quads per row, quads, quads per thread; the SSE2 chain split
 // of the b sums (8-pixel steps: nB2 quads per row, n8 pixels, tB tail pixels)
 // and of the A sums (4-pixel steps: nA quads, tA tail pixels).
@@ -93,9 +102,7 @@ __device__ __forceinline__ LgJ lg_j(const LevelDev &J, int inx, int iny, int w, 
     return r;
 }
 // d[i] = DESCALE(bilinear J, 9) - I of the quad's pixels (ip: I* as packed pairs);
-// the diff is folded into the dot product's accumulator: (v + 256 - 512 I) >> 9.
-// Taps outside the level take their reflect-101 source (the padded J buffer of
-// calcOpticalFlowPyrLK: copyMakeBorder(..., BORDER_REFLECT_101)).
+// the diff is folded into the dot product's accumulator: (v + 256 - 512 I) >> 9
 __device__ __forceinline__ void lg_diffs(const LgJ &J, int y, int qx, const uint2 &ip, int (&d)[4]) {
     const int I[4] = {lo16(ip.x), hi16(ip.x), lo16(ip.y), hi16(ip.y)};
     if (J.in) {
@@ -106,14 +113,10 @@ __device__ __forceinline__ void lg_diffs(const LgJ &J, int y, int qx, const uint
         for (int i = 0; i < 4; i++)
             d[i] = sdot2(__builtin_amdgcn_perm(b1, b0, J.s[i]), J.W1,
                          sdot2(__builtin_amdgcn_perm(a1, a0, J.s[i]), J.W0, 256 - 512 * I[i])) >> 9;
-    } else {  // a window reaching past the level: reflect-101 taps, pixel by pixel
-        const uint8_t *r0 = J.J.p + (long long)refl101(J.iny + y, J.J.h) * J.pitch;
-        const uint8_t *r1 = J.J.p + (long long)refl101(J.iny + y + 1, J.J.h) * J.pitch;
-#pragma unroll 1
-        for (int i = 0; i < 4; i++) {
-            const int xa = refl101(J.inx + 4 * qx + i, J.J.w), xb = refl101(J.inx + 4 * qx + i + 1, J.J.w);
-            d[i] = PSN_DESCALE(r0[xa] * J.w00 + r0[xb] * J.w01 + r1[xa] * J.w10 + r1[xb] * J.w11, 9) - I[i];
-        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            d[i] = lg_j_refl(J.J, J.iny + y, J.inx + 4 * qx + i, J.w00, J.w01, J.w10, J.w11) - I[i];
     }
 }
 
@@ -332,6 +335,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                 int T11[5] = {0, 0, 0, 0, 0}, T22[5] = {0, 0, 0, 0, 0}, T12[5] = {0, 0, 0, 0, 0};
                 int M12[5] = {0, 0, 0, 0, 0}, m12[5] = {0, 0, 0, 0, 0};
                 int qx = x0;
+#pragma unroll 1
                 for (int j = 0; j < cnt; j++) {
                     const uint2 xp = XPs[j * NT + tid], yp = YPs[j * NT + tid];
                     const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
@@ -482,6 +486,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                 int dmax = 0;
                 {
                     int y = y0, qx = x0;
+#pragma unroll 1
                     for (int k = 0; k < cnt; k++) {
                         const int ix = k * NT + tid;
                         const uint2 ip = IPs[ix], xp = XPs[ix], yp = YPs[ix];

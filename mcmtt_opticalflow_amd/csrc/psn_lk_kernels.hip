@@ -113,12 +113,29 @@ __device__ __forceinline__ void pyr_tile(const PyrBuildArgs &a, int bx, int by, 
     // level-0 region
     {
         const int m = (off0 + n0 + 3) >> 2;  // dwords per row
-        const bool dw = a.channels == 1 && s0x >= 0 && s0y >= 0 && ax + 4 * m <= W0 && s0y + n0 <= H0 &&
+        const bool dw = s0x >= 0 && s0y >= 0 && ax + 4 * m <= W0 && s0y + n0 <= H0 &&
                         ((uintptr_t)a.src & 3) == 0 && (a.src_stride & 3) == 0;
-        if (dw) {
+        if (dw && a.channels == 1) {
             for (int r = ty; r < n0; r += TY) {
                 const uint32_t *srow = (const uint32_t *)(a.src + (size_t)(s0y + r) * a.src_stride + ax);
                 for (int d = tx; d < m; d += TX) *(uint32_t *)(B0 + r * S0 + 4 * d) = srow[d];
+            }
+        } else if (dw) {
+            // BGR interior region: 4 pixels = 3 aligned dwords -> RGB2Gray<uchar> -> one dword
+            for (int r = ty; r < n0; r += TY) {
+                const uint32_t *srow = (const uint32_t *)(a.src + (size_t)(s0y + r) * a.src_stride + 3 * ax);
+                for (int d = tx; d < m; d += TX) {
+                    const uint32_t w0 = srow[3 * d], w1 = srow[3 * d + 1], w2 = srow[3 * d + 2];
+                    const uint32_t bgr[12] = {w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255, w0 >> 24,
+                                              w1 & 255, (w1 >> 8) & 255, (w1 >> 16) & 255, w1 >> 24,
+                                              w2 & 255, (w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24};
+                    uint32_t out = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; k++)
+                        out |= ((bgr[3 * k] * 1868 + bgr[3 * k + 1] * 9617 + bgr[3 * k + 2] * 4899 + (1 << 13)) >> 14)
+                               << (8 * k);
+                    *(uint32_t *)(B0 + r * S0 + 4 * d) = out;
+                }
             }
         } else {
             for (int r = ty; r < n0; r += TY) {
@@ -235,7 +252,10 @@ __global__ __launch_bounds__(256) void pyramid_kernel(PyrBuildArgs a) {
         }
         return;
     }
-    pyr_tile<256>(a, blockIdx.x, blockIdx.y, smem);
+    // XCD-aware tile order (as lk_kernel_bx): runs of consecutive row-major tiles
+    // share one XCD's L2, so the halo a tile re-reads of its neighbours is an L2 hit
+    const int n = gridDim.x * gridDim.y, t = xcd_remap((int)(blockIdx.y * gridDim.x + blockIdx.x), n);
+    pyr_tile<256>(a, t % gridDim.x, t / gridDim.x, smem);
 }
 
 void pyramid_grid(const PyrBuildArgs &a, int &tiles_x, int &tiles_y, int &lds_bytes) {

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from mcmtt_opticalflow_amd import _lib, lk, synth  # noqa: E402
 import hiprt  # noqa: E402
 
-PHASES = ["a_phase", "a_chains", "main_pass", "reduce", "fb_products", "fb_chains", "results"]
+PHASES = ["a_values", "a_runs_check_chains", "main_pass", "publish_check_eval", "fb_setup", "fb_tiles", "results"]
 
 
 def main():
