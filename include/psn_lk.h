@@ -39,7 +39,7 @@ extern "C" {
 #define PSN_LK_ERR_SLOT (-5)        /* ring slot out of range or never filled */
 #define PSN_LK_ERR_LEVEL_CAP (-6)   /* query needs more pyramid levels than the ring holds */
 #define PSN_LK_ERR_COMM (-7)        /* RCCL failure */
-#define PSN_LK_ERR_UNSUPPORTED (-8) /* window wider than PSN_LK_MAX_WIN_WIDTH (or a feature this build lacks) */
+#define PSN_LK_ERR_UNSUPPORTED (-8) /* window wider than PSN_LK_MAX_WIN_WIDTH or of 2^24+ px (or a feature this build lacks) */
 
 /* flags: OpenCV 2.4.6 values (video/tracking.hpp) + one accumulation-order bit */
 #define PSN_LK_USE_INITIAL_FLOW 4      /* cv::OPTFLOW_USE_INITIAL_FLOW */
@@ -51,10 +51,11 @@ extern "C" {
 #define PSN_LK_TERM_EPS 2
 
 #define PSN_LK_MAX_LEVELS 8
-/* Window limits: any height; widths up to PSN_LK_MAX_WIN_WIDTH (one window row
- * band of the large-window kernel in LDS). Tracker2D passes box.w x box.h
- * (PSNWhere_Tracker2D.cpp:871-877) and box.w x box.w (:776-782) uncapped; every
- * box inside a frame up to 6400 px wide is covered. */
+/* Window limits: widths up to PSN_LK_MAX_WIN_WIDTH (one window row band of the
+ * large-window kernel in LDS), areas below 2^24 pixels (h * ceil(w/4) < 2^22
+ * quads). Tracker2D passes box.w x box.h (PSNWhere_Tracker2D.cpp:871-877) and
+ * box.w x box.w (:776-782) uncapped; every box inside a frame up to 6400 px wide
+ * and 2^24 px in area (4K: 8.3 Mpx) is covered. */
 #define PSN_LK_MAX_WIN_WIDTH 6400
 
 /* Arguments of cv::calcOpticalFlowPyrLK after prevImg/nextImg/points. The
@@ -211,6 +212,8 @@ int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *
  *   PSN_LK_VARIANT_FUSED_HELPERS  tile-only workgroups per fused-ingest launch
  *   PSN_LK_VARIANT_LARGE       1 = every query runs the large-window kernel (lk_kernel_lg)
  *   PSN_LK_VARIANT_LG_LDS      LDS budget (bytes) of a large-window workgroup (its row bands)
+ *   PSN_LK_VARIANT_LG_JR       0 = the large-window kernel reads J from the level, never
+ *                              from an LDS copy of the window's J region
  * Queries are split into one launch per window class (single-tile / box kernel
  * per units-per-thread and tail build / row-tiled / large), each sized for its
  * own windows. */
@@ -222,6 +225,7 @@ int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *
 #define PSN_LK_VARIANT_FUSED_HELPERS 6
 #define PSN_LK_VARIANT_LARGE 7
 #define PSN_LK_VARIANT_LG_LDS 8
+#define PSN_LK_VARIANT_LG_JR 9
 int psn_lk_debug_set_variant(psn_lk_ctx *ctx, int key, int value);
 
 /* Window-sample counter (SURVEY 8(d)'s compute figure): while on, every box-

@@ -105,6 +105,7 @@ struct psn_lk_ctx {
     // lg_lds = LDS budget of one of its workgroups (row bands of the window)
     bool force_large = false;
     int lg_lds = 24 * 1024;
+    bool lg_jr = true;  // LG_JR: J region of the iterations in LDS where it fits
     // its window-value slots in HBM, one buffer per stream (launches on one
     // stream run in order; launches on different streams may overlap)
     struct LgWs {
@@ -678,6 +679,7 @@ struct PlannedQuery {
     int bx_upt = 0, bx_lds = 0;  // box kernel units per thread (0: does not fit)
     int tiled_tr = 0;           // row-tiled kernel: tile rows (0: window not LDS-resident)
     int lg_tr = 0;              // large-window kernel: band rows
+    bool lg_jr = false;         // + J region in LDS
     int cls = kClsLg, key = 0;  // the launch it goes to
 };
 
@@ -693,11 +695,19 @@ static int tiled_rows(const psn_lk_ctx *c, int w, int h) {
 }
 // Band rows of the large-window kernel's A phase within its LDS budget (>= 1 row;
 // the tile planes of the fallbacks set the floor of the budget).
-static int lg_rows(const psn_lk_ctx *c, int w, int h) {
+static int lg_rows(const psn_lk_ctx *c, int w, int h, bool jr) {
     int tr = 1;
-    const int budget = std::max(c->lg_lds, psn::lg_lds_bytes(w, 1));
-    while (tr < h && psn::lg_lds_bytes(w, tr + 1) <= budget) tr++;
+    const int budget = std::max(c->lg_lds, psn::lg_lds_bytes(w, h, 1, jr));
+    while (tr < h && psn::lg_lds_bytes(w, h, tr + 1, jr) <= budget) tr++;
     return tr;
+}
+// The J region of the large-window kernel's iterations in LDS: the workgroup
+// within kLgJrMaxLds, and the region's dword rows exactly divisible by the
+// staging's magic (q * (d - 1) < 2^22 and q * magic < 2^32 for every dword q).
+static bool lg_jr_fits(const psn_lk_ctx *c, int w, int h) {
+    if (!c->lg_jr || psn::lg_lds_bytes(w, h, 1, true) > psn::kLgJrMaxLds) return false;
+    const long long d = psn::bx_jrp(w) / 4, n = (long long)psn::st_jreg_h(h) * d;
+    return n * (d - 1) < (1LL << 22) && n * (long long)psn::div_magic((int)d) < (1LL << 32);
 }
 
 // Validate and plan one query.
@@ -710,8 +720,9 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
         return set_err(c, PSN_LK_ERR_SLOT, "slot never filled (%d, %d)", q.prev_slot, q.next_slot);
     if (p.win_w <= 2 || p.win_h <= 2) return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", p.win_w, p.win_h);
     if (p.max_level < 0 || q.num_pts < 0 || q.first_pt < 0) return set_err(c, PSN_LK_ERR_ARG, "bad query");
-    if (p.win_w > PSN_LK_MAX_WIN_WIDTH || (long long)p.win_w * p.win_h > (1LL << 30))
-        return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d wider than %d px", p.win_w, p.win_h, PSN_LK_MAX_WIN_WIDTH);
+    if (p.win_w > PSN_LK_MAX_WIN_WIDTH || (long long)p.win_h * ((p.win_w + 3) / 4) >= (1LL << 22))
+        return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d wider than %d px or above 2^24 px", p.win_w, p.win_h,
+                       PSN_LK_MAX_WIN_WIDTH);
     const int ml = psn_lk_effective_max_level(c->width, c->height, p.win_w, p.win_h, p.max_level);
     if (ml >= c->nlevels)
         return set_err(c, PSN_LK_ERR_LEVEL_CAP, "query needs %d levels, ring holds %d", ml + 1, c->nlevels);
@@ -734,7 +745,8 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
         }
     }
     pq.tiled_tr = tiled_rows(c, w, h);
-    pq.lg_tr = lg_rows(c, w, h);
+    pq.lg_jr = lg_jr_fits(c, w, h);
+    pq.lg_tr = lg_rows(c, w, h, pq.lg_jr);
     d.prev_slot = q.prev_slot;
     d.next_slot = q.next_slot;
     d.pt_begin = q.first_pt;
@@ -785,7 +797,11 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
     } else {
         pq.cls = kClsLg;
     }
-    if (pq.cls == kClsLg) d.tile_rows = pq.lg_tr;
+    if (pq.cls == kClsLg) {
+        d.tile_rows = pq.lg_tr;
+        d.lg_jr = pq.lg_jr ? 1 : 0;
+        if (pq.lg_jr) d.dv_bxjr = psn::div_magic(psn::bx_jrp(w) / 4);
+    }
     if (pq.cls == kClsTiled) d.tile_rows = pq.tiled_tr;
     return PSN_LK_OK;
 }
@@ -915,7 +931,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
     lds = 0;
     for (int i = 0; i < a.nq; i++) {
         slot = std::max(slot, psn::lg_slot_int2(a.q[i].win_w, a.q[i].win_h));
-        lds = std::max(lds, psn::lg_lds_bytes(a.q[i].win_w, a.q[i].tile_rows));
+        lds = std::max(lds, psn::lg_lds_bytes(a.q[i].win_w, a.q[i].win_h, a.q[i].tile_rows, a.q[i].lg_jr != 0));
     }
     const size_t slot_bytes = (size_t)slot * 8;
     const long long fit = std::max<long long>((long long)(kLgWsBudget / slot_bytes), 64);
@@ -1149,6 +1165,7 @@ int psn_lk_debug_set_variant(psn_lk_ctx *c, int key, int value) {
     case PSN_LK_VARIANT_FUSED_HELPERS: c->fused_helpers = std::max(0, value); return PSN_LK_OK;
     case PSN_LK_VARIANT_LARGE: c->force_large = value != 0; return PSN_LK_OK;
     case PSN_LK_VARIANT_LG_LDS: c->lg_lds = std::max(4 * 1024, std::min(value, 160 * 1024 - 1024)); return PSN_LK_OK;
+    case PSN_LK_VARIANT_LG_JR: c->lg_jr = value != 0; return PSN_LK_OK;
     default: return PSN_LK_ERR_ARG;
     }
 }

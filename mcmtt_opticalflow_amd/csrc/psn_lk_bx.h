@@ -210,6 +210,99 @@ __device__ __forceinline__ unsigned bx_sel(int sj, int i) {
     return 0x0c000c00u | ((unsigned)(sj + i + 1) << 16) | (unsigned)(sj + i);
 }
 
+// Window values of one unit (window row yy, quad column qq: 4 pixels) from the
+// level's I patch in LDS (rows of PM dwords from the window origin - (1, 1)
+// aligned down to a dword, byte shift sh): Scharr derivatives on packed 16-bit
+// pairs (zero outside the image unless IN: every derivative the window reads is
+// inside), bilinear I*, Ix*, Iy* by v_dot2 (the rounding folded in) as packed
+// pairs; gmx / gmn track the unit's gradients (pixels past w and invalid units
+// (uv false) give zero gradients). Shared by lk_kernel_bx (register-resident
+// units) and lk_kernel_lg (units streamed to its slot).
+template <bool IN, bool NOTAIL>
+__device__ __forceinline__ void bx_unit(const uint32_t *P32, int PM, int sh, int yy, int qq, bool uv, int w, int ipx,
+                                        int ipy, int cols, int rows, int iw00, int iw01, int iw10, int iw11, int c256,
+                                        int c8192, unsigned (&IPk)[2], unsigned (&XPk)[2], unsigned (&YPk)[2],
+                                        int &gmx, int &gmn) {
+    // the unit's 4 x 7-byte patch window as packed 16-bit pairs: even pairs
+    // E[r][k] = (byte 2k, byte 2k+1), odd pairs O[r-1][k] = (2k+1, 2k+2) of rows 1, 2
+    s16x2 E[4][4], O[2][2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint32_t *p = P32 + (yy + r) * PM + qq;
+        const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        E[r][0] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c010c00u));
+        E[r][1] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
+        E[r][2] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c050c04u));
+        E[r][3] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c070c06u));
+        if (r == 1 || r == 2) {
+            O[r - 1][0] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c020c01u));
+            O[r - 1][1] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
+        }
+    }
+    // column masks of pixels 2k, 2k+1 (zero derivative outside the image)
+    unsigned cm[3];
+#pragma unroll
+    for (int kk = 0; kk < 3; kk++)
+        cm[kk] = IN ? ~0u
+                    : ((unsigned)(ipx + 4 * qq + 2 * kk) < (unsigned)cols ? 0xffffu : 0u) |
+                          ((unsigned)(ipx + 4 * qq + 2 * kk + 1) < (unsigned)cols ? 0xffff0000u : 0u);
+    // Scharr on packed pairs (|values| <= 4080: exact in 16 bits): DX/DY pairs
+    // (2k, 2k+1) of the two derivative rows o = 0, 1
+    unsigned DXp[2][3], DYp[2][3];
+    const s16x2 k3 = {3, 3}, k10 = {10, 10};
+#pragma unroll
+    for (int o = 0; o < 2; o++) {
+        const unsigned rm = IN || (unsigned)(ipy + yy + o) < (unsigned)rows ? ~0u : 0u;
+        s16x2 SV[4], DV[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+            SV[kk] = (E[o][kk] + E[o + 2][kk]) * k3 + E[o + 1][kk] * k10;
+            DV[kk] = E[o + 2][kk] - E[o][kk];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 3; kk++) {
+            const s16x2 dvo = __builtin_bit_cast(
+                s16x2, __builtin_amdgcn_alignbyte(__builtin_bit_cast(unsigned, DV[kk + 1]),
+                                                  __builtin_bit_cast(unsigned, DV[kk]), 2));
+            const s16x2 dx = SV[kk + 1] - SV[kk];
+            const s16x2 dy = (DV[kk] + DV[kk + 1]) * k3 + dvo * k10;
+            DXp[o][kk] = __builtin_bit_cast(unsigned, dx) & cm[kk] & rm;
+            DYp[o][kk] = __builtin_bit_cast(unsigned, dy) & cm[kk] & rm;
+        }
+    }
+    // bilinear window values by v_dot2 on (x, x+1) pairs, rounding folded in
+    const unsigned Wa = pack_w(iw00, iw01), Wb = pack_w(iw10, iw11);
+    const unsigned b1p[4] = {__builtin_bit_cast(unsigned, O[0][0]), __builtin_bit_cast(unsigned, E[1][1]),
+                             __builtin_bit_cast(unsigned, O[0][1]), __builtin_bit_cast(unsigned, E[1][2])};
+    const unsigned b2p[4] = {__builtin_bit_cast(unsigned, O[1][0]), __builtin_bit_cast(unsigned, E[2][1]),
+                             __builtin_bit_cast(unsigned, O[1][1]), __builtin_bit_cast(unsigned, E[2][2])};
+    int ix[4], iy[4], iv[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const bool pv = uv && (NOTAIL || 4 * qq + i < w);
+        const int h = i >> 1;
+        // pairs (i, i+1): even i from the stored pairs, odd i shifted by 16 bits
+        const unsigned x0 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[0][h + 1], DXp[0][h], 2) : DXp[0][h];
+        const unsigned x1 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[1][h + 1], DXp[1][h], 2) : DXp[1][h];
+        const unsigned y0_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[0][h + 1], DYp[0][h], 2) : DYp[0][h];
+        const unsigned y1_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[1][h + 1], DYp[1][h], 2) : DYp[1][h];
+        iv[i] = sdot2(b2p[i], Wb, sdot2k(b1p[i], Wa, c256)) >> 9;
+        const int gx = sdot2(x1, Wb, sdot2k(x0, Wa, c8192)) >> 14;
+        const int gy = sdot2(y1_, Wb, sdot2k(y0_, Wa, c8192)) >> 14;
+        ix[i] = gx & -(int)pv;
+        iy[i] = gy & -(int)pv;
+        gmx = max(gmx, max(ix[i], iy[i]));
+        gmn = min(gmn, min(ix[i], iy[i]));
+    }
+    IPk[0] = pack_w(iv[0], iv[1]);
+    IPk[1] = pack_w(iv[2], iv[3]);
+    XPk[0] = pack_w(ix[0], ix[1]);
+    XPk[1] = pack_w(ix[2], ix[3]);
+    YPk[0] = pack_w(iy[0], iy[1]);
+    YPk[1] = pack_w(iy[2], iy[3]);
+}
+
 // Ordered float sum of a zero-padded LDS chain (16-B aligned, ceil(len/16)
 // blocks of 16 floats; +0 pads leave an integer-valued sum unchanged) onto acc,
 // with one block in flight while one is summed: the LDS latency (~100 cycles)

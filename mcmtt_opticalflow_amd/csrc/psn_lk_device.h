@@ -304,4 +304,116 @@ __device__ __forceinline__ LevelDev ring_level_u(const RingGeo &r, int slot, int
     return L;
 }
 
+typedef const void __attribute__((address_space(1))) *gptr_t;
+typedef void __attribute__((address_space(3))) *lptr_t;
+
+// Asynchronous LDS-DMA gather of a PW x PH u8 region of a pyramid level
+// (reflect-101 addressing) into LDS, one dword per pixel. Wave w issues the
+// 64-pixel chunks w, w+NW, ...; completion = s_waitcnt vmcnt(0) + barrier.
+template <int NT>
+__device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH,
+                                           unsigned mg_pw) {
+    const int n = PW * PH;
+    const bool interior = gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    Walk wk;
+    wk.init_m(threadIdx.x, NT, PW, mg_pw);
+    for (int c0 = wid * 64; c0 < n; c0 += NT, wk.step()) {
+        if (c0 + lane < n) {
+            int gy = gy0 + wk.y, gx = gx0 + wk.x;
+            if (!interior) {
+                gy = refl101(gy, L.h);
+                gx = refl101(gx, L.w);
+            }
+            const uint8_t *src = L.p + (size_t)gy * L.pitch + gx;
+            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + c0), 1, 0, 0);
+        }
+    }
+}
+// The I patch of one level (PH rows, lk_pat_m(w) dwords per row from the
+// aligned-down column gx0 & ~3) into LDS bytes: interior patches move as
+// aligned dwords by LDS-DMA (lane i of a chunk lands at dst + 4 * i, so the
+// chunk of dwords c0.. is contiguous in LDS); patches crossing the image border
+// reflect their rows, move the dwords that lie inside the image the same way and
+// gather the others' bytes through reflect-101.
+template <int NT>
+__device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m,
+                                          unsigned dv_m) {
+    const int ax = gx0 & ~3;
+    const int n = PH * m;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w) {
+        // the row's last dword may read up to 6 bytes past the image width:
+        // inside the 256-B pitch, the next row, or the ring's slack
+        for (int c0 = wid * 64; c0 < n; c0 += NT) {
+            const int q = c0 + lane;
+            if (q < n) {
+                const int r = qdiv(q, dv_m), j = q - r * m;
+                const uint8_t *src = L.p + (size_t)(gy0 + r) * L.pitch + ax + 4 * j;
+                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + 4 * c0), 4, 0, 0);
+            }
+        }
+    } else {
+        // across the border: reflect-101 rows; dwords whose 4 columns are inside the
+        // image still move by LDS-DMA (lanes with such a dword: the DMA writes lane i's
+        // dword at dst + 4 * (c0 + i)), the others gather their 4 reflected bytes
+        for (int c0 = wid * 64; c0 < n; c0 += NT) {
+            const int q = c0 + lane;
+            if (q < n) {
+                const int r = qdiv(q, dv_m), j = q - r * m;
+                const uint8_t *row = L.p + (size_t)refl101(gy0 + r, L.h) * L.pitch;
+                const int x = ax + 4 * j;
+                if (x >= 0 && x + 4 <= L.w) {
+                    __builtin_amdgcn_global_load_lds((gptr_t)(row + x), (lptr_t)(dst + 4 * c0), 4, 0, 0);
+                } else {
+                    unsigned v = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++) v |= (unsigned)row[refl101(x + b, L.w)] << (8 * b);
+                    *(unsigned *)(dst + 4 * q) = v;
+                }
+            }
+        }
+    }
+}
+// dma_patch for rows of any width (no division magic): each thread's (row,
+// dword) by a Walk over the PH x m dword grid.
+template <int NT>
+__device__ __forceinline__ void dma_rows(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m) {
+    const int ax = gx0 & ~3;
+    const int n = PH * m;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const bool in = gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w;
+    Walk wk;
+    wk.init(threadIdx.x, NT, m);
+    for (int c0 = wid * 64; c0 < n; c0 += NT, wk.step()) {
+        if (c0 + lane >= n) continue;
+        const int x = ax + 4 * wk.x;
+        if (in) {  // as dma_patch: a row's last dword may read a few bytes past PW
+            __builtin_amdgcn_global_load_lds((gptr_t)(L.p + (size_t)(gy0 + wk.y) * L.pitch + x), (lptr_t)(dst + 4 * c0),
+                                             4, 0, 0);
+        } else {
+            const uint8_t *row = L.p + (size_t)refl101(gy0 + wk.y, L.h) * L.pitch;
+            if (x >= 0 && x + 4 <= L.w) {
+                __builtin_amdgcn_global_load_lds((gptr_t)(row + x), (lptr_t)(dst + 4 * c0), 4, 0, 0);
+            } else {
+                unsigned v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) v |= (unsigned)row[refl101(x + b, L.w)] << (8 * b);
+                *(unsigned *)(dst + 4 * (c0 + lane)) = v;
+            }
+        }
+    }
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// A workgroup barrier that leaves vector-memory loads in flight (__syncthreads'
+// fence would wait for them): every thread's LDS data it orders was already
+// waited for (dma_wait / lgkmcnt) by the thread that wrote it. The empty asm
+// keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void barrier_inflight() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+
 }  // namespace psn

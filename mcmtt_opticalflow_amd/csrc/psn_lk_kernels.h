@@ -49,7 +49,11 @@ struct LkQueryDev {
     int qidx;             // the caller's query index (LkLaunchArgs::counts)
     // box-window kernel: row tiles of the err-chain fallback
     // and the division magics of its I-patch / J-region dword rows
-    int bx_tre, bx_hw;  // + half waves per fallback tile
+    int bx_tre;
+    union {
+        int bx_hw;  // box kernel: half waves per fallback tile
+        int lg_jr;  // large-window kernel: 1 = the iterations read J from an LDS copy of its region
+    };
     unsigned dv_bxpm, dv_bxjr;
 };
 __host__ __device__ inline unsigned div_magic(int d) { return d > 0 ? ((1u << 22) + (unsigned)d - 1u) / (unsigned)d : 0u; }
@@ -267,15 +271,20 @@ constexpr int kLgTQE = 128;  // quads per err fallback tile (one row-major chain
 __host__ __device__ constexpr int lg_sreg(int tq) { return ((tq + 15) & ~15) + 4; }  // SSE chain region (floats)
 __host__ __device__ constexpr int lg_plane(int tq) { return 4 * lg_sreg(tq) + ((4 * tq + 15) & ~15) + 4; }
 __host__ __device__ inline int lg_scr_bytes() { return align16((kBxXInts + 32) * 4); }
-__host__ __device__ inline int lg_tiles_bytes() {
-    const int a = 2 * 3 * lg_plane(kLgTQA) * 4, b = 2 * 2 * lg_plane(kLgTQB) * 4;
-    return (a > b ? a : b) + 1024;  // + slack: the chain sums read up to 5 blocks past a chain (discarded)
+__host__ __device__ inline int lg_tiles_a_bytes() { return 2 * 3 * lg_plane(kLgTQA) * 4 + 1024; }
+// + slack: the chain sums read up to 5 blocks past a chain (discarded)
+__host__ __device__ inline int lg_tiles_b_bytes() { return 2 * 2 * lg_plane(kLgTQB) * 4 + 1024; }
+// A phase band: tr + 3 rows of the I patch, bx_pm(w) dwords each
+__host__ __device__ inline int lg_band_bytes(int w, int tr) { return align16((tr + 3) * 4 * bx_pm(w)); }
+// J region of the iterations (lg_jr): st_jreg_h(h) rows of bx_jrp(w) bytes, after the b tiles
+__host__ __device__ inline int lg_jr_bytes(int w, int h) { return align16(st_jreg_h(h) * bx_jrp(w)); }
+__host__ __device__ inline int lg_lds_bytes(int w, int h, int tr, bool jr) {
+    int u = lg_band_bytes(w, tr);
+    u = u > lg_tiles_a_bytes() ? u : lg_tiles_a_bytes();
+    const int it = lg_tiles_b_bytes() + (jr ? lg_jr_bytes(w, h) : 0);
+    return lg_scr_bytes() + (u > it ? u : it);
 }
-__host__ __device__ inline int lg_band_bytes(int w, int tr) { return lk_tile_pimg_bytes(w, tr) + lk_tile_dg_bytes(w, tr); }
-__host__ __device__ inline int lg_lds_bytes(int w, int tr) {
-    const int u = lg_band_bytes(w, tr), t = lg_tiles_bytes();
-    return lg_scr_bytes() + (u > t ? u : t);
-}
+constexpr int kLgJrMaxLds = 80 * 1024;  // J region in LDS while the workgroup fits this (2 per CU)
 __host__ __device__ inline int lg_quads_per_thread(int w, int h) { return (h * ((w + 3) >> 2) + kLgNT - 1) / kLgNT; }
 // window-value slot of one workgroup, in 8-byte units
 __host__ __device__ inline long long lg_slot_int2(int w, int h) { return 3LL * kLgNT * lg_quads_per_thread(w, h); }

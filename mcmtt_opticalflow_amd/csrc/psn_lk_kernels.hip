@@ -795,89 +795,6 @@ __device__ __forceinline__ void block_sums3(int &s1, int &s2, unsigned &a, int *
     }
 }
 
-typedef const void __attribute__((address_space(1))) *gptr_t;
-typedef void __attribute__((address_space(3))) *lptr_t;
-
-// Asynchronous LDS-DMA gather of a PW x PH u8 region of a pyramid level
-// (reflect-101 addressing) into LDS, one dword per pixel. Wave w issues the
-// 64-pixel chunks w, w+NW, ...; completion = s_waitcnt vmcnt(0) + barrier.
-template <int NT>
-__device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH,
-                                           unsigned mg_pw) {
-    const int n = PW * PH;
-    const bool interior = gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w;
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    Walk wk;
-    wk.init_m(threadIdx.x, NT, PW, mg_pw);
-    for (int c0 = wid * 64; c0 < n; c0 += NT, wk.step()) {
-        if (c0 + lane < n) {
-            int gy = gy0 + wk.y, gx = gx0 + wk.x;
-            if (!interior) {
-                gy = refl101(gy, L.h);
-                gx = refl101(gx, L.w);
-            }
-            const uint8_t *src = L.p + (size_t)gy * L.pitch + gx;
-            __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + c0), 1, 0, 0);
-        }
-    }
-}
-// The I patch of one level (PH rows, lk_pat_m(w) dwords per row from the
-// aligned-down column gx0 & ~3) into LDS bytes: interior patches move as
-// aligned dwords by LDS-DMA (lane i of a chunk lands at dst + 4 * i, so the
-// chunk of dwords c0.. is contiguous in LDS); patches crossing the image border
-// reflect their rows, move the dwords that lie inside the image the same way and
-// gather the others' bytes through reflect-101.
-template <int NT>
-__device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m,
-                                          unsigned dv_m) {
-    const int ax = gx0 & ~3;
-    const int n = PH * m;
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w) {
-        // the row's last dword may read up to 6 bytes past the image width:
-        // inside the 256-B pitch, the next row, or the ring's slack
-        for (int c0 = wid * 64; c0 < n; c0 += NT) {
-            const int q = c0 + lane;
-            if (q < n) {
-                const int r = qdiv(q, dv_m), j = q - r * m;
-                const uint8_t *src = L.p + (size_t)(gy0 + r) * L.pitch + ax + 4 * j;
-                __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + 4 * c0), 4, 0, 0);
-            }
-        }
-    } else {
-        // across the border: reflect-101 rows; dwords whose 4 columns are inside the
-        // image still move by LDS-DMA (lanes with such a dword: the DMA writes lane i's
-        // dword at dst + 4 * (c0 + i)), the others gather their 4 reflected bytes
-        for (int c0 = wid * 64; c0 < n; c0 += NT) {
-            const int q = c0 + lane;
-            if (q < n) {
-                const int r = qdiv(q, dv_m), j = q - r * m;
-                const uint8_t *row = L.p + (size_t)refl101(gy0 + r, L.h) * L.pitch;
-                const int x = ax + 4 * j;
-                if (x >= 0 && x + 4 <= L.w) {
-                    __builtin_amdgcn_global_load_lds((gptr_t)(row + x), (lptr_t)(dst + 4 * c0), 4, 0, 0);
-                } else {
-                    unsigned v = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; b++) v |= (unsigned)row[refl101(x + b, L.w)] << (8 * b);
-                    *(unsigned *)(dst + 4 * q) = v;
-                }
-            }
-        }
-    }
-}
-__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// A workgroup barrier that leaves vector-memory loads in flight (__syncthreads'
-// fence would wait for them): every thread's LDS data it orders was already
-// waited for (dma_wait / lgkmcnt) by the thread that wrote it. The empty asm
-// keeps the compiler from moving LDS accesses across it.
-__device__ __forceinline__ void barrier_inflight() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-}
-
-
 // Element walk of a region with m elements per row: this thread's first
 // element (row, column) and the per-NT step (computed once per kernel).
 struct JWalk {
@@ -2208,84 +2125,8 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             for (int k = 0; k < UPT; k++) {
                 const bool uv = u0 + k < U;
                 const int yy = uv ? y : 0, qq = uv ? q : 0;
-                // the unit's 4 x 7-byte patch window as packed 16-bit pairs: even pairs
-                // E[r][k] = (byte 2k, byte 2k+1), odd pairs O[r-1][k] = (2k+1, 2k+2) of rows 1, 2
-                s16x2 E[4][4], O[2][2];
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const uint32_t *p = P32 + (yy + r) * PM + qq;
-                    const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
-                    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
-                    E[r][0] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c010c00u));
-                    E[r][1] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c030c02u));
-                    E[r][2] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c050c04u));
-                    E[r][3] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c070c06u));
-                    if (r == 1 || r == 2) {
-                        O[r - 1][0] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c020c01u));
-                        O[r - 1][1] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(hi, lo, 0x0c040c03u));
-                    }
-                }
-                // column masks of pixels 2k, 2k+1 (zero derivative outside the image)
-                unsigned cm[3];
-#pragma unroll
-                for (int kk = 0; kk < 3; kk++)
-                    cm[kk] = IN ? ~0u
-                                : ((unsigned)(ipx + 4 * qq + 2 * kk) < (unsigned)cols ? 0xffffu : 0u) |
-                                      ((unsigned)(ipx + 4 * qq + 2 * kk + 1) < (unsigned)cols ? 0xffff0000u : 0u);
-                // Scharr on packed pairs (|values| <= 4080: exact in 16 bits): DX/DY pairs
-                // (2k, 2k+1) of the two derivative rows o = 0, 1
-                unsigned DXp[2][3], DYp[2][3];
-                const s16x2 k3 = {3, 3}, k10 = {10, 10};
-#pragma unroll
-                for (int o = 0; o < 2; o++) {
-                    const unsigned rm = IN || (unsigned)(ipy + yy + o) < (unsigned)rows ? ~0u : 0u;
-                    s16x2 SV[4], DV[4];
-#pragma unroll
-                    for (int kk = 0; kk < 4; kk++) {
-                        SV[kk] = (E[o][kk] + E[o + 2][kk]) * k3 + E[o + 1][kk] * k10;
-                        DV[kk] = E[o + 2][kk] - E[o][kk];
-                    }
-#pragma unroll
-                    for (int kk = 0; kk < 3; kk++) {
-                        const s16x2 dvo = __builtin_bit_cast(
-                            s16x2, __builtin_amdgcn_alignbyte(__builtin_bit_cast(unsigned, DV[kk + 1]),
-                                                              __builtin_bit_cast(unsigned, DV[kk]), 2));
-                        const s16x2 dx = SV[kk + 1] - SV[kk];
-                        const s16x2 dy = (DV[kk] + DV[kk + 1]) * k3 + dvo * k10;
-                        DXp[o][kk] = __builtin_bit_cast(unsigned, dx) & cm[kk] & rm;
-                        DYp[o][kk] = __builtin_bit_cast(unsigned, dy) & cm[kk] & rm;
-                    }
-                }
-                // bilinear window values by v_dot2 on (x, x+1) pairs, rounding folded in
-                const unsigned Wa = pack_w(iw00, iw01), Wb = pack_w(iw10, iw11);
-                const unsigned b1p[4] = {__builtin_bit_cast(unsigned, O[0][0]), __builtin_bit_cast(unsigned, E[1][1]),
-                                         __builtin_bit_cast(unsigned, O[0][1]), __builtin_bit_cast(unsigned, E[1][2])};
-                const unsigned b2p[4] = {__builtin_bit_cast(unsigned, O[1][0]), __builtin_bit_cast(unsigned, E[2][1]),
-                                         __builtin_bit_cast(unsigned, O[1][1]), __builtin_bit_cast(unsigned, E[2][2])};
-                int ix[4], iy[4], iv[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const bool pv = uv && (NOTAIL || 4 * qq + i < w);
-                    const int h = i >> 1;
-                    // pairs (i, i+1): even i from the stored pairs, odd i shifted by 16 bits
-                    const unsigned x0 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[0][h + 1], DXp[0][h], 2) : DXp[0][h];
-                    const unsigned x1 = (i & 1) ? __builtin_amdgcn_alignbyte(DXp[1][h + 1], DXp[1][h], 2) : DXp[1][h];
-                    const unsigned y0_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[0][h + 1], DYp[0][h], 2) : DYp[0][h];
-                    const unsigned y1_ = (i & 1) ? __builtin_amdgcn_alignbyte(DYp[1][h + 1], DYp[1][h], 2) : DYp[1][h];
-                    iv[i] = sdot2(b2p[i], Wb, sdot2k(b1p[i], Wa, c256)) >> 9;
-                    const int gx = sdot2(x1, Wb, sdot2k(x0, Wa, c8192)) >> 14;
-                    const int gy = sdot2(y1_, Wb, sdot2k(y0_, Wa, c8192)) >> 14;
-                    ix[i] = gx & -(int)pv;
-                    iy[i] = gy & -(int)pv;
-                    gmx = max(gmx, max(ix[i], iy[i]));
-                    gmn = min(gmn, min(ix[i], iy[i]));
-                }
-                IP[k][0] = pack_w(iv[0], iv[1]);
-                IP[k][1] = pack_w(iv[2], iv[3]);
-                XP[k][0] = pack_w(ix[0], ix[1]);
-                XP[k][1] = pack_w(ix[2], ix[3]);
-                YP[k][0] = pack_w(iy[0], iy[1]);
-                YP[k][1] = pack_w(iy[2], iy[3]);
+                bx_unit<IN, NOTAIL>(P32, PM, sh, yy, qq, uv, w, ipx, ipy, cols, rows, iw00, iw01, iw10, iw11, c256,
+                                    c8192, IP[k], XP[k], YP[k], gmx, gmn);
                 // materialize the unit's results here: no sinking of its arithmetic
                 // past later units (which would keep its patch bytes live)
                 asm volatile("" : "+v"(IP[k][0]), "+v"(IP[k][1]), "+v"(XP[k][0]), "+v"(XP[k][1]), "+v"(YP[k][0]),

@@ -37,7 +37,16 @@ __device__ __forceinline__ unsigned lg_sel(int s) { return 0x0c000c00u | ((unsig
 struct LgGeo {
     int w, h, QW, NQ, K;
     int nB2, n8, tB, nA, tA;
+    float rQW, rK;  // 1 / QW, 1 / K (lg_div)
 };
+// n / d for 0 <= n < 2^24 (quad indices; the planner keeps windows below 2^22
+// quads) by the float reciprocal r = 1 / d and one correction step
+__device__ __forceinline__ int lg_div(int n, int d, float r) {
+    int t = (int)__fmul_rn((float)n, r);
+    const int m = n - t * d;
+    t += m < 0 ? -1 : (m >= d ? 1 : 0);
+    return t;
+}
 __device__ __forceinline__ LgGeo lg_geo(int w, int h, bool sse) {
     LgGeo g;
     g.w = w;
@@ -50,43 +59,56 @@ __device__ __forceinline__ LgGeo lg_geo(int w, int h, bool sse) {
     g.tB = w - g.n8;
     g.nA = sse ? w / 4 : 0;
     g.tA = w - 4 * g.nA;
+    g.rQW = __fdiv_rn(1.f, (float)g.QW);
+    g.rK = __fdiv_rn(1.f, (float)g.K);
     return g;
 }
 // terms of the SSE chains (one per SSE quad) and of the tail chain before quad q
 __device__ __forceinline__ int lg_sse_before(const LgGeo &g, int q, int nS) {
-    const int y = q / g.QW;
+    const int y = lg_div(q, g.QW, g.rQW);
     return y * nS + min(q - y * g.QW, nS);
 }
 __device__ __forceinline__ int lg_tail_before(const LgGeo &g, int q, int nS, int t) {
-    const int y = q / g.QW;
+    const int y = lg_div(q, g.QW, g.rQW);
     return y * t + min(max(4 * (q - y * g.QW - nS), 0), t);
 }
 
-// One quad's J - I* (4 pixels) at window row y, quad column qx.
+// One quad's J - I* (4 pixels) at window row y, quad column qx: from the LDS copy
+// of the J region (lds), or from the level (in: every tap inside it).
 struct LgJ {
-    const uint8_t *jb;  // interior: J at the window origin aligned down to a dword
+    const uint32_t *jl;  // lds: the region's dword holding the window origin
+    const uint8_t *jb;   // in: J at the window origin aligned down to a dword
     LevelDev J;
-    int inx, iny, pitch;
+    int inx, iny, pitch, jrp4;
     unsigned W0, W1, s[4];
     int w00, w01, w10, w11;
-    bool in;
+    bool lds, in;
 };
 __device__ __forceinline__ LgJ lg_j(const LevelDev &J, int inx, int iny, int w, int h, int w00, int w01, int w10,
-                                    int w11) {
+                                    int w11, const uint32_t *jr, int jrp4, int jr_x0, int jr_y0) {
     LgJ r;
     r.J = J;
     r.inx = inx;
     r.iny = iny;
     r.pitch = J.pitch;
+    r.jrp4 = jrp4;
     r.w00 = w00;
     r.w01 = w01;
     r.w10 = w10;
     r.w11 = w11;
     r.W0 = pack_w(w00, w01);
     r.W1 = pack_w(w10, w11);
+    r.lds = jr != nullptr;
     // every tap of the window (columns inx .. inx + w, rows iny .. iny + h) inside the level
     r.in = inx >= 0 && iny >= 0 && inx + w + 1 <= J.w && iny + h + 1 <= J.h;
-    const int sh = r.in ? (inx & 3) : 0;
+    int sh = r.in ? (inx & 3) : 0;
+    if (r.lds) {
+        const int ox = inx - jr_x0;
+        sh = ox & 3;
+        r.jl = jr + (iny - jr_y0) * jrp4 + (ox >> 2);
+    } else {
+        r.jl = nullptr;
+    }
 #pragma unroll
     for (int i = 0; i < 4; i++) r.s[i] = lg_sel(sh + i);
     r.jb = r.in ? J.p + (long long)iny * J.pitch + (inx - sh) : J.p;
@@ -95,13 +117,26 @@ __device__ __forceinline__ LgJ lg_j(const LevelDev &J, int inx, int iny, int w, 
 // d[i] = DESCALE(bilinear J, 9) - I of the quad's pixels (ip: I* as packed pairs);
 // the diff is folded into the dot product's accumulator: (v + 256 - 512 I) >> 9.
 // Taps outside the level take their reflect-101 source (the padded J buffer of
-// calcOpticalFlowPyrLK: copyMakeBorder(..., BORDER_REFLECT_101)).
+// calcOpticalFlowPyrLK: copyMakeBorder(..., BORDER_REFLECT_101)); the LDS copy
+// holds them already (dma_patch).
 __device__ __forceinline__ void lg_diffs(const LgJ &J, int y, int qx, const uint2 &ip, int (&d)[4]) {
     const int I[4] = {lo16(ip.x), hi16(ip.x), lo16(ip.y), hi16(ip.y)};
-    if (J.in) {
-        const uint32_t *r0 = (const uint32_t *)(J.jb + (long long)y * J.pitch + 4 * qx);
-        const uint32_t *r1 = (const uint32_t *)((const uint8_t *)r0 + J.pitch);
-        const uint32_t a0 = r0[0], a1 = r0[1], b0 = r1[0], b1 = r1[1];
+    if (J.lds || J.in) {
+        uint32_t a0, a1, b0, b1;
+        if (J.lds) {
+            const uint32_t *r0 = J.jl + y * J.jrp4 + qx;
+            a0 = r0[0];
+            a1 = r0[1];
+            b0 = r0[J.jrp4];
+            b1 = r0[J.jrp4 + 1];
+        } else {
+            const uint32_t *r0 = (const uint32_t *)(J.jb + (long long)y * J.pitch + 4 * qx);
+            const uint32_t *r1 = (const uint32_t *)((const uint8_t *)r0 + J.pitch);
+            a0 = r0[0];
+            a1 = r0[1];
+            b0 = r1[0];
+            b1 = r1[1];
+        }
 #pragma unroll
         for (int i = 0; i < 4; i++)
             d[i] = sdot2(__builtin_amdgcn_perm(b1, b0, J.s[i]), J.W1,
@@ -121,43 +156,82 @@ __device__ __forceinline__ void lg_diffs(const LgJ &J, int y, int qx, const uint
 // SSE chain regions of up to TQ terms and a tail region of up to 4*TQ terms
 // (16-float blocks + 4: conflict-free across the chain lanes' 16-B reads)
 
-// Ordered chains from quad qs on, tile by tile: `write(tile quad range, buffer)`
-// writes the tile's products (waves 1-3, one quad per thread), chain lanes
-// (wave 0, lanes < NCH) zero their regions' pads and sum the previous tile
-// meanwhile; double-buffered, one barrier per tile. Returns acc (chain lanes:
-// their chain's sum onto its base).
-template <int NPL, int TQ, typename Write, typename Geo>
-__device__ __forceinline__ float lg_tiles(int qs, int NQ, float *buf, int nch, float acc, Write write, Geo geo) {
+// One quad's window values as the fallback writers hold them between tiles.
+struct LgQ {
+    uint2 ip, xp, yp;
+};
+
+// Ordered chains from quad qs on, tile by tile: waves 1-3 write a tile's products
+// (one quad per thread: `load(q)` fetches quad q's window values, `store(v, q,
+// tile start, buffer)` writes its products), chain lanes (wave 0, lanes < NCH)
+// sum the previous tile meanwhile; double-buffered, one barrier per tile, each
+// writer's loads for tile g+2 in flight while tile g is summed. `before(q, s, t)`
+// gives the SSE / tail chain terms before quad q (uniform); a chain lane zeroes
+// the 16-float block holding the end of its region for tile g+2 right after
+// summing tile g from the same buffer (the writers fill the block's front a
+// barrier later). Returns acc (chain lanes: their chain's sum onto its base).
+template <int NPL, int TQ, typename Load, typename Store, typename Before, typename Mark>
+__device__ __forceinline__ float lg_tiles(int qs, int NQ, float *buf, int nch, float acc, Load load, Store store,
+                                          Before before, Mark mark) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int PL = lg_plane(TQ), SR = lg_sreg(TQ);
     const bool chl = tid < nch;
     const int cs = lane / 5, cc = lane - 5 * cs;
     const int ntiles = (NQ - qs + TQ - 1) / TQ;
-    auto region = [&](float *b) { return b + cs * PL + (cc < 4 ? cc * SR : 4 * SR); };
-    auto pad = [&](int g, float *b) {
-        if (!chl) return;
-        int nsse, ntail;
-        geo(qs + g * TQ, min(qs + (g + 1) * TQ, NQ), nsse, ntail);
-        const int len = cc < 4 ? nsse : ntail;
-        float *rg = region(b);
-        for (int i = len; i < ((len + 15) & ~15); i++) rg[i] = 0.f;
-    };
     if (ntiles <= 0) return acc;
-    write(qs, min(qs + TQ, NQ), buf);
+    auto region = [&](float *b) { return b + cs * PL + (cc < 4 ? cc * SR : 4 * SR); };
+    // chain terms before tile boundaries g .. g+3 (uniform), rolled per tile
+    int bs[4], bt[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) before(min(qs + i * TQ, NQ), bs[i], bt[i]);
+    auto pad = [&](int i0, float *b) {  // the tile between boundaries i0, i0 + 1
+        if (!chl) return;
+        const int len = cc < 4 ? bs[i0 + 1] - bs[i0] : bt[i0 + 1] - bt[i0];
+        if (len & 15) {
+            float4 *z = (float4 *)(region(b) + (len & ~15));
+            const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+            z[0] = zero;
+            z[1] = zero;
+            z[2] = zero;
+            z[3] = zero;
+        }
+    };
+    // writer thread tid (waves 1-3) takes quad tid - 64 of each tile
+    auto quad_of = [&](int g) { return tid >= 64 && tid - 64 < TQ ? qs + g * TQ + tid - 64 : NQ; };
     pad(0, buf);
+    if (ntiles > 1) pad(1, buf + NPL * PL);
+    __syncthreads();
+    LgQ v{};
+    int q = quad_of(0);
+    if (q < NQ) store(load(q), q, qs, buf);
+    q = quad_of(1);
+    if (q < NQ) v = load(q);
     __syncthreads();
     for (int g = 0; g < ntiles; g++) {
         float *cur = buf + (g & 1) * NPL * PL, *nxt = buf + ((g + 1) & 1) * NPL * PL;
-        if (g + 1 < ntiles) write(qs + (g + 1) * TQ, min(qs + (g + 2) * TQ, NQ), nxt);
-        if (tid < 64) {
-            int nsse, ntail;
-            geo(qs + g * TQ, min(qs + (g + 1) * TQ, NQ), nsse, ntail);
-            const int len = chl ? (cc < 4 ? nsse : ntail) : 0;
-            const int nbmax = __builtin_amdgcn_readlane(wave_max_scan((len + 15) >> 4), 63);
-            if (chl) acc = chain_sum_pl<false>(region(cur), len, nbmax, acc);
-            if (g + 1 < ntiles) pad(g + 1, nxt);
+        if (g + 1 < ntiles) {
+            if (q < NQ) store(v, q, qs + (g + 1) * TQ, nxt);
+            q = quad_of(g + 2);
+            if (q < NQ) v = load(q);
         }
+        if (tid < 64) {
+            const int ns = bs[1] - bs[0], nt = bt[1] - bt[0];
+            const int len = chl ? (cc < 4 ? ns : nt) : 0;
+            const int nbmax = (max(ns, nt) + 15) >> 4;
+            mark(2);
+            if (chl) acc = chain_sum_pl<false>(region(cur), len, nbmax, acc);
+            mark(3);
+            if (g + 2 < ntiles) pad(2, cur);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            bs[i] = bs[i + 1];
+            bt[i] = bt[i + 1];
+        }
+        before(min(qs + (g + 4) * TQ, NQ), bs[3], bt[3]);
+        mark(0);
         __syncthreads();
+        mark(1);
     }
     return acc;
 }
@@ -183,6 +257,8 @@ __device__ __forceinline__ float lg_tiles(int qs, int NQ, float *buf, int nch, f
     } while (0)
 #endif
 
+constexpr int kLgMB = 4;  // quads per batch of slot loads in the passes over the window
+
 __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NT = kLgNT;
@@ -192,6 +268,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
     int *EP = (int *)(RS + 16);
     uint8_t *U = smem + lg_scr_bytes();   // band staging | tile planes
     float *PL = (float *)U;
+    uint32_t *JR = (uint32_t *)(U + lg_tiles_b_bytes());  // J region (lg_jr), after the b tiles
     uint8_t *const slot = (uint8_t *)A.lg_ws + (long long)blockIdx.x * A.lg_slot * 8;
     const float FLT_SCALE = 1.f / (1 << 20);
     int par = 0;
@@ -211,9 +288,10 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
         uint2 *IPs = (uint2 *)slot, *XPs = IPs + NT * K, *YPs = XPs + NT * K;
         const int q0 = min(tid * K, NQ), cnt = min(NQ - q0, K);  // this thread's quads [q0, q0 + cnt)
         const int y0 = q0 / QW, x0 = q0 - y0 * QW;
-        const int PW = w + 3, DW = w + 1;
+        const int PM = bx_pm(w);  // I patch dwords per row
+        const bool jrm = Q.lg_jr != 0;
+        const int JRW = st_jreg_w(w), JRH = st_jreg_h(h), JRP4 = bx_jrp(w) >> 2;
         uint8_t *Pimg = U;
-        short2 *Dg = (short2 *)(U + lk_tile_pimg_bytes(w, TR));
 
         const float hwx = __fmul_rn((float)(w - 1), 0.5f), hwy = __fmul_rn((float)(h - 1), 0.5f);
         const float px0 = A.prev[2 * pi], py0 = A.prev[2 * pi + 1];
@@ -226,7 +304,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
         float errv = 0.f;
         unsigned nwin = 0;  // window passes (A phase + iterations): the sample count / (w*h)
 #ifdef PSN_LK_STAMPS
-        unsigned long long lg_acc[16] = {}, lg_t = 0, lg_t0 = 0;
+        unsigned long long lg_acc[24] = {}, lg_t = 0, lg_t0 = 0;
         LG_CLK(lg_t0);
         lg_t = lg_t0;
 #endif
@@ -236,6 +314,23 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
             const LevelDev J = ring_level_u(A.ring, Q.next_slot, level);
             const int cols = I.w, rows = I.h;
             const float scale = ldexpf(1.f, -level);
+            // the LDS copy of the J region around the window (lg_jr): restaged when the
+            // window at (inx, iny) leaves it (the A phase's bands and tiles reuse its LDS)
+            bool jr_valid = false;
+            int jr_x0 = 0, jr_y0 = 0;
+            auto window_j = [&](int inx, int iny, int w00, int w01, int w10, int w11) {
+                if (jrm && !(jr_valid && inx >= jr_x0 && iny >= jr_y0 && inx + w + 1 <= jr_x0 + JRW &&
+                             iny + h + 1 <= jr_y0 + JRH)) {
+                    // every reader of the previous copy passed a barrier since
+                    jr_x0 = (inx - kStJMargin) & ~3;
+                    jr_y0 = iny - kStJMargin;
+                    dma_patch<NT>((uint8_t *)JR, J, jr_y0, jr_x0, JRW, JRH, JRP4, Q.dv_bxjr);
+                    dma_wait();
+                    __syncthreads();
+                    jr_valid = true;
+                }
+                return lg_j(J, inx, iny, w, h, w00, w01, w10, w11, jrm ? JR : nullptr, JRP4, jr_x0, jr_y0);
+            };
             float px = __fmul_rn(px0, scale), py = __fmul_rn(py0, scale);
             float nx, ny;
             if (level == maxL) {
@@ -268,58 +363,42 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
             ny = __fsub_rn(ny, hwy);
             nwin++;
 
-            // ---- A phase (1): window values, band by band (every thread on the
-            // band's quads): I patch rows -> Scharr -> bilinear I*, Ix*, Iy* ----
-            for (int r0 = 0; r0 < h; r0 += TR) {
-                const int th = min(TR, h - r0);
-                __syncthreads();  // the previous band's (tile's, level's, point's) LDS readers are done
-                stage_one<NT>(Pimg, I, ipy + r0 - 1, ipx - 1, PW, th + 3);
-                __syncthreads();
-                {  // Scharr on (th+1) x (w+1) positions; zero outside the image
-                    Walk wk;
-                    wk.init(tid, NT, DW);
-                    for (int idx = tid; idx < (th + 1) * DW; idx += NT, wk.step()) {
-                        const int yy = wk.y, xx = wk.x;
-                        const int gy = ipy + r0 + yy, gx = ipx + xx;
-                        short2 d = make_short2(0, 0);
-                        if ((unsigned)gy < (unsigned)rows && (unsigned)gx < (unsigned)cols) {
-                            const uint8_t *p = Pimg + yy * PW + xx;
-                            const int v0l = 3 * (p[0] + p[2 * PW]) + 10 * p[PW];
-                            const int v0r = 3 * (p[2] + p[2 * PW + 2]) + 10 * p[PW + 2];
-                            const int v1l = p[2 * PW] - p[0];
-                            const int v1c = p[2 * PW + 1] - p[1];
-                            const int v1r = p[2 * PW + 2] - p[2];
-                            d.x = (short)(v0r - v0l);
-                            d.y = (short)(3 * (v1l + v1r) + 10 * v1c);
+            // ---- A phase (1): window values, band by band: the band's I patch rows
+            // by LDS-DMA, then each quad's Scharr + bilinear values (bx_unit) into
+            // the slot ----
+            {
+                const int sh = (ipx - 1) & 3;
+                const bool interior = ipx >= 0 && ipy >= 0 && ipx + 4 * QW + 2 <= cols && ipy + h + 1 <= rows;
+                const int c256 = 1 << 8, c8192 = 1 << 13;
+                const uint32_t *P32 = (const uint32_t *)Pimg;
+                int gdum0 = 0, gdum1 = 0;  // (the A runs below track the gradients)
+                auto band = [&](auto inner) {
+                    constexpr bool IN = decltype(inner)::value;
+                    for (int r0 = 0; r0 < h; r0 += TR) {
+                        const int th = min(TR, h - r0);
+                        __syncthreads();  // the previous band's (tile's, level's, point's) LDS readers are done
+                        dma_rows<NT>(Pimg, I, ipy + r0 - 1, ipx - 1, w + 3, th + 3, PM);
+                        dma_wait();
+                        __syncthreads();
+                        LG_MARK(7);  // band staging
+                        Walk wk;
+                        wk.init(tid, NT, QW);
+                        for (int qb = tid; qb < th * QW; qb += NT, wk.step()) {
+                            unsigned ip[2], xp[2], yp[2];
+                            bx_unit<IN, false>(P32, PM, sh, wk.y, wk.x, true, w, ipx, ipy + r0, cols, rows, iw00, iw01,
+                                               iw10, iw11, c256, c8192, ip, xp, yp, gdum0, gdum1);
+                            const int q = (r0 + wk.y) * QW + wk.x, t = lg_div(q, K, G.rK), idx = (q - t * K) * NT + t;
+                            IPs[idx] = make_uint2(ip[0], ip[1]);
+                            XPs[idx] = make_uint2(xp[0], xp[1]);
+                            YPs[idx] = make_uint2(yp[0], yp[1]);
                         }
-                        Dg[idx] = d;
+                        LG_MARK(9);  // band quads
                     }
-                }
-                __syncthreads();
-                {
-                    Walk wk;
-                    wk.init(tid, NT, QW);
-                    for (int qb = tid; qb < th * QW; qb += NT, wk.step()) {
-                        const int yl = wk.y, qx = wk.x;
-                        int iv[4], gxv[4], gyv[4];
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int x = 4 * qx + i;
-                            iv[i] = gxv[i] = gyv[i] = 0;
-                            if (x < w) {
-                                const uint8_t *p = Pimg + (yl + 1) * PW + x + 1;
-                                iv[i] = PSN_DESCALE(p[0] * iw00 + p[1] * iw01 + p[PW] * iw10 + p[PW + 1] * iw11, 9);
-                                const short2 *d = Dg + yl * DW + x;
-                                gxv[i] = PSN_DESCALE(d[0].x * iw00 + d[1].x * iw01 + d[DW].x * iw10 + d[DW + 1].x * iw11, 14);
-                                gyv[i] = PSN_DESCALE(d[0].y * iw00 + d[1].y * iw01 + d[DW].y * iw10 + d[DW + 1].y * iw11, 14);
-                            }
-                        }
-                        const int q = (r0 + yl) * QW + qx, t = q / K, idx = (q - t * K) * NT + t;
-                        IPs[idx] = make_uint2(pack_w(iv[0], iv[1]), pack_w(iv[2], iv[3]));
-                        XPs[idx] = make_uint2(pack_w(gxv[0], gxv[1]), pack_w(gxv[2], gxv[3]));
-                        YPs[idx] = make_uint2(pack_w(gyv[0], gyv[1]), pack_w(gyv[2], gyv[3]));
-                    }
-                }
+                };
+                if (interior)
+                    band(std::true_type());
+                else
+                    band(std::false_type());
             }
             __syncthreads();  // the window values of every band for every thread
             LG_MARK(0);  // A phase: window values
@@ -332,8 +411,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                 int T11[5] = {0, 0, 0, 0, 0}, T22[5] = {0, 0, 0, 0, 0}, T12[5] = {0, 0, 0, 0, 0};
                 int M12[5] = {0, 0, 0, 0, 0}, m12[5] = {0, 0, 0, 0, 0};
                 int qx = x0;
-                for (int j = 0; j < cnt; j++) {
-                    const uint2 xp = XPs[j * NT + tid], yp = YPs[j * NT + tid];
+                auto quad = [&](const uint2 &xp, const uint2 &yp) {
                     const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
                     const int gy[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
                     // (A11 / A22 runs saturate at 2^30: a long run never wraps; a run past 2^25
@@ -356,7 +434,19 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
 #pragma unroll
                     for (int i = 0; i < 4; i++) gmax = max(gmax, max(abs(gx[i]), abs(gy[i])));
                     if (++qx == QW) qx = 0;
+                };
+                int k = 0;
+                for (; k + kLgMB <= cnt; k += kLgMB) {
+                    uint2 xp[kLgMB], yp[kLgMB];
+#pragma unroll
+                    for (int u = 0; u < kLgMB; u++) {
+                        xp[u] = XPs[(k + u) * NT + tid];
+                        yp[u] = YPs[(k + u) * NT + tid];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kLgMB; u++) quad(xp[u], yp[u]);
                 }
+                for (; k < cnt; k++) quad(XPs[k * NT + tid], YPs[k * NT + tid]);
                 // A11 / A22 terms are >= 0: the maximum prefix is the total
                 int T[15], M[15], m[15];
 #pragma unroll
@@ -392,19 +482,22 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                     // ordered chains from half wave h0 on (every earlier prefix is an exact
                     // integer: the chain lanes start from base0)
                     const int qs = min(h0 * 32 * K, NQ);
-                    auto geoA = [&](int a, int b, int &nsse, int &ntail) {
-                        nsse = lg_sse_before(G, b, G.nA) - lg_sse_before(G, a, G.nA);
-                        ntail = lg_tail_before(G, b, G.nA, G.tA) - lg_tail_before(G, a, G.nA, G.tA);
+                    auto geoA = [&](int q, int &bs, int &bt) {
+                        bs = lg_sse_before(G, q, G.nA);
+                        bt = lg_tail_before(G, q, G.nA, G.tA);
                     };
-                    auto writeA = [&](int a, int b, float *buf) {
-                        const int q = a + tid - 64;  // waves 1-3 write
-                        if (tid < 64 || q >= b) return;
-                        const int t = q / K, idx = (q - t * K) * NT + t;
-                        const uint2 xp = XPs[idx], yp = YPs[idx];
-                        const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
-                        const int gy[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
+                    auto loadA = [&](int q) {
+                        const int t = lg_div(q, K, G.rK), idx = (q - t * K) * NT + t;
+                        LgQ v;
+                        v.xp = XPs[idx];
+                        v.yp = YPs[idx];
+                        return v;
+                    };
+                    auto storeA = [&](const LgQ &v, int q, int a, float *buf) {
+                        const int gx[4] = {lo16(v.xp.x), hi16(v.xp.x), lo16(v.xp.y), hi16(v.xp.y)};
+                        const int gy[4] = {lo16(v.yp.x), hi16(v.yp.x), lo16(v.yp.y), hi16(v.yp.y)};
                         const int PLA = lg_plane(kLgTQA), SR = lg_sreg(kLgTQA);
-                        const int y = q / QW, qx = q - y * QW;
+                        const int y = lg_div(q, QW, G.rQW), qx = q - y * QW;
                         if (qx < G.nA) {
                             const int pos = lg_sse_before(G, q, G.nA) - lg_sse_before(G, a, G.nA);
 #pragma unroll
@@ -426,7 +519,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                             }
                         }
                     };
-                    float acc = lg_tiles<3, kLgTQA>(qs, NQ, PL, 15, (float)base0, writeA, geoA);
+                    float acc = lg_tiles<3, kLgTQA>(qs, NQ, PL, 15, (float)base0, loadA, storeA, geoA, [&](int) {});
                     if (tid < 64) {  // wave 0 combines in the SSE2 build's order
                         const int av = __float_as_int(acc);
 #pragma unroll
@@ -475,16 +568,14 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                 nwin++;
                 int w00, w01, w10, w11;
                 bilin_weights(__fsub_rn(nx, (float)inx), __fsub_rn(ny, (float)iny), w00, w01, w10, w11);
-                const LgJ JJ = lg_j(J, inx, iny, w, h, w00, w01, w10, w11);
+                const LgJ JJ = window_j(inx, iny, w00, w01, w10, w11);
                 // ---- main pass: the thread's quads in order, the 10 b chains as runs ----
                 int T1[5] = {0, 0, 0, 0, 0}, M1[5] = {0, 0, 0, 0, 0}, m1[5] = {0, 0, 0, 0, 0};
                 int T2[5] = {0, 0, 0, 0, 0}, M2[5] = {0, 0, 0, 0, 0}, m2[5] = {0, 0, 0, 0, 0};
                 int dmax = 0;
                 {
                     int y = y0, qx = x0;
-                    for (int k = 0; k < cnt; k++) {
-                        const int ix = k * NT + tid;
-                        const uint2 ip = IPs[ix], xp = XPs[ix], yp = YPs[ix];
+                    auto quad = [&](const uint2 &ip, const uint2 &xp, const uint2 &yp) {
                         int d[4];
                         lg_diffs(JJ, y, qx, ip, d);
                         const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
@@ -509,6 +600,24 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                             qx = 0;
                             y++;
                         }
+                    };
+                    // batches of kLgMB quads: their slot loads in flight together
+                    int k = 0;
+                    for (; k + kLgMB <= cnt; k += kLgMB) {
+                        uint2 ip[kLgMB], xp[kLgMB], yp[kLgMB];
+#pragma unroll
+                        for (int u = 0; u < kLgMB; u++) {
+                            const int ix = (k + u) * NT + tid;
+                            ip[u] = IPs[ix];
+                            xp[u] = XPs[ix];
+                            yp[u] = YPs[ix];
+                        }
+#pragma unroll
+                        for (int u = 0; u < kLgMB; u++) quad(ip[u], xp[u], yp[u]);
+                    }
+                    for (; k < cnt; k++) {
+                        const int ix = k * NT + tid;
+                        quad(IPs[ix], XPs[ix], YPs[ix]);
                     }
                 }
                 LG_MARK(2);  // main pass
@@ -546,20 +655,24 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                     // ordered float chains from half wave h0 on (chain lanes: wave 0, lanes
                     // 0-9, from their exact prefixes base0), tiles of kLgTQB quads
                     const int qs = min(h0 * 32 * K, NQ);
-                    auto geoB = [&](int a, int b, int &nsse, int &ntail) {
-                        nsse = lg_sse_before(G, b, G.nB2) - lg_sse_before(G, a, G.nB2);
-                        ntail = lg_tail_before(G, b, G.nB2, G.tB) - lg_tail_before(G, a, G.nB2, G.tB);
+                    auto geoB = [&](int q, int &bs, int &bt) {
+                        bs = lg_sse_before(G, q, G.nB2);
+                        bt = lg_tail_before(G, q, G.nB2, G.tB);
                     };
-                    auto writeB = [&](int a, int b, float *buf) {
-                        const int q = a + tid - 64;  // waves 1-3 write
-                        if (tid < 64 || q >= b) return;
-                        const int t = q / K, idx = (q - t * K) * NT + t;
-                        const int y = q / QW, qx = q - y * QW;
-                        const uint2 ip = IPs[idx], xp = XPs[idx], yp = YPs[idx];
+                    auto loadB = [&](int q) {
+                        const int t = lg_div(q, K, G.rK), idx = (q - t * K) * NT + t;
+                        LgQ v;
+                        v.ip = IPs[idx];
+                        v.xp = XPs[idx];
+                        v.yp = YPs[idx];
+                        return v;
+                    };
+                    auto storeB = [&](const LgQ &v, int q, int a, float *buf) {
+                        const int y = lg_div(q, QW, G.rQW), qx = q - y * QW;
                         int d[4];
-                        lg_diffs(JJ, y, qx, ip, d);
-                        const int gx[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
-                        const int gy[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
+                        lg_diffs(JJ, y, qx, v.ip, d);
+                        const int gx[4] = {lo16(v.xp.x), hi16(v.xp.x), lo16(v.xp.y), hi16(v.xp.y)};
+                        const int gy[4] = {lo16(v.yp.x), hi16(v.yp.x), lo16(v.yp.y), hi16(v.yp.y)};
                         const int PLB = lg_plane(kLgTQB), SR = lg_sreg(kLgTQB);
                         if (qx < G.nB2) {
                             const int pos = lg_sse_before(G, q, G.nB2) - lg_sse_before(G, a, G.nB2);
@@ -581,7 +694,19 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                         }
                     };
                     LG_MARK(4);
-                    const float acc = lg_tiles<2, kLgTQB>(qs, NQ, PL, 10, (float)base0, writeB, geoB);
+                    auto markB = [&](int i) {
+                        if (i == 0) {
+                            LG_MARK(18);  // ordered b chains: pads of the next tile
+                            LG_COUNT(14);
+                        } else if (i == 1) {
+                            LG_MARK(13);  // barrier wait
+                        } else if (i == 2) {
+                            LG_MARK(16);  // writes, loads, tile geometry
+                        } else {
+                            LG_MARK(17);  // chain sums
+                        }
+                    };
+                    const float acc = lg_tiles<2, kLgTQB>(qs, NQ, PL, 10, (float)base0, loadB, storeB, geoB, markB);
                     LG_MARK(5);  // ordered b chains
                     if (tid < 64) {  // wave 0 combines in the SSE2 build's order
                         const int a = __float_as_int(acc);
@@ -637,13 +762,13 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                 }
                 int w00, w01, w10, w11;
                 bilin_weights(__fsub_rn(qxf, (float)iqx), __fsub_rn(qyf, (float)iqy), w00, w01, w10, w11);
-                const LgJ JJ = lg_j(J, iqx, iqy, w, h, w00, w01, w10, w11);
+                const LgJ JJ = window_j(iqx, iqy, w00, w01, w10, w11);
                 unsigned e = 0;
                 {
                     int y = y0, qx = x0;
-                    for (int k = 0; k < cnt; k++) {
+                    auto quad = [&](const uint2 &ip) {
                         int d[4];
-                        lg_diffs(JJ, y, qx, IPs[k * NT + tid], d);
+                        lg_diffs(JJ, y, qx, ip, d);
 #pragma unroll
                         for (int i = 0; i < 4; i++)
                             if (4 * qx + i < w) e = sat_add(e, (unsigned)abs(d[i]));
@@ -651,7 +776,16 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                             qx = 0;
                             y++;
                         }
+                    };
+                    int k = 0;
+                    for (; k + kLgMB <= cnt; k += kLgMB) {
+                        uint2 ip[kLgMB];
+#pragma unroll
+                        for (int u = 0; u < kLgMB; u++) ip[u] = IPs[(k + u) * NT + tid];
+#pragma unroll
+                        for (int u = 0; u < kLgMB; u++) quad(ip[u]);
                     }
+                    for (; k < cnt; k++) quad(IPs[k * NT + tid]);
                 }
                 e = wave_sum_sat(e);
                 if (lane == 0) EP[tid >> 6] = (int)e;
@@ -664,12 +798,12 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                     float acc = 0.f;
                     for (int a = 0; a < NQ; a += kLgTQE) {
                         const int b = min(a + kLgTQE, NQ);
-                        const int pa = (a / QW) * w + 4 * (a % QW);  // row-major pixel index of quad a
+                        const int pa = lg_div(a, QW, G.rQW) * w + 4 * (a - lg_div(a, QW, G.rQW) * QW);  // row-major pixel index of quad a
                         __syncthreads();
                         const int q = a + tid;
                         if (q < b) {
-                            const int t = q / K, idx = (q - t * K) * NT + t;
-                            const int y = q / QW, qx = q - y * QW;
+                            const int t = lg_div(q, K, G.rK), idx = (q - t * K) * NT + t;
+                            const int y = lg_div(q, QW, G.rQW), qx = q - y * QW;
                             int d[4];
                             lg_diffs(JJ, y, qx, IPs[idx], d);
 #pragma unroll
@@ -677,7 +811,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                                 if (4 * qx + i < w) PL[y * w + 4 * qx + i - pa] = (float)abs(d[i]);
                         }
                         __syncthreads();
-                        const int pb = b < NQ ? (b / QW) * w + 4 * (b % QW) : w * h;
+                        const int pb = b < NQ ? lg_div(b, QW, G.rQW) * w + 4 * (b - lg_div(b, QW, G.rQW) * QW) : w * h;
                         if (tid == 0) acc = chain_sum(PL, pb - pa, acc);
                     }
                     if (tid == 0) RS[8] = acc;
@@ -694,7 +828,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
             LG_CLK(t_end);
             lg_acc[15] = t_end - lg_t0;
             if (tid == 0 && A.stamps)
-                for (int i = 0; i < 16; i++) A.stamps[(size_t)g * 64 + i] = lg_acc[i];
+                for (int i = 0; i < 24; i++) A.stamps[(size_t)g * 64 + i] = lg_acc[i];
         }
 #endif
         if (tid == 0) {

@@ -393,17 +393,20 @@ def test_configs3_2048_points(oracle_mod, win):
 BORDER_PTS_1080 = np.array([[3, 4], [1915.5, 1077.25], [-20, 500], [960, 1079.5], [40, 1060]], np.float32)
 
 
+@pytest.mark.parametrize("jr", [1, 0])
 @pytest.mark.parametrize("win,flags", [((100, 250), 0), ((160, 400), 0), ((200, 200), 0), ((130, 130), 0),
                                        ((111, 277), 0), ((100, 250), ACCUM_SCALAR), ((150, 375), GET_MIN_EIGENVALS)])
-def test_lk_large_windows_1080p(oracle_mod, win, flags):
+def test_lk_large_windows_1080p(oracle_mod, win, flags, jr):
     """Tracker2D box windows above the LDS-resident sizes (PETS-scale pedestrians
     at 1080p: forward w x h, backward w x w) run lk_kernel_lg, bit for bit the
-    oracle -- SSE2 tails, the scalar build, min-eigenvalue output, border points."""
+    oracle -- SSE2 tails, the scalar build, min-eigenvalue output, border points;
+    with the iterations' J region in LDS where it fits (jr=1) and from the level
+    (jr=0, variant lg_jr=0)."""
     sc, f0, f1 = scene_pair(13, 1920, 1080, 24, box_w=win[0], box_h=win[1])
     pts = np.concatenate([sc.points_at(0), BORDER_PTS_1080])
     ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
-    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
-    assert_same(gpu, ref, f"win {win} flags {flags}")
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags, variants={"lg_jr": jr})
+    assert_same(gpu, ref, f"win {win} flags {flags} jr {jr}")
     assert ref[1].sum() >= 12
 
 
@@ -416,15 +419,15 @@ def test_lk_large_window_4k_5level(oracle_mod):
     assert_same(gpu, ref, "4k 128x320")
 
 
-@pytest.mark.parametrize("lg_lds", [0, 4096])
+@pytest.mark.parametrize("lg_lds,jr", [(0, 1), (4096, 1), (0, 0)])
 @pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
-def test_lk_large_kernel_all_shapes(oracle_mod, lg_lds, flags):
+def test_lk_large_kernel_all_shapes(oracle_mod, lg_lds, jr, flags):
     """The large-window kernel forced for every window (variant large=1), with
-    its default row bands and with 4 KB bands (many bands per window: the
-    ordered chains continue band to band)."""
+    its default row bands and with 4 KB bands (many bands per window), the J
+    region in LDS and from the level (lg_jr=0)."""
     sc, f0, f1 = scene_pair(15, 640, 480, 40)
     pts = np.concatenate([sc.points_at(0), np.array([[0, 0], [639.5, 479.5], [-8, 200], [320, 485]], np.float32)])
-    env = {"large": 1}
+    env = {"large": 1, "lg_jr": jr}
     if lg_lds:
         env["lg_lds"] = lg_lds
     for win in [(21, 21), (3, 3), (9, 15), (33, 33), (64, 64), (45, 120), (37, 50), (100, 60)]:

@@ -29,13 +29,15 @@ def main():
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--shapes", default="64x64,64x160")
     ap.add_argument("--lib", default=None, help="a libpsn_lk.so build to time (default: the product library)")
+    ap.add_argument("--variants", default="", help="context variants, e.g. lg_jr=0,large=1")
     args = ap.parse_args()
+    variants = {k: int(v) for k, v in (kv.split("=") for kv in args.variants.split(",") if kv)}
     sc = synth.make_scene(0, 1920, 1080, args.points, nboxes=8)
     f0, f1 = sc.frame(0), sc.frame(1)
     pts = sc.points_at(1)
     L = _lib.load(args.lib)
-    out = {"points": args.points, "reps": args.reps}
-    with lk.LKContext(1920, 1080, ring_slots=2, max_level_cap=3) as ctx:
+    out = {"points": args.points, "reps": args.reps, "variants": variants}
+    with lk.LKContext(1920, 1080, ring_slots=2, max_level_cap=3, variants=variants) as ctx:
         ctx.push_frame(0, f0)
         ctx.push_frame(1, f1)
         for shape in args.shapes.split(","):

@@ -29,6 +29,8 @@ def main():
     variants = {"large": 1}
     if os.environ.get("LG_LDS"):
         variants["lg_lds"] = int(os.environ["LG_LDS"])
+    if os.environ.get("LG_JR"):
+        variants["lg_jr"] = int(os.environ["LG_JR"])
     sc = synth.make_scene(0, 1920, 1080, npts, nboxes=8, box_w=w, box_h=h)
     f0, f1 = sc.frame(0), sc.frame(1)
     pts = sc.points_at(1)
@@ -54,6 +56,8 @@ def main():
            "wg_cycles_mean": float(tot.mean()), "wg_cycles_max": int(tot.max()),
            "iterations_mean": float(s[:, 10].mean()), "fallback_fraction": round(float(s[:, 11].sum() / it), 3),
            "mean": {k: round(float(v), 1) for k, v in zip(PHASES, s[:, :7].mean(0))},
+           "a_values_split": {k: round(float(s[:, i].mean()), 1) for i, k in [(7, "stage"), (8, "scharr"), (9, "quads")]},
+           "fb_tiles_split": {k: round(float(s[:, i].sum() / max(int(s[:, 11].sum()), 1)), 1) for i, k in [(16, "pre"), (17, "chain_sums"), (18, "pad"), (13, "barrier"), (14, "tiles")]},
            "per_iteration": {k: round(float(s[:, i].sum() / it), 1) for i, k in enumerate(PHASES) if i >= 2}}
     print(json.dumps(out, indent=1))
 
