@@ -531,6 +531,11 @@ static int wait_prev_build(psn_lk_ctx *c, int slot, hipStream_t s) {
     return PSN_LK_OK;
 }
 
+// Top-level tile of a standalone pyramid build (the level-0 region of a tile is
+// 2^top * T + 3 * (2^top - 1) px square: larger tiles re-read less halo).
+#ifndef PSN_PYR_TILE
+#define PSN_PYR_TILE 8
+#endif
 // Pyramid-build arguments of `slot` from a device source frame.
 static psn::PyrBuildArgs build_args(const psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
     psn::PyrBuildArgs a{};
@@ -538,7 +543,7 @@ static psn::PyrBuildArgs build_args(const psn_lk_ctx *c, int slot, const uint8_t
     a.src_stride = stride;
     a.channels = channels;
     a.nlevels = c->nlevels;
-    a.tile = (c->nlevels - 1) <= 4 ? 8 : 4;
+    a.tile = (c->nlevels - 1) <= 4 ? PSN_PYR_TILE : 4;
     for (int l = 0; l < c->nlevels; l++) a.lv[l] = c->h_slots[(size_t)slot * psn::kMaxLevels + l];
     return a;
 }
@@ -553,6 +558,7 @@ static int push_device_impl(psn_lk_ctx *c, int slot, const uint8_t *dev, int str
         c->pend = true;
         c->pend_slot = slot;
         c->pend_args = a;
+        c->pend_args.tile = (c->nlevels - 1) <= 4 ? 8 : 4;  // inside the LK launch's LDS budget
         return PSN_LK_OK;
     }
     hipStream_t s = c->stream;

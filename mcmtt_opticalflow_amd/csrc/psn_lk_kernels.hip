@@ -2652,12 +2652,12 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     const int ep = ++fb_epoch, wv = ftid >> 6, fl = ftid & 63;
                     auto tag = [&](int g) { return ep * 16 + g; };
                     auto spin = [&](int idx, int want) {
-                        int n = 0;
-                        for (; n < (1 << 22); n++) {  // (a bound: never a hang)
+                        for (int n = 0; n < (1 << 22); n++) {  // (a bound: never a hang)
                             if (__builtin_amdgcn_readfirstlane(FLG[idx]) == want) break;
                             __builtin_amdgcn_s_sleep(1);
                         }
-                        if (n == (1 << 22)) FLG[6] = 1;  // the tile may be half written: fail the point
+                        // the bound ran out: the tile may be half written, fail the point
+                        if (__builtin_amdgcn_readfirstlane(FLG[idx]) != want) FLG[6] = 1;
                         asm volatile("" ::: "memory");
                     };
                     for (int g = max(h0, 2 * wv); g <= min(2 * wv + 1, g_last); g++) {
