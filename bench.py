@@ -414,9 +414,11 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ticks = []  # host time after each step (its frame's results are in host memory): no sync added
     for i in range(steps):
         j = warmup + i
         gathered = step(t, seq[j], seq[j + 1])
+        ticks.append(time.perf_counter())
         t += 1
     torch.cuda.synchronize()
     barrier(world)
@@ -454,6 +456,7 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         isolated = isolated_launches(args, C)
     box_sizes = [[[int(fd.scene.box_ws[k]), int(fd.scene.box_hs[k])] for k in range(args.boxes)] for fd in feeds]
     return {"elapsed": elapsed, "steps": steps, "warmup": warmup, "cams_per_rank": C, "world": world,
+            "step_ends": [x - t0 for x in ticks],
             "box_sizes": box_sizes, "isolated": isolated,
             "measure_steps": measure,
             "per_kernel": per_kernel, "ts": ts, "samples": samples, "objs_last": objs_last,
@@ -734,6 +737,24 @@ def tracker_roofline(args, r, C, profile):
     return out
 
 
+def segment_rates(r, cams, nseg=5):
+    """SURVEY 8(d)'s median of 5: the timed steps cut into five consecutive
+    segments by the host clock at each step's end (this rank's view; no sync
+    inside the timed region), camera-frames/s per segment and their median.
+    `value` stays the whole timed region's rate."""
+    ends = r.get("step_ends") or []
+    n = len(ends)
+    if n < nseg:
+        return None
+    cuts = [round(k * n / nseg) for k in range(nseg + 1)]
+    vals = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        t_a = ends[a - 1] if a > 0 else 0.0
+        vals.append(cams * (b - a) / (ends[b - 1] - t_a))
+    return {"n": nseg, "steps_each": [b - a for a, b in zip(cuts[:-1], cuts[1:])],
+            "values": [round(v, 2) for v in vals], "median": round(float(np.median(vals)), 2)}
+
+
 def tracker_line(args, r, world, C, scaling, profile):
     """The JSON line of a Tracker2D run (rank 0)."""
     fps_all = world * C * r["steps"] / r["elapsed"]
@@ -785,6 +806,7 @@ def tracker_line(args, r, world, C, scaling, profile):
                     "definition": "SURVEY 8(d): sum over points and levels of w*h*(1 + iterations), "
                                   "counted on the device"},
         "frames_per_set_per_s": round(r["steps"] / r["elapsed"], 2),
+        "segments": segment_rates(r, world * C),
         "result_objects_last_frame": r["objs_last"],
         "cpu_baseline": None,
     }

@@ -179,6 +179,10 @@ def test_lk_empty_and_errors():
         with pytest.raises(PsnLkError) as e:  # wider than one LDS row band
             ctx.track([q], np.array([[30, 20]], np.float32))
         assert e.value.code == -8
+        q = glk.make_query(0, 1, 0, 1, glk.make_params((4096, 4097), 0))
+        with pytest.raises(PsnLkError) as e:  # 2^22 quads: past the kernel's exact quad division
+            ctx.track([q], np.array([[30, 20]], np.float32))
+        assert e.value.code == -8
 
 
 def test_lk_batched_queries_ring(oracle_mod):
