@@ -284,7 +284,10 @@ __host__ __device__ inline int lg_lds_bytes(int w, int h, int tr, bool jr) {
     const int it = lg_tiles_b_bytes() + (jr ? lg_jr_bytes(w, h) : 0);
     return lg_scr_bytes() + (u > it ? u : it);
 }
-constexpr int kLgJrMaxLds = 80 * 1024;  // J region in LDS while the workgroup fits this (2 per CU)
+#ifndef PSN_LG_JR_MAX_KB
+#define PSN_LG_JR_MAX_KB 80
+#endif
+constexpr int kLgJrMaxLds = PSN_LG_JR_MAX_KB * 1024;  // J region in LDS while the workgroup fits this (80 KB: 2 per CU)
 __host__ __device__ inline int lg_quads_per_thread(int w, int h) { return (h * ((w + 3) >> 2) + kLgNT - 1) / kLgNT; }
 // window-value slot of one workgroup, in 8-byte units
 __host__ __device__ inline long long lg_slot_int2(int w, int h) { return 3LL * kLgNT * lg_quads_per_thread(w, h); }
