@@ -265,8 +265,11 @@ inline int bx_err_rows(int w, int h, int pb) {
 // patch + Scharr plane (A phase) and the double-buffered tile planes of the
 // ordered-chain fallbacks (A: 3 planes of kLgTQA quads, b: 2 of kLgTQB).
 constexpr int kLgNT = 256;
-constexpr int kLgTQA = 128;  // quads per A fallback tile (<= 192: waves 1-3 write a tile)
-constexpr int kLgTQB = 128;  // quads per b fallback tile (<= 192)
+#ifndef PSN_LG_TQ
+#define PSN_LG_TQ 128
+#endif
+constexpr int kLgTQA = PSN_LG_TQ;  // quads per A fallback tile (<= 192: waves 1-3 write a tile)
+constexpr int kLgTQB = PSN_LG_TQ;  // quads per b fallback tile (<= 192)
 constexpr int kLgTQE = 128;  // quads per err fallback tile (one row-major chain)
 __host__ __device__ constexpr int lg_sreg(int tq) { return ((tq + 15) & ~15) + 4; }  // SSE chain region (floats)
 __host__ __device__ constexpr int lg_plane(int tq) { return 4 * lg_sreg(tq) + ((4 * tq + 15) & ~15) + 4; }
