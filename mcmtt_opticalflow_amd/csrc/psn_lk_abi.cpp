@@ -686,6 +686,7 @@ struct PlannedQuery {
     int tiled_tr = 0;           // row-tiled kernel: tile rows (0: window not LDS-resident)
     int lg_tr = 0;              // large-window kernel: band rows
     bool lg_jr = false;         // + J region in LDS
+    int lg_tq = 192;            // + quads per ordered-chain tile
     int cls = kClsLg, key = 0;  // the launch it goes to
 };
 
@@ -701,19 +702,31 @@ static int tiled_rows(const psn_lk_ctx *c, int w, int h) {
 }
 // Band rows of the large-window kernel's A phase within its LDS budget (>= 1 row;
 // the tile planes of the fallbacks set the floor of the budget).
-static int lg_rows(const psn_lk_ctx *c, int w, int h, bool jr) {
+static int lg_rows(const psn_lk_ctx *c, int w, int h, bool jr, int tq) {
     int tr = 1;
-    const int budget = std::max(c->lg_lds, psn::lg_lds_bytes(w, h, 1, jr));
-    while (tr < h && psn::lg_lds_bytes(w, h, tr + 1, jr) <= budget) tr++;
+    const int budget = std::max(c->lg_lds, psn::lg_lds_bytes(w, h, 1, jr, tq));
+    while (tr < h && psn::lg_lds_bytes(w, h, tr + 1, jr, tq) <= budget) tr++;
     return tr;
 }
-// The J region of the large-window kernel's iterations in LDS: the workgroup
-// within kLgJrMaxLds, and the region's dword rows exactly divisible by the
-// staging's magic (q * (d - 1) < 2^22 and q * magic < 2^32 for every dword q).
-static bool lg_jr_fits(const psn_lk_ctx *c, int w, int h) {
-    if (!c->lg_jr || psn::lg_lds_bytes(w, h, 1, true) > psn::kLgJrMaxLds) return false;
+// The large-window kernel's plan: the J region of the iterations in LDS with the
+// largest ordered-chain tile (kLgTQs) that keeps the workgroup within
+// kLgJrMaxLds (J staging needs the region's dword rows exactly divisible by the
+// staging's magic: q * (d - 1) < 2^22 and q * magic < 2^32 for every dword q),
+// else J from the level with kLgTQNoJr-quad tiles (measured with
+// tools/gpu_lg_ab.sh, 512 points: 100x250 981 -> 858 us with 192-quad tiles;
+// without the LDS J region 192-quad tiles were slower than 128 at 140x357).
+static void lg_plan(const psn_lk_ctx *c, int w, int h, bool &jr, int &tq) {
+    jr = false;
+    tq = psn::kLgTQNoJr;
+    if (!c->lg_jr) return;
     const long long d = psn::bx_jrp(w) / 4, n = (long long)psn::st_jreg_h(h) * d;
-    return n * (d - 1) < (1LL << 22) && n * (long long)psn::div_magic((int)d) < (1LL << 32);
+    if (!(n * (d - 1) < (1LL << 22) && n * (long long)psn::div_magic((int)d) < (1LL << 32))) return;
+    for (int t : psn::kLgTQs)
+        if (psn::lg_lds_bytes(w, h, 1, true, t) <= psn::kLgJrMaxLds) {
+            jr = true;
+            tq = t;
+            return;
+        }
 }
 
 // Validate and plan one query.
@@ -751,8 +764,8 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
         }
     }
     pq.tiled_tr = tiled_rows(c, w, h);
-    pq.lg_jr = lg_jr_fits(c, w, h);
-    pq.lg_tr = lg_rows(c, w, h, pq.lg_jr);
+    lg_plan(c, w, h, pq.lg_jr, pq.lg_tq);
+    pq.lg_tr = lg_rows(c, w, h, pq.lg_jr, pq.lg_tq);
     d.prev_slot = q.prev_slot;
     d.next_slot = q.next_slot;
     d.pt_begin = q.first_pt;
@@ -804,6 +817,7 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
         pq.cls = kClsLg;
     }
     if (pq.cls == kClsLg) {
+        pq.key = pq.lg_tq;  // one launch per tile size
         d.tile_rows = pq.lg_tr;
         d.lg_jr = pq.lg_jr ? 1 : 0;
         if (pq.lg_jr) d.dv_bxjr = psn::div_magic(psn::bx_jrp(w) / 4);
@@ -937,7 +951,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
     lds = 0;
     for (int i = 0; i < a.nq; i++) {
         slot = std::max(slot, psn::lg_slot_int2(a.q[i].win_w, a.q[i].win_h));
-        lds = std::max(lds, psn::lg_lds_bytes(a.q[i].win_w, a.q[i].win_h, a.q[i].tile_rows, a.q[i].lg_jr != 0));
+        lds = std::max(lds, psn::lg_lds_bytes(a.q[i].win_w, a.q[i].win_h, a.q[i].tile_rows, a.q[i].lg_jr != 0, key));
     }
     const size_t slot_bytes = (size_t)slot * 8;
     const long long fit = std::max<long long>((long long)(kLgWsBudget / slot_bytes), 64);
@@ -949,7 +963,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
     a.lg_slot = slot;
     a.lk_wgs = wgs;
     a.total_wgs = wgs;
-    HIPCHK(c, psn::launch_lk_lg(a, grid, lds, c->stream));
+    HIPCHK(c, psn::launch_lk_lg(a, grid, lds, key, c->stream));
     return PSN_LK_OK;
 }
 

@@ -263,28 +263,29 @@ inline int bx_err_rows(int w, int h, int pb) {
 // (3 x 256 x K uint2: I*, Ix*, Iy* of every quad as packed pairs, K quads per
 // thread) and LDS: the chain-check records | a union of one row band of the I
 // patch + Scharr plane (A phase) and the double-buffered tile planes of the
-// ordered-chain fallbacks (A: 3 planes of kLgTQA quads, b: 2 of kLgTQB).
+// ordered-chain fallbacks (A: 3 planes of TQ quads, b: 2 of TQ).
 constexpr int kLgNT = 256;
-#ifndef PSN_LG_TQ
-#define PSN_LG_TQ 128
-#endif
-constexpr int kLgTQA = PSN_LG_TQ;  // quads per A fallback tile (<= 192: waves 1-3 write a tile)
-constexpr int kLgTQB = PSN_LG_TQ;  // quads per b fallback tile (<= 192)
+// fallback tile sizes (quads per tile; <= 192: waves 1-3 write a tile, one quad
+// per thread): the kernel is built for each, the planner takes the largest whose
+// workgroup keeps the J region in LDS within kLgJrMaxLds, else (J from the
+// level) kLgTQNoJr
+constexpr int kLgTQs[2] = {192, 128};
+constexpr int kLgTQNoJr = 128;
 constexpr int kLgTQE = 128;  // quads per err fallback tile (one row-major chain)
 __host__ __device__ constexpr int lg_sreg(int tq) { return ((tq + 15) & ~15) + 4; }  // SSE chain region (floats)
 __host__ __device__ constexpr int lg_plane(int tq) { return 4 * lg_sreg(tq) + ((4 * tq + 15) & ~15) + 4; }
 __host__ __device__ inline int lg_scr_bytes() { return align16((kBxXInts + 32) * 4); }
-__host__ __device__ inline int lg_tiles_a_bytes() { return 2 * 3 * lg_plane(kLgTQA) * 4 + 1024; }
+__host__ __device__ constexpr int lg_tiles_a_bytes(int tq) { return 2 * 3 * lg_plane(tq) * 4 + 1024; }
 // + slack: the chain sums read up to 5 blocks past a chain (discarded)
-__host__ __device__ inline int lg_tiles_b_bytes() { return 2 * 2 * lg_plane(kLgTQB) * 4 + 1024; }
+__host__ __device__ constexpr int lg_tiles_b_bytes(int tq) { return 2 * 2 * lg_plane(tq) * 4 + 1024; }
 // A phase band: tr + 3 rows of the I patch, bx_pm(w) dwords each
 __host__ __device__ inline int lg_band_bytes(int w, int tr) { return align16((tr + 3) * 4 * bx_pm(w)); }
 // J region of the iterations (lg_jr): st_jreg_h(h) rows of bx_jrp(w) bytes, after the b tiles
 __host__ __device__ inline int lg_jr_bytes(int w, int h) { return align16(st_jreg_h(h) * bx_jrp(w)); }
-__host__ __device__ inline int lg_lds_bytes(int w, int h, int tr, bool jr) {
+__host__ __device__ inline int lg_lds_bytes(int w, int h, int tr, bool jr, int tq) {
     int u = lg_band_bytes(w, tr);
-    u = u > lg_tiles_a_bytes() ? u : lg_tiles_a_bytes();
-    const int it = lg_tiles_b_bytes() + (jr ? lg_jr_bytes(w, h) : 0);
+    u = u > lg_tiles_a_bytes(tq) ? u : lg_tiles_a_bytes(tq);
+    const int it = lg_tiles_b_bytes(tq) + (jr ? lg_jr_bytes(w, h) : 0);
     return lg_scr_bytes() + (u > it ? u : it);
 }
 #ifndef PSN_LG_JR_MAX_KB
@@ -309,7 +310,7 @@ hipError_t launch_lk(const LkLaunchArgs &a, int total_wgs, int threads, int lds_
 // (no scalar-tail chain: a build without its per-pixel bookkeeping)
 hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, bool notail, int lds_bytes, hipStream_t s);
 // Large-window kernel (psn_lk_large.hip): `grid` workgroups over a.lk_wgs points.
-hipError_t launch_lk_lg(const LkLaunchArgs &a, int grid, int lds_bytes, hipStream_t s);
+hipError_t launch_lk_lg(const LkLaunchArgs &a, int grid, int lds_bytes, int tq, hipStream_t s);
 hipError_t lg_kernels_init();
 hipError_t lk_kernels_init();   // raises the dynamic-LDS limit once
 

@@ -259,6 +259,8 @@ __device__ __forceinline__ float lg_tiles(int qs, int NQ, float *buf, int nch, f
 
 constexpr int kLgMB = 4;  // quads per batch of slot loads in the passes over the window
 
+// TQ: quads per ordered-chain tile (kLgTQs; the planner's choice per query)
+template <int TQ>
 __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NT = kLgNT;
@@ -268,7 +270,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
     int *EP = (int *)(RS + 16);
     uint8_t *U = smem + lg_scr_bytes();   // band staging | tile planes
     float *PL = (float *)U;
-    uint32_t *JR = (uint32_t *)(U + lg_tiles_b_bytes());  // J region (lg_jr), after the b tiles
+    uint32_t *JR = (uint32_t *)(U + lg_tiles_b_bytes(TQ));  // J region (lg_jr), after the b tiles
     uint8_t *const slot = (uint8_t *)A.lg_ws + (long long)blockIdx.x * A.lg_slot * 8;
     const float FLT_SCALE = 1.f / (1 << 20);
     int par = 0;
@@ -496,7 +498,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                     auto storeA = [&](const LgQ &v, int q, int a, float *buf) {
                         const int gx[4] = {lo16(v.xp.x), hi16(v.xp.x), lo16(v.xp.y), hi16(v.xp.y)};
                         const int gy[4] = {lo16(v.yp.x), hi16(v.yp.x), lo16(v.yp.y), hi16(v.yp.y)};
-                        const int PLA = lg_plane(kLgTQA), SR = lg_sreg(kLgTQA);
+                        const int PLA = lg_plane(TQ), SR = lg_sreg(TQ);
                         const int y = lg_div(q, QW, G.rQW), qx = q - y * QW;
                         if (qx < G.nA) {
                             const int pos = lg_sse_before(G, q, G.nA) - lg_sse_before(G, a, G.nA);
@@ -519,7 +521,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                             }
                         }
                     };
-                    float acc = lg_tiles<3, kLgTQA>(qs, NQ, PL, 15, (float)base0, loadA, storeA, geoA, [&](int) {});
+                    float acc = lg_tiles<3, TQ>(qs, NQ, PL, 15, (float)base0, loadA, storeA, geoA, [&](int) {});
                     if (tid < 64) {  // wave 0 combines in the SSE2 build's order
                         const int av = __float_as_int(acc);
 #pragma unroll
@@ -653,7 +655,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                 } else {
                     LG_COUNT(11);
                     // ordered float chains from half wave h0 on (chain lanes: wave 0, lanes
-                    // 0-9, from their exact prefixes base0), tiles of kLgTQB quads
+                    // 0-9, from their exact prefixes base0), tiles of TQ quads
                     const int qs = min(h0 * 32 * K, NQ);
                     auto geoB = [&](int q, int &bs, int &bt) {
                         bs = lg_sse_before(G, q, G.nB2);
@@ -673,7 +675,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                         lg_diffs(JJ, y, qx, v.ip, d);
                         const int gx[4] = {lo16(v.xp.x), hi16(v.xp.x), lo16(v.xp.y), hi16(v.xp.y)};
                         const int gy[4] = {lo16(v.yp.x), hi16(v.yp.x), lo16(v.yp.y), hi16(v.yp.y)};
-                        const int PLB = lg_plane(kLgTQB), SR = lg_sreg(kLgTQB);
+                        const int PLB = lg_plane(TQ), SR = lg_sreg(TQ);
                         if (qx < G.nB2) {
                             const int pos = lg_sse_before(G, q, G.nB2) - lg_sse_before(G, a, G.nB2);
 #pragma unroll
@@ -706,7 +708,7 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                             LG_MARK(17);  // chain sums
                         }
                     };
-                    const float acc = lg_tiles<2, kLgTQB>(qs, NQ, PL, 10, (float)base0, loadB, storeB, geoB, markB);
+                    const float acc = lg_tiles<2, TQ>(qs, NQ, PL, 10, (float)base0, loadB, storeB, geoB, markB);
                     LG_MARK(5);  // ordered b chains
                     if (tid < 64) {  // wave 0 combines in the SSE2 build's order
                         const int a = __float_as_int(acc);
@@ -842,15 +844,24 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
     }
 }
 
-hipError_t launch_lk_lg(const LkLaunchArgs &a, int grid, int lds_bytes, hipStream_t s) {
+hipError_t launch_lk_lg(const LkLaunchArgs &a, int grid, int lds_bytes, int tq, hipStream_t s) {
     if (grid <= 0 || a.lk_wgs <= 0) return hipSuccess;
     if (!a.lg_ws || a.lg_slot <= 0 || lds_bytes > 160 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lk_kernel_lg, dim3(grid), dim3(kLgNT), lds_bytes, s, a);
+    switch (tq) {
+        case 192: hipLaunchKernelGGL(lk_kernel_lg<192>, dim3(grid), dim3(kLgNT), lds_bytes, s, a); break;
+        case 128: hipLaunchKernelGGL(lk_kernel_lg<128>, dim3(grid), dim3(kLgNT), lds_bytes, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
 hipError_t lg_kernels_init() {
-    return hipFuncSetAttribute((const void *)lk_kernel_lg, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    const void *f[2] = {(const void *)lk_kernel_lg<192>, (const void *)lk_kernel_lg<128>};
+    for (const void *k : f) {
+        const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace psn
