@@ -56,7 +56,7 @@ def main():
            "wg_cycles_mean": float(tot.mean()), "wg_cycles_max": int(tot.max()),
            "iterations_mean": float(s[:, 10].mean()), "fallback_fraction": round(float(s[:, 11].sum() / it), 3),
            "mean": {k: round(float(v), 1) for k, v in zip(PHASES, s[:, :7].mean(0))},
-           "a_values_split": {k: round(float(s[:, i].mean()), 1) for i, k in [(7, "stage"), (8, "scharr"), (9, "quads")]},
+           "a_values_split": {k: round(float(s[:, i].mean()), 1) for i, k in [(7, "stage"), (9, "quads")]},
            "fb_tiles_split": {k: round(float(s[:, i].sum() / max(int(s[:, 11].sum()), 1)), 1) for i, k in [(16, "pre"), (17, "chain_sums"), (18, "pad"), (13, "barrier"), (14, "tiles")]},
            "per_iteration": {k: round(float(s[:, i].sum() / it), 1) for i, k in enumerate(PHASES) if i >= 2}}
     print(json.dumps(out, indent=1))
