@@ -382,11 +382,19 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
 
     ahead = args.stage_ahead
 
+    parts = [] if args.step_profile else None  # (launch, pushes, complete_next) host ms per step
+
     def step(t, dets, next_dets):
+        c0 = time.perf_counter()
         group.launch(t, dets, gridfast=gridfast, seed=t)  # after complete_next(t-1): a confirmation
+        c1 = time.perf_counter()
         for k, fd in enumerate(feeds):  # frame t+ahead uploads (and builds) while frame t runs
             fd.push(group, k, t + ahead)
+        c2 = time.perf_counter()
         group.complete_next(t + 1, next_dets, gridfast=gridfast, seed=t + 1, raw=True)
+        if parts is not None:
+            parts.append((t, round(1e3 * (c1 - c0), 3), round(1e3 * (c2 - c1), 3),
+                          round(1e3 * (time.perf_counter() - c2), 3), group.debug_host_times()))
         for k in range(C):  # the hand-off slots (psn_t2d_pack_result) in host memory
             rc = T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
             if rc:
@@ -408,8 +416,10 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     measure = 0 if args.verify else args.measure_steps
     seq = [group.records(all_dets(t)) for t in range(warmup + steps + measure + 1)]
     t = 0
+    wticks = [time.perf_counter()]
     for i in range(warmup):
         step(t, seq[i], seq[i + 1])
+        wticks.append(time.perf_counter())
         t += 1
     barrier(world)
     torch.cuda.synchronize()
@@ -424,6 +434,11 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     barrier(world)
     elapsed = time.perf_counter() - t0
     elapsed = pdist.max_over_ranks(elapsed)
+    if parts is not None:
+        for p_ in parts:
+            if sum(p_[1:4]) > 4.0:
+                print(f"step {p_[0]}: launch {p_[1]} ms, pushes {p_[2]} ms, complete_next {p_[3]} ms {p_[4]}",
+                      file=sys.stderr)
     # after the timed region (events between the launches would perturb it): per-launch
     # HIP-event durations of every LK launch and the device window-sample count
     lkh = group.lk_handle()
@@ -457,6 +472,7 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     box_sizes = [[[int(fd.scene.box_ws[k]), int(fd.scene.box_hs[k])] for k in range(args.boxes)] for fd in feeds]
     return {"elapsed": elapsed, "steps": steps, "warmup": warmup, "cams_per_rank": C, "world": world,
             "step_ends": [x - t0 for x in ticks],
+            "warmup_step_ms": [round(1e3 * (b - a), 3) for a, b in zip(wticks[:-1], wticks[1:])],
             "box_sizes": box_sizes, "isolated": isolated,
             "measure_steps": measure,
             "per_kernel": per_kernel, "ts": ts, "samples": samples, "objs_last": objs_last,
@@ -751,8 +767,13 @@ def segment_rates(r, cams, nseg=5):
     for a, b in zip(cuts[:-1], cuts[1:]):
         t_a = ends[a - 1] if a > 0 else 0.0
         vals.append(cams * (b - a) / (ends[b - 1] - t_a))
+    dts = np.diff(np.concatenate([[0.0], np.asarray(ends)]))
+    slow = np.argsort(dts)[::-1][:3]
     return {"n": nseg, "steps_each": [b - a for a, b in zip(cuts[:-1], cuts[1:])],
-            "values": [round(v, 2) for v in vals], "median": round(float(np.median(vals)), 2)}
+            "values": [round(v, 2) for v in vals], "median": round(float(np.median(vals)), 2),
+            "step_ms_median": round(1e3 * float(np.median(dts)), 4),
+            "slowest_steps": [[int(i), round(1e3 * float(dts[i]), 3)] for i in slow],
+            "warmup_step_ms": r.get("warmup_step_ms")}
 
 
 def tracker_line(args, r, world, C, scaling, profile):
@@ -1178,6 +1199,7 @@ def parse_args(argv=None):
     ap.add_argument("--leg-steps", type=int, default=40)
     ap.add_argument("--measure-steps", type=int, default=20,
                     help="frames after the timed region with per-launch HIP-event timing (roofline)")
+    ap.add_argument("--step-profile", action="store_true", help="tracker mode: host ms of each slow step to stderr")
     ap.add_argument("--no-isolated", dest="isolated", action="store_false",
                     help="skip the isolated-launch timing of the frame-set's LK launches (roofline.isolated)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

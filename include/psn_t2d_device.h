@@ -68,6 +68,14 @@ int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_la
  * its step-1 inliers, or these features when no step keeps 4 inliers. */
 int psn_t2d_chain_begin_device(const psn_t2d_chain_dev *c, int min_count, void *hip_stream);
 
+/* d_dst[0, bytes) = h_src[0, bytes) by a kernel that reads the pinned host block
+ * (hipHostMalloc'd; both pointers 16-B aligned) over the bus, asynchronous on
+ * `hip_stream`. The Tracker2D pass inputs (chain boxes / counts / points,
+ * forward inputs: kilobytes) go up this way: a runtime copy of a small pinned
+ * block can hold the calling thread until the engine's earlier work drains
+ * (measured: 7-9 ms host stalls behind the staged frames' uploads). */
+int psn_t2d_upload_device(void *d_dst, const void *h_src, size_t bytes, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

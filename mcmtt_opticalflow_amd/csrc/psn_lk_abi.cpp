@@ -114,6 +114,7 @@ struct psn_lk_ctx {
         size_t bytes = 0;
     };
     std::vector<LgWs> lg_ws;
+    std::vector<void *> lg_retired;  // outgrown slot buffers, freed at destroy (hipFree would wait for the device)
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     unsigned long long *d_samples = nullptr;  // psn_lk_debug_count_samples
     bool count_samples = false;
@@ -315,6 +316,8 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     for (auto &ws : c->lg_ws)
         if (ws.p) (void)hipFree(ws.p);
     c->lg_ws.clear();
+    for (void *p : c->lg_retired) (void)hipFree(p);
+    c->lg_retired.clear();
     for (void *p : {(void *)c->d_samples, (void *)c->d_ctr, (void *)c->d_pyr, (void *)c->d_slots, (void *)c->d_src, (void *)c->d_prev, (void *)c->d_next,
                     (void *)c->d_err, (void *)c->d_status, (void *)c->d_gf_kp, (void *)c->d_gf_cnt, (void *)c->d_gf_xy,
                     (void *)c->d_gf_oc, (void *)c->d_gf_ot})
@@ -826,7 +829,11 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
     return PSN_LK_OK;
 }
 
-// The large-window kernel's slot buffer of the current stream, grown to `bytes`.
+// The large-window kernel's slot buffer of the current stream, grown to `bytes`
+// (to a power of two from 16 MB: the demand varies per call with the point
+// count and window sizes). The outgrown buffer may still be read by launches in
+// flight on the stream: it is retired, not freed, so growth never waits for
+// the device (at most the geometric sum, < 2x the final size, stays reserved).
 static int ensure_lg_ws(psn_lk_ctx *c, size_t bytes, void **out) {
     psn_lk_ctx::LgWs *ws = nullptr;
     for (auto &e : c->lg_ws)
@@ -837,14 +844,13 @@ static int ensure_lg_ws(psn_lk_ctx *c, size_t bytes, void **out) {
         ws->s = c->stream;
     }
     if (ws->bytes < bytes) {
-        if (ws->p) {  // earlier launches on this stream may still read the old slots
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            (void)hipFree(ws->p);
-            ws->p = nullptr;
-            ws->bytes = 0;
-        }
-        HIPCHK(c, hipMalloc(&ws->p, bytes));
-        ws->bytes = bytes;
+        size_t cap = (size_t)16 << 20;
+        while (cap < bytes) cap <<= 1;
+        void *p = nullptr;
+        HIPCHK(c, hipMalloc(&p, cap));
+        if (ws->p) c->lg_retired.push_back(ws->p);
+        ws->p = p;
+        ws->bytes = cap;
     }
     *out = ws->p;
     return PSN_LK_OK;

@@ -197,8 +197,30 @@ __global__ __launch_bounds__(128) void chain_begin_kernel(psn_t2d_chain_dev C, i
     }
 }
 
+// Pinned host block -> HBM: 16-B loads over the bus, grid-strided.
+__global__ __launch_bounds__(256) void upload_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src, size_t n16,
+                                                     uint8_t *__restrict__ dtail, const uint8_t *__restrict__ stail,
+                                                     int ntail) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < ntail) dtail[threadIdx.x] = stail[threadIdx.x];
+}
+
 }  // namespace
 }  // namespace psn
+
+extern "C" int psn_t2d_upload_device(void *d_dst, const void *h_src, size_t bytes, void *stream) {
+    if (bytes == 0) return PSN_LK_OK;
+    if (!d_dst || !h_src || ((uintptr_t)d_dst & 15) || ((uintptr_t)h_src & 15)) return PSN_LK_ERR_ARG;
+    void *src = nullptr;  // the block's device address (hipHostMalloc'd memory is mapped)
+    if (hipHostGetDevicePointer(&src, const_cast<void *>(h_src), 0) != hipSuccess || !src) return PSN_LK_ERR_ARG;
+    const size_t n16 = bytes / 16;
+    const int ntail = (int)(bytes % 16);
+    const int grid = (int)std::max<size_t>(1, std::min<size_t>((n16 + 255) / 256, 512));
+    hipLaunchKernelGGL(psn::upload_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4 *)d_dst,
+                       (const uint4 *)src, n16, (uint8_t *)d_dst + n16 * 16, (const uint8_t *)src + n16 * 16, ntail);
+    return hipGetLastError() == hipSuccess ? PSN_LK_OK : PSN_LK_ERR_HIP;
+}
 
 extern "C" int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *stream) {
     if (n < 0 || (n > 0 && !d_cnt)) return PSN_LK_ERR_ARG;

@@ -373,6 +373,15 @@ void Tracker2DFlow::Finalize() {
     cams_.clear();
 }
 
+// Buffer capacities grow geometrically (powers of two from `floor`): a regrow
+// drains the streams and reallocates pinned memory (milliseconds), so a
+// tracker population that creeps up frame by frame regrows O(log n) times.
+static size_t grow_cap(size_t need, size_t floor) {
+    size_t c = floor;
+    while (c < need) c *= 2;
+    return c;
+}
+
 // Chain buffers for nchains detections: grown only between passes (no chain in
 // flight on the chain stream).
 int Tracker2DFlow::EnsureChains(size_t nchains) {
@@ -388,7 +397,7 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
         chain_info_[r].valid = false;
         fread_rec_[r] = false;
     }
-    const size_t K = std::max<size_t>(nchains, 16);
+    const size_t K = grow_cap(nchains, 16);
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, npt = K * cap;
     bool ok = true;
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
@@ -438,7 +447,7 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
         keep_pts.assign(b.h_fwd_out, b.h_fwd_out + 2 * b.nfwd_pts);
     }
     b.release_forward();
-    const size_t F = std::max<size_t>(nfwd_pts, 1024), J = std::max<size_t>(nfwd_jobs, 16);
+    const size_t F = grow_cap(nfwd_pts, 1024), J = grow_cap(nfwd_jobs, 16);
     bool ok = true;
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
     auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
@@ -618,7 +627,8 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
             chk(hipMemcpyAsync(b.h_rawcnt, db.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
             chk(hipMemcpyAsync(b.h_in, db.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
             // boxes and last steps (GridFAST wrote the counts and points on the device)
-            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, dall.in_off_cnt, hipMemcpyHostToDevice, st), "chain boxes");
+            if (!rc && (rc = psn_t2d_upload_device(db.d_inblk, b.h_inblk, dall.in_off_cnt, st)))
+                err_ = "chain boxes upload";
         } else {
             for (PassCam &p : pc)
                 for (size_t i = 0; i < p.dets->size(); i++) {
@@ -637,8 +647,9 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
                 }
             // boxes, last steps, counts and points in one copy (whole rows: a chain
             // row's unused tail is never read)
-            chk(hipMemcpyAsync(db.d_inblk, b.h_inblk, dall.in_off_in + K * cap * 8, hipMemcpyHostToDevice, st),
-                "chain inputs");
+            // (a kernel reads the pinned block: psn_t2d_upload_device)
+            if (!rc && (rc = psn_t2d_upload_device(db.d_inblk, b.h_inblk, dall.in_off_in + K * cap * 8, st)))
+                err_ = "chain inputs upload";
         }
         if (rc) return rc;
         // the result block's last reader (a forward launch three frames back) first
@@ -831,7 +842,8 @@ int Tracker2DFlow::PassLaunchForward(std::vector<PassCam> &pc) {
         // (one input block: the other stream's last launch has read it)
         chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_fend_[par ^ 1], 0), "forward input block event");
         chk(hipStreamWaitEvent(fs, (hipEvent_t)ev_fcopied_[par], 0), "forward block event");
-        chk(hipMemcpyAsync(b.d_fiblk, b.h_fiblk, b.fi_off_pts + F * 8, hipMemcpyHostToDevice, fs), "forward inputs");
+        if (!rc && (rc = psn_t2d_upload_device(b.d_fiblk, b.h_fiblk, b.fi_off_pts + F * 8, fs)))
+            err_ = "forward inputs upload";
         if (rc) return rc;
         rc = psn_lk_set_stream(lk_, fs);
         if (!rc)
