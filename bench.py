@@ -430,6 +430,8 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         gathered = step(t, seq[j], seq[j + 1])
         ticks.append(time.perf_counter())
         t += 1
+        if i == args.diag_sync_at:  # diagnostic runs only: a device sync inside the timed region
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
@@ -1199,6 +1201,7 @@ def parse_args(argv=None):
     ap.add_argument("--leg-steps", type=int, default=40)
     ap.add_argument("--measure-steps", type=int, default=20,
                     help="frames after the timed region with per-launch HIP-event timing (roofline)")
+    ap.add_argument("--diag-sync-at", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--step-profile", action="store_true", help="tracker mode: host ms of each slow step to stderr")
     ap.add_argument("--no-isolated", dest="isolated", action="store_false",
                     help="skip the isolated-launch timing of the frame-set's LK launches (roofline.isolated)")

@@ -69,12 +69,16 @@ int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_la
 int psn_t2d_chain_begin_device(const psn_t2d_chain_dev *c, int min_count, void *hip_stream);
 
 /* d_dst[0, bytes) = h_src[0, bytes) by a kernel that reads the pinned host block
- * (hipHostMalloc'd; both pointers 16-B aligned) over the bus, asynchronous on
+ * (hipHostMalloc'd, coherent; both pointers 16-B aligned) over the bus, asynchronous on
  * `hip_stream`. The Tracker2D pass inputs (chain boxes / counts / points,
  * forward inputs: kilobytes) go up this way: a runtime copy of a small pinned
  * block can hold the calling thread until the engine's earlier work drains
- * (measured: 7-9 ms host stalls behind the staged frames' uploads). */
+ * (measured: 7-9 ms host stalls, the first copies after a device sync). */
 int psn_t2d_upload_device(void *d_dst, const void *h_src, size_t bytes, void *hip_stream);
+/* h_dst[0, bytes) = d_src[0, bytes): the kernel writes the pinned host block
+ * (hipHostMalloc'd, coherent; both pointers 16-B aligned) over the bus,
+ * asynchronous on `hip_stream` (the pass's result copies). */
+int psn_t2d_download_device(void *h_dst, const void *d_src, size_t bytes, void *hip_stream);
 
 #ifdef __cplusplus
 }

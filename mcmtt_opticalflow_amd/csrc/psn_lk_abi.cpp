@@ -46,9 +46,11 @@ struct psn_lk_ctx {
     // the ingest stream (created at the highest priority: a build gates later
     // LK launches and must not wait behind them for compute-unit slots)
     // Consecutive uploads go round-robin to kCopyStreams copy streams: the cameras
-    // of a frame-set upload in parallel on several DMA engines (one engine moves
-    // a 1080p BGR frame in ~0.3 ms; four in a row were the frame's critical path).
-    static constexpr int kCopyStreams = 4;
+    // of a frame-set upload in parallel on two DMA engines (one engine moves a
+    // 1080p BGR frame in ~0.3 ms). Two, not four: after a device sync the first
+    // upload on each further copy stream held the host ~7 ms (round-4 A/B over
+    // 4/2/1/0 copy streams, tools/gpu_envab.sh: 2 had the best segment median).
+    static constexpr int kCopyStreams = 2;
     hipStream_t copy_streams[kCopyStreams] = {};
     hipStream_t copy_stream = nullptr;  // copy_streams[0]
     int copy_rr = 0;

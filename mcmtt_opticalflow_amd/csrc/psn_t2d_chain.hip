@@ -197,8 +197,8 @@ __global__ __launch_bounds__(128) void chain_begin_kernel(psn_t2d_chain_dev C, i
     }
 }
 
-// Pinned host block -> HBM: 16-B loads over the bus, grid-strided.
-__global__ __launch_bounds__(256) void upload_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src, size_t n16,
+// HBM <-> a mapped pinned host block: 16-B accesses over the bus, grid-strided.
+__global__ __launch_bounds__(256) void copy_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src, size_t n16,
                                                      uint8_t *__restrict__ dtail, const uint8_t *__restrict__ stail,
                                                      int ntail) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -209,17 +209,34 @@ __global__ __launch_bounds__(256) void upload_kernel(uint4 *__restrict__ dst, co
 }  // namespace
 }  // namespace psn
 
-extern "C" int psn_t2d_upload_device(void *d_dst, const void *h_src, size_t bytes, void *stream) {
-    if (bytes == 0) return PSN_LK_OK;
-    if (!d_dst || !h_src || ((uintptr_t)d_dst & 15) || ((uintptr_t)h_src & 15)) return PSN_LK_ERR_ARG;
-    void *src = nullptr;  // the block's device address (hipHostMalloc'd memory is mapped)
-    if (hipHostGetDevicePointer(&src, const_cast<void *>(h_src), 0) != hipSuccess || !src) return PSN_LK_ERR_ARG;
+// One copy kernel between HBM and a mapped pinned host block (either side).
+static int copy_mapped(void *dst, const void *src, size_t bytes, hipStream_t stream) {
     const size_t n16 = bytes / 16;
     const int ntail = (int)(bytes % 16);
     const int grid = (int)std::max<size_t>(1, std::min<size_t>((n16 + 255) / 256, 512));
-    hipLaunchKernelGGL(psn::upload_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint4 *)d_dst,
-                       (const uint4 *)src, n16, (uint8_t *)d_dst + n16 * 16, (const uint8_t *)src + n16 * 16, ntail);
+    hipLaunchKernelGGL(psn::copy_kernel, dim3(grid), dim3(256), 0, stream, (uint4 *)dst, (const uint4 *)src, n16,
+                       (uint8_t *)dst + n16 * 16, (const uint8_t *)src + n16 * 16, ntail);
     return hipGetLastError() == hipSuccess ? PSN_LK_OK : PSN_LK_ERR_HIP;
+}
+
+// The device address of a pinned host block (hipHostMalloc'd memory is mapped).
+static void *mapped(const void *h) {
+    void *p = nullptr;
+    return hipHostGetDevicePointer(&p, const_cast<void *>(h), 0) == hipSuccess ? p : nullptr;
+}
+
+extern "C" int psn_t2d_upload_device(void *d_dst, const void *h_src, size_t bytes, void *stream) {
+    if (bytes == 0) return PSN_LK_OK;
+    if (!d_dst || !h_src || ((uintptr_t)d_dst & 15) || ((uintptr_t)h_src & 15)) return PSN_LK_ERR_ARG;
+    const void *src = mapped(h_src);
+    return src ? copy_mapped(d_dst, src, bytes, (hipStream_t)stream) : PSN_LK_ERR_ARG;
+}
+
+extern "C" int psn_t2d_download_device(void *h_dst, const void *d_src, size_t bytes, void *stream) {
+    if (bytes == 0) return PSN_LK_OK;
+    if (!h_dst || !d_src || ((uintptr_t)h_dst & 15) || ((uintptr_t)d_src & 15)) return PSN_LK_ERR_ARG;
+    void *dst = mapped(h_dst);
+    return dst ? copy_mapped(dst, d_src, bytes, (hipStream_t)stream) : PSN_LK_ERR_ARG;
 }
 
 extern "C" int psn_t2d_gate_counts_device(int *d_cnt, int n, int min_count, const int *d_last_step, void *stream) {

@@ -401,7 +401,7 @@ int Tracker2DFlow::EnsureChains(size_t nchains) {
     const size_t cap = PSN_T2D_CHAIN_CAP, S = PSN_T2D_CHAIN_STEPS, npt = K * cap;
     bool ok = true;
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
-    auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
+    auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocCoherent) == hipSuccess; };
     b.layout_in(K, cap);
     for (DeviceBuffers::Scratch &x : b.sc) {
         dm((void **)&x.d_inblk, b.in_bytes);
@@ -450,7 +450,7 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
     const size_t F = grow_cap(nfwd_pts, 1024), J = grow_cap(nfwd_jobs, 16);
     bool ok = true;
     auto dm = [&](void **p, size_t bytes) { ok = ok && hipMalloc(p, bytes) == hipSuccess; };
-    auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess; };
+    auto hm = [&](void **p, size_t bytes) { ok = ok && hipHostMalloc(p, bytes, hipHostMallocCoherent) == hipSuccess; };
     b.fi_off_pts = (J * 4 + 255) & ~(size_t)255;
     b.fo_off_pts = (F + 255) & ~(size_t)255;
     dm((void **)&b.d_fiblk, b.fi_off_pts + F * 8);
@@ -624,8 +624,9 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
             }
             chk(hipEventRecord((hipEvent_t)ev_gf_, st), "gridfast event");
             gf_rec_ = !rc;
-            chk(hipMemcpyAsync(b.h_rawcnt, db.d_cnt, K * 4, hipMemcpyDeviceToHost, st), "feature counts");
-            chk(hipMemcpyAsync(b.h_in, db.d_in, K * cap * 8, hipMemcpyDeviceToHost, st), "features");
+            if (!rc && ((rc = psn_t2d_download_device(b.h_rawcnt, db.d_cnt, K * 4, st)) ||
+                        (rc = psn_t2d_download_device(b.h_in, db.d_in, K * cap * 8, st))))
+                err_ = "features download";
             // boxes and last steps (GridFAST wrote the counts and points on the device)
             if (!rc && (rc = psn_t2d_upload_device(db.d_inblk, b.h_inblk, dall.in_off_cnt, st)))
                 err_ = "chain boxes upload";
@@ -893,16 +894,16 @@ int Tracker2DFlow::PassCopy(std::vector<PassCam> &pc) {
                 fs = (hipStream_t)FwdStream(pc.empty() ? fwd_par_ : pc[0].fwd_par);
     const int rb = pc.empty() ? -1 : pc[0].rb;
     if (K && bp && rb >= 0)
-        chk(hipMemcpyAsync(bp->h_res[rb], bp->d_res[rb], bp->res_sets_off + K * S * cap * 8, hipMemcpyDeviceToHost, st),
-            "chain results");
+        if (!rc && (rc = psn_t2d_download_device(bp->h_res[rb], bp->d_res[rb], bp->res_sets_off + K * S * cap * 8, st)))
+            err_ = "chain results download";
     if (!pc.empty() && pc[0].fwd_rb >= 0) F = pc[0].fwd_n;  // the forward launch from the previous frame's chains
     if (F && bp) {
         // status and points in one copy, on the chain stream after the forward
         // launch (the forward stream goes on with the next frame's launch)
         const int par = pc[0].fwd_par;
         chk(hipStreamWaitEvent(st, (hipEvent_t)ev_fend_[par], 0), "forward end wait");
-        chk(hipMemcpyAsync(bp->h_foblk, bp->d_foblk[par], bp->fo_off_pts + F * 8, hipMemcpyDeviceToHost, st),
-            "forward results");
+        if (!rc && (rc = psn_t2d_download_device(bp->h_foblk, bp->d_foblk[par], bp->fo_off_pts + F * 8, st)))
+            err_ = "forward results download";
         chk(hipEventRecord((hipEvent_t)ev_fcopied_[par], st), "forward copied event");
     }
     // everything the pass enqueued precedes these records (the forward work of
