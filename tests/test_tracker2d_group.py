@@ -288,3 +288,47 @@ def test_group_large_boxes_match_oracle(oracle_mod, gridfast):
                 _check_result(g_res, r_res, what)
                 n_obj += len(g_res["objects"])
     assert n_obj >= 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("coherent", [True, False])
+@pytest.mark.parametrize("nbytes", [0, 5, 16, 1000, 4096 + 7, 300003])
+def test_pass_copy_kernels(nbytes, coherent):
+    """psn_t2d_upload_device / psn_t2d_download_device (the Tracker2D pass's
+    input and result copies): byte-exact both ways through a pinned block, the
+    16-B body and the byte tail, rejected when misaligned."""
+    import ctypes
+
+    import hiprt
+    from mcmtt_opticalflow_amd import _lib
+
+    L = _lib.load()
+    vp = ctypes.c_void_p
+    for f in (L.psn_t2d_upload_device, L.psn_t2d_download_device):
+        f.argtypes = [vp, vp, ctypes.c_size_t, vp]
+    H = hiprt.hip()
+    H.hipHostMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t, ctypes.c_uint]
+    H.hipHostFree.argtypes = [vp]
+    flags = 0x40000000 if coherent else 0  # hipHostMallocCoherent / hipHostMallocDefault
+    hin, hout = vp(), vp()
+    assert H.hipHostMalloc(ctypes.byref(hin), max(nbytes, 16) + 16, flags) == 0
+    assert H.hipHostMalloc(ctypes.byref(hout), max(nbytes, 16) + 16, flags) == 0
+    try:
+        rng = np.random.default_rng(nbytes)
+        src = rng.integers(0, 256, nbytes, dtype=np.uint8)
+        ctypes.memmove(hin.value, src.ctypes.data, nbytes)
+        ctypes.memset(hout.value, 0xA5, max(nbytes, 16) + 16)
+        dev = hiprt.DeviceBuffer(max(nbytes, 16) + 16)
+        assert L.psn_t2d_upload_device(dev.addr, hin.value, nbytes, None) == 0
+        assert L.psn_t2d_download_device(hout.value, dev.addr, nbytes, None) == 0
+        assert H.hipDeviceSynchronize() == 0
+        got = np.ctypeslib.as_array((ctypes.c_uint8 * (max(nbytes, 16) + 16)).from_address(hout.value)).copy()
+        assert np.array_equal(got[:nbytes], src)
+        assert np.all(got[nbytes:] == 0xA5)  # nothing written past the block
+        if nbytes:
+            assert L.psn_t2d_upload_device(dev.addr + 4, hin.value, nbytes, None) != 0
+            assert L.psn_t2d_download_device(hout.value + 8, dev.addr, nbytes, None) != 0
+        dev.free()
+    finally:
+        H.hipHostFree(hin)
+        H.hipHostFree(hout)
