@@ -388,10 +388,14 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         c0 = time.perf_counter()
         group.launch(t, dets, gridfast=gridfast, seed=t)  # after complete_next(t-1): a confirmation
         c1 = time.perf_counter()
-        for k, fd in enumerate(feeds):  # frame t+ahead uploads (and builds) while frame t runs
-            fd.push(group, k, t + ahead)
+        if not args.push_last:
+            for k, fd in enumerate(feeds):  # frame t+ahead uploads (and builds) while frame t runs
+                fd.push(group, k, t + ahead)
         c2 = time.perf_counter()
         group.complete_next(t + 1, next_dets, gridfast=gridfast, seed=t + 1, raw=True)
+        if args.push_last:  # frame t+1's work is on the GPU before the uploads are issued
+            for k, fd in enumerate(feeds):
+                fd.push(group, k, t + ahead)
         if parts is not None:
             parts.append((t, round(1e3 * (c1 - c0), 3), round(1e3 * (c2 - c1), 3),
                           round(1e3 * (time.perf_counter() - c2), 3), group.debug_host_times()))
@@ -1202,6 +1206,8 @@ def parse_args(argv=None):
     ap.add_argument("--measure-steps", type=int, default=20,
                     help="frames after the timed region with per-launch HIP-event timing (roofline)")
     ap.add_argument("--diag-sync-at", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--push-last", action="store_true",
+                    help="tracker mode: push frame t+ahead after complete_next(t+1) instead of before it")
     ap.add_argument("--step-profile", action="store_true", help="tracker mode: host ms of each slow step to stderr")
     ap.add_argument("--no-isolated", dest="isolated", action="store_false",
                     help="skip the isolated-launch timing of the frame-set's LK launches (roofline.isolated)")
