@@ -383,6 +383,20 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     ahead = args.stage_ahead
 
     parts = [] if args.step_profile else None  # (launch, pushes, complete_next) host ms per step
+    # N > 1: frame t's exchange is enqueued at step t and its gathered slots are
+    # consumed (the Associator3D hand-off) at step t+1, while frame t+1 runs
+    pending = []
+
+    def consume(g):
+        if recorded is not None:
+            recorded.append(np.array(g, copy=True).reshape(-1))
+        return g
+
+    def drain():
+        g = None
+        while pending:
+            g = consume(exch.wait(pending.pop(0)))
+        return g
 
     def step(t, dets, next_dets):
         c0 = time.perf_counter()
@@ -403,10 +417,10 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
             rc = T.psn_t2d_pack_result(ctypes.byref(group.result_struct(k)), send[k].ctypes.data, slot_bytes)
             if rc:
                 raise t2d.T2dError(rc, "psn_t2d_pack_result")
-        g = exch.allgather(send) if exch else send
-        if recorded is not None:
-            recorded.append(np.array(g, copy=True).reshape(-1))
-        return g
+        if not exch:
+            return consume(send)
+        pending.append(exch.start(send))
+        return consume(exch.wait(pending.pop(0))) if len(pending) > 1 else None
 
     def all_dets(t):
         return [fd.detections(t2d, t) for fd in feeds]
@@ -425,6 +439,7 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         step(t, seq[i], seq[i + 1])
         wticks.append(time.perf_counter())
         t += 1
+    drain()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -436,6 +451,8 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         t += 1
         if i == args.diag_sync_at:  # diagnostic runs only: a device sync inside the timed region
             torch.cuda.synchronize()
+    g_last = drain()  # the last timed frame's hand-off
+    gathered = g_last if g_last is not None else gathered
     torch.cuda.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
@@ -456,6 +473,8 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
             j = warmup + steps + i
             gathered = step(t, seq[j], seq[j + 1])
             t += 1
+        g_last = drain()
+        gathered = g_last if g_last is not None else gathered
         torch.cuda.synchronize()
         per_kernel, ts = launches.read()
         samples = sampler.read()
@@ -874,7 +893,8 @@ def tracker_main(args):
 
 def tracker_legs(args, profile):
     """Extra single-GPU lines of the default run: configs[3] on one GPU (8 cameras
-    x 2048 points, the strong-scaling run's N=1), the GridFAST Run, configs[4]."""
+    x 2048 points, the strong-scaling run's N=1), the GridFAST Run, PETS-like mixed
+    boxes, the realistic Run (GridFAST + PETS boxes), configs[4]."""
     legs = {}
     a3 = argparse.Namespace(**{**vars(args), "total_cameras": 8, "points": 2048, "boxes": 32, "verify": False,
                                "isolated": False})
@@ -892,6 +912,14 @@ def tracker_legs(args, profile):
     lm = tracker_line(am, rm, 1, args.cameras, "weak", None)
     legs["mixed_boxes"] = {k: lm[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["mixed_boxes"]["lk_launches"] = {k: lm["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
+    # the reference Run's real per-frame work together (PSNWhere_Tracker2D.cpp:735-757, 776-782,
+    # 871-877): GridFAST per detection feeding PETS-sized box windows
+    ar = argparse.Namespace(**{**vars(args), "features": "gridfast", "box_dist": "pets", "verify": False,
+                               "isolated": False})
+    rr = tracker_run(ar, steps=args.leg_steps, warmup=3)
+    lr = tracker_line(ar, rr, 1, args.cameras, "weak", None)
+    legs["realistic"] = {k: lr[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
+    legs["realistic"]["lk_launches"] = {k: lr["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
     legs["config4"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3)["line"]
     legs["config4_frames_in_hbm"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3,
                                                 ingest="hbm")["line"]

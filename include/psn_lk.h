@@ -52,11 +52,16 @@ extern "C" {
 
 #define PSN_LK_MAX_LEVELS 8
 /* Window limits: widths up to PSN_LK_MAX_WIN_WIDTH (one window row band of the
- * large-window kernel in LDS), areas below 2^24 pixels (h * ceil(w/4) < 2^22
- * quads). Tracker2D passes box.w x box.h (PSNWhere_Tracker2D.cpp:871-877) and
- * box.w x box.w (:776-782) uncapped; every box inside a frame up to 6400 px wide
- * and 2^24 px in area (4K: 8.3 Mpx) is covered. */
+ * large-window kernel in LDS) and h * ceil(w/4) < 2^22 quads (about 2^24 px);
+ * psn_lk_window_supported() is the whole predicate, what psn_lk_track checks
+ * after winSize > 2 (else PSN_LK_ERR_UNSUPPORTED). Tracker2D passes box.w x box.h
+ * (PSNWhere_Tracker2D.cpp:871-877) and box.w x box.w (:776-782) uncapped: a
+ * forward window of a box inside a frame of < 2^24 px is always supported, but a
+ * backward box.w x box.w window is not when box.w > 4096 (4097^2 > 2^24): the
+ * Tracker2D host checks the same predicate per chain / forward call and flags
+ * such a box instead of failing the frame. */
 #define PSN_LK_MAX_WIN_WIDTH 6400
+#define PSN_LK_MAX_WIN_QUADS (1L << 22)
 
 /* Arguments of cv::calcOpticalFlowPyrLK after prevImg/nextImg/points. The
  * reference passes only winSize and leaves the rest at their defaults
@@ -90,6 +95,12 @@ void psn_lk_default_params(psn_lk_params *p);
 /* Effective maxLevel of buildOpticalFlowPyramid for an image/window (the
  * level-count truncation rule). Returns < 0 on bad arguments. */
 int psn_lk_effective_max_level(int width, int height, int win_w, int win_h, int max_level);
+
+/* 1 when an LK window of w x h px is within the window limits above
+ * (w <= PSN_LK_MAX_WIN_WIDTH and h * ceil(w/4) < PSN_LK_MAX_WIN_QUADS), else 0:
+ * the predicate psn_lk_track applies after winSize > 2, and the one the
+ * Tracker2D host applies to each chain's box.w x box.w and each forward box. */
+int psn_lk_window_supported(int w, int h);
 
 /* Per-camera context (replaces CPSNWhere_Tracker2D::Initialize's ring setup,
  * PSNWhere_Tracker2D.cpp:129-139): a device ring of `ring_slots` pyramids of

@@ -114,6 +114,7 @@ struct psn_lk_ctx {
         hipStream_t s = nullptr;
         void *p = nullptr;
         size_t bytes = 0;
+        hipEvent_t done = nullptr;  // recorded on s after each launch that used a slot buffer of s
     };
     std::vector<LgWs> lg_ws;
     std::vector<void *> lg_retired;  // outgrown slot buffers, freed at destroy (hipFree would wait for the device)
@@ -187,6 +188,10 @@ void psn_lk_default_params(psn_lk_params *p) {
     p->min_eig_threshold = 1e-4;
 }
 
+int psn_lk_window_supported(int w, int h) {
+    return w > 0 && h > 0 && w <= PSN_LK_MAX_WIN_WIDTH && (long long)h * ((w + 3) / 4) < (long long)PSN_LK_MAX_WIN_QUADS;
+}
+
 int psn_lk_effective_max_level(int width, int height, int win_w, int win_h, int max_level) {
     if (width <= 0 || height <= 0 || max_level < 0) return PSN_LK_ERR_ARG;
     int sw = width, sh = height;
@@ -202,6 +207,10 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     if (!out || width <= 0 || height <= 0 || ring_slots <= 0 || max_level_cap < 0 ||
         max_level_cap > psn::kPyrMaxTop)
         return PSN_LK_ERR_ARG;
+    // the pyramid tiles' LDS plan (guarded at build time for every top level:
+    // psn::pyr_tiles_fit; kept here so a context never launches past the CU's LDS)
+    if (psn::kStScratchBytes + psn::pyr_lds_bytes(max_level_cap, psn::pyr_tile_edge(max_level_cap)) > psn::kMaxLdsBytes)
+        return PSN_LK_ERR_UNSUPPORTED;
     *out = nullptr;
     psn_lk_ctx *c = new (std::nothrow) psn_lk_ctx();
     if (!c) return PSN_LK_ERR_NOMEM;
@@ -313,10 +322,16 @@ void psn_lk_destroy(psn_lk_ctx *c) {
     for (uint8_t *p : c->d_stage)
         if (p) (void)hipFree(p);
     if (c->jpeg) psn_jpeg_destroy(c->jpeg);
-    // (a caller's stream in lg_ws may be gone by now: wait for the whole device)
-    if (!c->lg_ws.empty()) (void)hipDeviceSynchronize();
+    // the last launch that used each stream's slot buffers (the current and the
+    // retired ones: the stream runs in order) -- not the whole device, which
+    // other contexts and groups share (a caller's stream may be gone by now, its
+    // recorded event stays valid)
     for (auto &ws : c->lg_ws)
+        if (ws.done) (void)hipEventSynchronize(ws.done);
+    for (auto &ws : c->lg_ws) {
         if (ws.p) (void)hipFree(ws.p);
+        if (ws.done) (void)hipEventDestroy(ws.done);
+    }
     c->lg_ws.clear();
     for (void *p : c->lg_retired) (void)hipFree(p);
     c->lg_retired.clear();
@@ -537,10 +552,8 @@ static int wait_prev_build(psn_lk_ctx *c, int slot, hipStream_t s) {
 }
 
 // Top-level tile of a standalone pyramid build (the level-0 region of a tile is
-// 2^top * T + 3 * (2^top - 1) px square: larger tiles re-read less halo).
-#ifndef PSN_PYR_TILE
-#define PSN_PYR_TILE 8
-#endif
+// 2^top * T + 3 * (2^top - 1) px square: larger tiles re-read less halo;
+// psn::pyr_tile_edge, guarded against the LDS at build time).
 // Pyramid-build arguments of `slot` from a device source frame.
 static psn::PyrBuildArgs build_args(const psn_lk_ctx *c, int slot, const uint8_t *dev, int stride, int channels) {
     psn::PyrBuildArgs a{};
@@ -548,7 +561,7 @@ static psn::PyrBuildArgs build_args(const psn_lk_ctx *c, int slot, const uint8_t
     a.src_stride = stride;
     a.channels = channels;
     a.nlevels = c->nlevels;
-    a.tile = (c->nlevels - 1) <= 4 ? PSN_PYR_TILE : 4;
+    a.tile = psn::pyr_tile_edge(c->nlevels - 1);
     for (int l = 0; l < c->nlevels; l++) a.lv[l] = c->h_slots[(size_t)slot * psn::kMaxLevels + l];
     return a;
 }
@@ -744,7 +757,7 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
         return set_err(c, PSN_LK_ERR_SLOT, "slot never filled (%d, %d)", q.prev_slot, q.next_slot);
     if (p.win_w <= 2 || p.win_h <= 2) return set_err(c, PSN_LK_ERR_WINSIZE, "winSize %dx%d <= 2", p.win_w, p.win_h);
     if (p.max_level < 0 || q.num_pts < 0 || q.first_pt < 0) return set_err(c, PSN_LK_ERR_ARG, "bad query");
-    if (p.win_w > PSN_LK_MAX_WIN_WIDTH || (long long)p.win_h * ((p.win_w + 3) / 4) >= (1LL << 22))
+    if (!psn_lk_window_supported(p.win_w, p.win_h))
         return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d wider than %d px or above 2^24 px", p.win_w, p.win_h,
                        PSN_LK_MAX_WIN_WIDTH);
     const int ml = psn_lk_effective_max_level(c->width, c->height, p.win_w, p.win_h, p.max_level);
@@ -822,6 +835,9 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
         pq.cls = kClsLg;
     }
     if (pq.cls == kClsLg) {
+        // (the kernel's LDS plan within the CU's: never an invalid launch)
+        if (psn::lg_lds_bytes(w, h, pq.lg_tr, pq.lg_jr, pq.lg_tq) > psn::kMaxLdsBytes)
+            return set_err(c, PSN_LK_ERR_UNSUPPORTED, "window %dx%d: large-window LDS plan above 160 KB", w, h);
         pq.key = pq.lg_tq;  // one launch per tile size
         d.tile_rows = pq.lg_tr;
         d.lg_jr = pq.lg_jr ? 1 : 0;
@@ -860,6 +876,20 @@ static int ensure_lg_ws(psn_lk_ctx *c, size_t bytes, void **out) {
 // HBM budget of one stream's large-window slots: one slot per point up to it,
 // beyond it the grid strides (a slot per resident workgroup at the least)
 static constexpr size_t kLgWsBudget = 512ull << 20;
+
+// The launch just enqueued on c->stream built `slot` (a fused build): readers on
+// other streams wait for that launch alone -- the event is recorded right after
+// it, not after the call's later launches of other classes.
+static int mark_fused_build(psn_lk_ctx *c, int slot) {
+    HIPCHK(c, hipEventRecord(c->slot_ready[slot], c->stream));
+    c->ready_rec[slot] = 1;
+    c->build_gen[slot]++;
+    bool mine = false;  // this stream built it: ordered after the build
+    for (auto &w : c->waited[slot])
+        if (w.first == c->stream) w.second = c->build_gen[slot], mine = true;
+    if (!mine) c->waited[slot].emplace_back(c->stream, c->build_gen[slot]);
+    return PSN_LK_OK;
+}
 
 // One launch of a planned group (queries of one class, <= kMaxQueries).
 static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls, int key, const float *d_prev,
@@ -910,6 +940,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
             // the 168-VGPR variant (three per CU; one-camera launches fit at two)
             if (oept == 2 && E <= 8 && lds_ow <= 53 * 1024 && wgs > 2 * c->num_cus) threads += 200000;
         }
+        bool builds = false;
         if (c->pend && fused_slot < 0 && !d_counts) {  // fuse the deferred build into this launch's tail
             int tx, ty, plds;
             psn::pyramid_grid(c->pend_args, tx, ty, plds);
@@ -926,9 +957,10 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
             lds = std::max(lds, psn::kStScratchBytes + plds);
             c->pend = false;
             fused_slot = c->pend_slot;
+            builds = true;
         }
         HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, true, c->stream));
-        return PSN_LK_OK;
+        return builds ? mark_fused_build(c, fused_slot) : PSN_LK_OK;
     }
     if (cls == kClsBx) {
         const int upt = key / 10;
@@ -962,7 +994,9 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
         lds = std::max(lds, psn::lg_lds_bytes(a.q[i].win_w, a.q[i].win_h, a.q[i].tile_rows, a.q[i].lg_jr != 0, key));
     }
     const size_t slot_bytes = (size_t)slot * 8;
-    const long long fit = std::max<long long>((long long)(kLgWsBudget / slot_bytes), 64);
+    // (within the budget also for the largest windows: one slot of a 2^24-px window
+    // is ~100 MB, so no floor on the slot count past what the budget holds)
+    const long long fit = std::max<long long>((long long)(kLgWsBudget / slot_bytes), 1);
     const int grid = (int)std::min<long long>(wgs, fit);
     void *ws = nullptr;
     int rc = ensure_lg_ws(c, slot_bytes * grid, &ws);
@@ -972,6 +1006,11 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
     a.lk_wgs = wgs;
     a.total_wgs = wgs;
     HIPCHK(c, psn::launch_lk_lg(a, grid, lds, key, c->stream));
+    for (auto &e : c->lg_ws)
+        if (e.s == c->stream) {
+            if (!e.done) HIPCHK(c, hipEventCreateWithFlags(&e.done, hipEventDisableTiming));
+            HIPCHK(c, hipEventRecord(e.done, c->stream));
+        }
     return PSN_LK_OK;
 }
 
@@ -1056,15 +1095,6 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
     if (timed && !groups.empty()) {
         const size_t dom = (size_t)(std::max_element(group_px.begin(), group_px.end()) - group_px.begin());
         c->track_tag[(size_t)ti] = kernel_tag(groups[dom].first, groups[dom].second) + (groups.size() > 1 ? 1000 : 0);
-    }
-    if (fused_slot >= 0) {  // readers on other streams wait for the launch that built it
-        HIPCHK(c, hipEventRecord(c->slot_ready[fused_slot], c->stream));
-        c->ready_rec[fused_slot] = 1;
-        c->build_gen[fused_slot]++;
-        bool mine = false;  // this stream built it: ordered after the build
-        for (auto &w : c->waited[fused_slot])
-            if (w.first == c->stream) w.second = c->build_gen[fused_slot], mine = true;
-        if (!mine) c->waited[fused_slot].emplace_back(c->stream, c->build_gen[fused_slot]);
     }
     if (c->pend) {  // no launch took it (no single-tile launch)
         int rc = flush_pending(c);

@@ -101,7 +101,7 @@ struct LkLaunchArgs {
 };
 
 // LDS bytes a query needs for a given tile height (shared by host planner and kernel).
-__host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
+__host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 __host__ __device__ inline int lk_jreg_w(int w) { return w + 1 + 2 * kJMargin; }
 __host__ __device__ inline int lk_jreg_h(int h) { return h + 1 + 2 * kJMargin; }
 __host__ __device__ inline int lk_off_dw(int w, int h) { return align16(2 * w * h); }
@@ -274,7 +274,7 @@ constexpr int kLgTQNoJr = 128;
 constexpr int kLgTQE = 128;  // quads per err fallback tile (one row-major chain)
 __host__ __device__ constexpr int lg_sreg(int tq) { return ((tq + 15) & ~15) + 4; }  // SSE chain region (floats)
 __host__ __device__ constexpr int lg_plane(int tq) { return 4 * lg_sreg(tq) + ((4 * tq + 15) & ~15) + 4; }
-__host__ __device__ inline int lg_scr_bytes() { return align16((kBxXInts + 32) * 4); }
+__host__ __device__ constexpr int lg_scr_bytes() { return align16((kBxXInts + 32) * 4); }
 __host__ __device__ constexpr int lg_tiles_a_bytes(int tq) { return 2 * 3 * lg_plane(tq) * 4 + 1024; }
 // + slack: the chain sums read up to 5 blocks past a chain (discarded)
 __host__ __device__ constexpr int lg_tiles_b_bytes(int tq) { return 2 * 2 * lg_plane(tq) * 4 + 1024; }
@@ -295,6 +295,51 @@ constexpr int kLgJrMaxLds = PSN_LG_JR_MAX_KB * 1024;  // J region in LDS while t
 __host__ __device__ inline int lg_quads_per_thread(int w, int h) { return (h * ((w + 3) >> 2) + kLgNT - 1) / kLgNT; }
 // window-value slot of one workgroup, in 8-byte units
 __host__ __device__ inline long long lg_slot_int2(int w, int h) { return 3LL * kLgNT * lg_quads_per_thread(w, h); }
+
+// ---- pyramid tiles (pyramid_kernel, and the builds fused into lk_kernel_st) ----
+// Region of level l (l < top) that a top-level tile needs, per axis:
+// start = 2^(top-l)*t0 - 2*(2^(top-l)-1), size = 2^(top-l)*T + 3*(2^(top-l)-1).
+__host__ __device__ constexpr int pyr_region_n(int top, int l, int T) {
+    return (1 << (top - l)) * T + 3 * ((1 << (top - l)) - 1);
+}
+// Level-0 region rows in LDS: the region starts at an aligned-down column
+// (offset 0..3) so interior rows move as dwords.
+__host__ __device__ constexpr int pyr_s0(int n0) { return (n0 + 3 + 3) & ~3; }
+__host__ __device__ constexpr int pyr_lds_off(int top, int l, int T) {
+    int off = 0;
+    for (int m = 0; m < l; m++) {
+        const int n = pyr_region_n(top, m, T);
+        off += align16(m == 0 ? pyr_s0(n) * n : n * n);
+    }
+    return off;
+}
+__host__ __device__ constexpr int pyr_lds_bytes(int top, int T) {
+    return top == 0 ? 0 : pyr_lds_off(top, top, T) + align16(2 * pyr_region_n(top, 0, T) * pyr_region_n(top, 1, T));
+}
+// Top-level tile edge of a build (a build parameter, PSN_PYR_TILE; tops past 4
+// take 4)
+#ifndef PSN_PYR_TILE
+#define PSN_PYR_TILE 8
+#endif
+constexpr int kPyrTile = PSN_PYR_TILE;
+constexpr int kPyrTileDeep = 4;
+__host__ __device__ constexpr int pyr_tile_edge(int top) { return top <= 4 ? kPyrTile : kPyrTileDeep; }
+// Build-time guards (a bad build parameter fails the compile instead of a launch
+// with hipErrorInvalidValue): every top level a context may build, standalone and
+// fused behind the single-tile kernel's scratch, fits the CU's LDS.
+constexpr int kMaxLdsBytes = 160 * 1024;
+__host__ __device__ constexpr bool pyr_tiles_fit(int top) {
+    return top > kPyrMaxTop || (kStScratchBytes + pyr_lds_bytes(top, pyr_tile_edge(top)) <= kMaxLdsBytes &&
+                                pyr_tiles_fit(top + 1));
+}
+static_assert(kPyrTile >= 1 && pyr_tiles_fit(1), "PSN_PYR_TILE: a pyramid tile's LDS plan exceeds 160 KB");
+// The large-window kernel's LDS plan: its A tiles of every tile size beside the
+// records, and the J-region cap
+static_assert(lg_scr_bytes() + lg_tiles_a_bytes(kLgTQs[0]) <= kMaxLdsBytes &&
+                  lg_scr_bytes() + lg_tiles_a_bytes(kLgTQs[1]) <= kMaxLdsBytes,
+              "kLgTQs: a large-window tile plan exceeds 160 KB");
+static_assert(kLgJrMaxLds > 0 && kLgJrMaxLds <= kMaxLdsBytes, "PSN_LG_JR_MAX_KB exceeds 160 KB");
+static_assert(kBxMaxLds <= kMaxLdsBytes && kBxLdsTarget <= kBxMaxLds, "box-kernel LDS caps exceed 160 KB");
 
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel
 constexpr int kStMaxLds = 150 * 1024;

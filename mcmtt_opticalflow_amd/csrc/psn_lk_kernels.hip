@@ -57,28 +57,7 @@ namespace psn {
 // Pyramid
 // ---------------------------------------------------------------------------
 
-// Region of level l (l < top) that a top-level tile needs, per axis:
-// start = 2^(top-l)*t0 - 2*(2^(top-l)-1), size = 2^(top-l)*T + 3*(2^(top-l)-1).
-__host__ __device__ inline int pyr_region_n(int top, int l, int T) {
-    int sp = 1 << (top - l);
-    return sp * T + 3 * (sp - 1);
-}
-// Level-0 region rows in LDS: the region starts at an aligned-down column
-// (offset 0..3) so interior rows move as dwords.
-__host__ __device__ inline int pyr_s0(int n0) { return (n0 + 3 + 3) & ~3; }
-__host__ __device__ inline int pyr_lds_off(int top, int l, int T) {
-    int off = 0;
-    for (int m = 0; m < l; m++) {
-        int n = pyr_region_n(top, m, T);
-        off += align16(m == 0 ? pyr_s0(n) * n : n * n);
-    }
-    return off;
-}
-__host__ __device__ inline int pyr_lds_bytes(int top, int T) {
-    if (top == 0) return 0;
-    int n0 = pyr_region_n(top, 0, T), n1 = pyr_region_n(top, 1, T);
-    return pyr_lds_off(top, top, T) + align16(2 * n0 * n1);
-}
+// (the LDS plan of a tile, pyr_lds_bytes, and its build-time guards: psn_lk_kernels.h)
 
 __device__ __forceinline__ uint8_t load_src(const PyrBuildArgs &a, int y, int x) {
     const uint8_t *row = a.src + (size_t)y * a.src_stride;

@@ -79,22 +79,37 @@ class ResultExchange:
     all of them in camera order (index == camID, PSNWhere_Associator3D.cpp:
     1105-1116) in host memory.
 
+    Pipelined: start(send) copies the frame's slots into a staging ring entry
+    and enqueues the exchange, returning a ticket at once; wait(ticket) blocks
+    only when the gathered slots are consumed (the bench consumes frame t's at
+    step t+1, while frame t+1 runs on the GPU), so the exchange is off the host's
+    critical path between one frame's completion and the next frame's launch.
+    The reference hands the vector over in-process and Associator3D runs right
+    after (PSNWhere.cpp:257-269); here it runs one frame behind Tracker2D. Up to
+    `depth` exchanges may be in flight; tickets are waited in start order.
+
     backend "psn_comm": the library's RCCL communicator (psn_comm_init /
     psn_comm_allgather over xGMI; the unique id travels over the
-    torch.distributed control group), pinned host -> device -> all-gather ->
-    pinned host on one HIP stream. backend "torch": the same exchange with
-    torch.distributed on CPU tensors (gloo), for the CPU tests."""
+    torch.distributed control group): staging pinned host -> device -> all-gather
+    -> pinned host, enqueued on one HIP stream with an event per ticket. backend
+    "torch": the same exchange with torch.distributed on CPU tensors (gloo,
+    async_op), for the CPU tests."""
 
-    def __init__(self, world: int, rank: int, bytes_per_rank: int, device: int = 0, backend: str = "psn_comm"):
+    def __init__(self, world: int, rank: int, bytes_per_rank: int, device: int = 0, backend: str = "psn_comm",
+                 depth: int = 3):
         import ctypes
 
         import torch
         import torch.distributed as dist
 
-        self.world, self.rank, self.nbytes, self.backend = world, rank, bytes_per_rank, backend
+        self.world, self.rank, self.nbytes, self.backend, self.depth = world, rank, bytes_per_rank, backend, depth
         self._comm = None
+        self._next = 0        # ring entry of the next start
+        self._inflight = []   # tickets started, not yet waited (start order)
         if backend == "torch":
-            self._recv = [torch.empty(bytes_per_rank, dtype=torch.uint8) for _ in range(world)]
+            self._send = [torch.empty(bytes_per_rank, dtype=torch.uint8) for _ in range(depth)]
+            self._recv = [torch.empty(world * bytes_per_rank, dtype=torch.uint8) for _ in range(depth)]
+            self._work = [None] * depth
             return
         from . import _lib
 
@@ -112,32 +127,64 @@ class ResultExchange:
         self._comm = comm
         dev = torch.device("cuda", device)
         self._stream = torch.cuda.Stream(dev)
-        self._send = torch.empty(bytes_per_rank, dtype=torch.uint8, device=dev)
-        self._recv_d = torch.empty(world * bytes_per_rank, dtype=torch.uint8, device=dev)
-        self._recv_h = torch.empty(world * bytes_per_rank, dtype=torch.uint8).pin_memory()
+        self._send_h = [torch.empty(bytes_per_rank, dtype=torch.uint8).pin_memory() for _ in range(depth)]
+        self._send = [torch.empty(bytes_per_rank, dtype=torch.uint8, device=dev) for _ in range(depth)]
+        self._recv_d = [torch.empty(world * bytes_per_rank, dtype=torch.uint8, device=dev) for _ in range(depth)]
+        self._recv_h = [torch.empty(world * bytes_per_rank, dtype=torch.uint8).pin_memory() for _ in range(depth)]
+        self._done = [torch.cuda.Event() for _ in range(depth)]
 
-    def allgather(self, send):
-        """send: uint8 numpy array of bytes_per_rank bytes (pinned for an async
-        upload) -> uint8 numpy array [world * bytes_per_rank] in camera order."""
+    def start(self, send) -> int:
+        """Enqueue the exchange of `send` (uint8, bytes_per_rank bytes; copied
+        before return, so the caller may refill it) and return its ticket."""
         import numpy as np
         import torch
         import torch.distributed as dist
 
+        if len(self._inflight) >= self.depth:
+            raise RuntimeError(f"ResultExchange: {self.depth} exchanges in flight; wait for the oldest first")
+        i = self._next
+        self._next = (i + 1) % self.depth
         src = torch.from_numpy(np.ascontiguousarray(send).reshape(-1))
         if self.backend == "torch":
-            dist.all_gather(self._recv, src.clone())
-            return torch.cat(self._recv).numpy()
-        with torch.cuda.stream(self._stream):
-            self._send.copy_(src, non_blocking=True)
-            rc = self._L.psn_comm_allgather(self._comm, self._send.data_ptr(), self._recv_d.data_ptr(), self.nbytes,
-                                            self._stream.cuda_stream)
-            if rc != 0:
-                raise RuntimeError(f"psn_comm_allgather failed ({rc})")
-            self._recv_h.copy_(self._recv_d, non_blocking=True)
-        self._stream.synchronize()
-        return self._recv_h.numpy()
+            self._send[i].copy_(src)
+            self._work[i] = dist.all_gather_into_tensor(self._recv[i], self._send[i], async_op=True)
+        else:
+            self._send_h[i].copy_(src)  # a few KB: the caller's buffer is free again
+            with torch.cuda.stream(self._stream):
+                self._send[i].copy_(self._send_h[i], non_blocking=True)
+                rc = self._L.psn_comm_allgather(self._comm, self._send[i].data_ptr(), self._recv_d[i].data_ptr(),
+                                                self.nbytes, self._stream.cuda_stream)
+                if rc != 0:
+                    raise RuntimeError(f"psn_comm_allgather failed ({rc})")
+                self._recv_h[i].copy_(self._recv_d[i], non_blocking=True)
+                self._done[i].record(self._stream)
+        self._inflight.append(i)
+        return i
+
+    def wait(self, ticket: int):
+        """The gathered slots of `ticket` (the oldest exchange in flight): uint8
+        numpy array [world * bytes_per_rank] in camera order, valid until this
+        ring entry is started again (`depth` starts later)."""
+        if not self._inflight or self._inflight[0] != ticket:
+            raise RuntimeError("ResultExchange.wait: tickets are waited in start order")
+        self._inflight.pop(0)
+        if self.backend == "torch":
+            self._work[ticket].wait()
+            self._work[ticket] = None
+            return self._recv[ticket].numpy()
+        self._done[ticket].synchronize()
+        return self._recv_h[ticket].numpy()
+
+    def pending(self) -> int:
+        return len(self._inflight)
+
+    def allgather(self, send):
+        """Blocking exchange: start + wait (uint8 numpy array [world * bytes_per_rank])."""
+        return self.wait(self.start(send))
 
     def close(self):
+        while self._inflight:
+            self.wait(self._inflight[0])
         if self._comm is not None:
             self._stream.synchronize()
             self._L.psn_comm_destroy(self._comm)

@@ -485,17 +485,18 @@ int Tracker2DFlow::EnsureForward(size_t nfwd_pts, size_t nfwd_jobs) {
 }
 
 // Error of a chain whose square window (box width, :782) the LK cannot run:
-// CV_Assert(winSize > 2) in the reference, or wider than PSN_LK_MAX_WIN_WIDTH.
+// CV_Assert(winSize > 2) in the reference, or outside the LK's window limits
+// (psn_lk_window_supported: the same predicate psn_lk_track applies).
 static int window_error(int win) {
     if (win <= 2) return PSN_LK_ERR_WINSIZE;
-    if (win > PSN_LK_MAX_WIN_WIDTH) return PSN_LK_ERR_UNSUPPORTED;
+    if (!psn_lk_window_supported(win, win)) return PSN_LK_ERR_UNSUPPORTED;
     return PSN_LK_OK;
 }
 
 // The same for a forward call's box window (:877).
 int Tracker2DFlow::forward_window_error(int w, int h) {
     if (w <= 2 || h <= 2) return PSN_LK_ERR_WINSIZE;
-    if (w > PSN_LK_MAX_WIN_WIDTH) return PSN_LK_ERR_UNSUPPORTED;
+    if (!psn_lk_window_supported(w, h)) return PSN_LK_ERR_UNSUPPORTED;
     return PSN_LK_OK;
 }
 

@@ -51,3 +51,16 @@ def test_bad_arguments_return_codes_not_crashes():
     assert L.psn_lk_sync(None) == -1
     assert L.psn_lk_track(None, None, 0, None, None, None, None) == -1
     assert L.psn_comm_init(0, 0, 0, None, ctypes.byref(out)) == -1
+
+
+@pytest.mark.parametrize("w,h,exp", [
+    (3, 3, 1), (6400, 1, 1), (6401, 1, 0), (6400, 2621, 1), (6400, 2622, 0),
+    (4095, 4095, 1), (4096, 4096, 0), (4200, 4200, 0), (4200, 100, 1), (0, 5, 0), (5, 0, 0),
+])
+def test_window_supported_predicate(w, h, exp):
+    """psn_lk_window_supported: width <= 6400 and h * ceil(w/4) < 2^22 quads --
+    the one predicate psn_lk_track and the Tracker2D host both apply (a square
+    backward window box.w x box.w is out past box.w = 4095)."""
+    L = _lib.load()
+    assert L.psn_lk_window_supported(w, h) == exp
+    assert exp == (0 < w <= 6400 and 0 < h and h * ((w + 3) // 4) < (1 << 22))

@@ -207,3 +207,70 @@ def test_tracker_results_exchange_gloo_world2():
                 assert (a["id"], a["box"], a["head"], a["score"]) == (b["id"], b["box"], b["head"], b["score"])
                 np.testing.assert_array_equal(a["prev"], b["prev"])
                 np.testing.assert_array_equal(a["curr"], b["curr"])
+
+
+def _pipelined_worker(rank, world, port, C, F, q):
+    """The bench's pipelined hand-off (ResultExchange.start / wait, gloo): frame
+    t's exchange is started at step t and consumed at step t+1; each rank's send
+    buffer is refilled right after start (the exchange copied it)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mcmtt_opticalflow_amd import dist as pdist
+        from mcmtt_opticalflow_amd import tracker2d as t2d
+
+        slot = t2d.result_slot_bytes(4, 1)
+        ex = pdist.ResultExchange(world, rank, C * slot, backend="torch", depth=2)
+        send = np.zeros((C, slot), np.uint8)
+        got, pending = {}, []
+
+        def consume(t, g):
+            rows = np.asarray(g).reshape(world * C, slot)
+            got[t] = [t2d.unpack_result(rows[cam], 4, 1) for cam in range(world * C)]
+
+        for t in range(F):
+            for k in range(C):
+                cam = rank * C + k
+                objs = [{"id": 100 * cam + t, "box": (float(cam), float(t), 8.0, 16.0), "head": (0.0, 0.0, 0.0, 0.0),
+                         "score": 0.5, "prev": np.full((k + 1, 2), cam + 0.25 * t, np.float32),
+                         "curr": np.full((k + 2, 2), t + 0.5, np.float32)}]
+                t2d.pack_result({"cam_id": cam, "frame_idx": t, "objects": objs, "detection_rects": [],
+                                 "tracker_rects": []}, send[k])
+            pending.append((t, ex.start(send)))
+            send[:] = 0xEE  # the caller's buffer is free again at once
+            if len(pending) > 1:
+                tt, tk = pending.pop(0)
+                consume(tt, ex.wait(tk))
+            with pytest.raises(RuntimeError):
+                ex.wait(pending[0][1] + 1)  # tickets are waited in start order
+        while pending:
+            tt, tk = pending.pop(0)
+            consume(tt, ex.wait(tk))
+        ex.close()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_exchange_gloo_world2():
+    world, C, F = 2, 2, 6
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, C, F, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, got in out:
+        assert sorted(got) == list(range(F))  # every frame consumed, once
+        for t, rows in got.items():
+            for cam, g in enumerate(rows):  # camera order: index == camID
+                assert g["cam_id"] == cam and g["frame_idx"] == t
+                (o,) = g["objects"]
+                assert o["id"] == 100 * cam + t and o["box"] == (float(cam), float(t), 8.0, 16.0)
+                np.testing.assert_array_equal(o["prev"], np.full(((cam % C) + 1, 2), cam + 0.25 * t, np.float32))
+                np.testing.assert_array_equal(o["curr"], np.full(((cam % C) + 2, 2), t + 0.5, np.float32))

@@ -61,3 +61,14 @@ def test_headline_mixed_boxes_matches_oracle(oracle_mod):
     v = _verify("--box-dist", "pets", "--cameras", "2", steps=2, warmup=2)
     assert v["mismatches"] == 0, v["first_mismatch"]
     assert v["objects_checked"] >= 2 * 8 * 3
+
+
+def test_headline_realistic_run_matches_oracle(oracle_mod):
+    """bench.py --features gridfast --box-dist pets (the realistic leg): the
+    reference Run's per-frame work together -- a masked GridFAST detection per
+    detection (PSNWhere_Tracker2D.cpp:735-757) feeding the backward chains with
+    box.w x box.w windows (:776-782) and the forward calls with box.w x box.h
+    windows (:871-877) on PETS-sized boxes (box kernel and large-window kernel)."""
+    v = _verify("--features", "gridfast", "--box-dist", "pets", "--cameras", "2", steps=2, warmup=2)
+    assert v["mismatches"] == 0, v["first_mismatch"]
+    assert v["objects_checked"] >= 2 * 8 * 2

@@ -423,6 +423,20 @@ def test_lk_large_window_4k_5level(oracle_mod):
     assert_same(gpu, ref, "4k 128x320")
 
 
+@pytest.mark.parametrize("win", [(1024, 300), (2048, 200), (212, 300), (4093, 40)])
+def test_lk_large_windows_4k_wide(oracle_mod, win):
+    """Wide windows at 4K near the large-window kernel's plan limits: 1024 and
+    2048 px wide (J from the level: the LDS J region would pass its cap; long
+    quad runs per thread and lg_div over 10^5 quads), 212 x 300 (just past the
+    80 KB cap where the planner turns the LDS J-region copy off), and 4093 px
+    wide (a row band of ~4 KB per I-patch row, quad rows of 1024 + a tail)."""
+    sc, f0, f1 = scene_pair(16, 3840, 2160, 4, box_w=min(win[0], 3000), box_h=win[1])
+    pts = np.concatenate([sc.points_at(0), np.array([[1920, 1080], [5, 2150]], np.float32)])
+    ref = oracle_ref(oracle_mod, f0, f1, pts, win, 4)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 4)
+    assert_same(gpu, ref, f"4k wide {win}")
+
+
 @pytest.mark.parametrize("lg_lds,jr", [(0, 1), (4096, 1), (0, 0)])
 @pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
 def test_lk_large_kernel_all_shapes(oracle_mod, lg_lds, jr, flags):

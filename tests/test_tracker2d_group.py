@@ -208,6 +208,28 @@ def test_group_window_errors():
         assert dets[0].valid == 0 and res["objects"] == []
 
 
+def test_group_unsupported_backward_window():
+    """A detection box wider than 4095 px gives a backward window box.w x box.w of
+    2^24+ px, past the LK's limits (psn_lk_window_supported): with >= 4 features
+    the frame fails with PSN_LK_ERR_UNSUPPORTED at the host's window check, before
+    any launch (the chain is flagged up front, not failed inside the LK pass), and
+    the group runs the next frame normally."""
+    W, H = 4400, 240
+    img = synth.texture(W, H, 5)
+    good = [[t2d.make_detection((40, 20, 60, 150), np.float32([[60, 40], [70, 80], [80, 120], [62, 100]]))]]
+    with t2d.Group(W, H, [0]) as g:
+        g.push_frame(0, img)
+        g.run(0, good)
+        g.push_frame(0, img)
+        wide = t2d.make_detection((20, 20, 4200, 200), np.float32([[100, 40], [900, 80], [2000, 120], [4000, 100]]))
+        with pytest.raises(t2d.T2dError) as e:
+            g.run(1, [[wide]])
+        assert e.value.code == -8  # PSN_LK_ERR_UNSUPPORTED
+        g.push_frame(0, img)
+        (dets, res), = g.run(2, good)
+        assert len(dets) == 1
+
+
 def test_group_failed_frame_after_regrow_matches_oracle(oracle_mod):
     """A frame that grows the chain buffers and then fails (a 2-px-wide detection
     with >= 4 features, CV_Assert(winSize > 2)) leaves the trackers of the frame

@@ -31,17 +31,19 @@ def main():
         variants["lg_lds"] = int(os.environ["LG_LDS"])
     if os.environ.get("LG_JR"):
         variants["lg_jr"] = int(os.environ["LG_JR"])
-    sc = synth.make_scene(0, 1920, 1080, npts, nboxes=8, box_w=w, box_h=h)
+    fw, fh = (3840, 2160) if os.environ.get("UHD") else (1920, 1080)
+    levels = int(os.environ.get("LEVELS", "4" if fw > 1920 else "3"))
+    sc = synth.make_scene(0, fw, fh, npts, nboxes=8, box_w=w, box_h=h)
     f0, f1 = sc.frame(0), sc.frame(1)
     pts = sc.points_at(1)
     L = _lib.load(_lib.STAMPS_LIB_PATH)
     st = hiprt.DeviceBuffer(npts * 64 * 8)
-    with lk.LKContext(1920, 1080, ring_slots=2, max_level_cap=3, variants=variants) as ctx:
+    with lk.LKContext(fw, fh, ring_slots=2, max_level_cap=levels, variants=variants) as ctx:
         ctx.push_frame(0, f0)
         ctx.push_frame(1, f1)
         rc = L.psn_lk_debug_set_stamps(ctx.handle, st.addr)
         assert rc == 0, "not a stamps build"
-        q = lk.make_query(1, 0, 0, npts, lk.make_params((w, h), 3))
+        q = lk.make_query(1, 0, 0, npts, lk.make_params((w, h), levels))
         for _ in range(2):
             ctx.track([q], pts)
         s = st.to_array((npts, 64), np.uint64).astype(np.int64)
@@ -58,7 +60,9 @@ def main():
            "mean": {k: round(float(v), 1) for k, v in zip(PHASES, s[:, :7].mean(0))},
            "a_values_split": {k: round(float(s[:, i].mean()), 1) for i, k in [(7, "stage"), (9, "quads")]},
            "fb_tiles_split": {k: round(float(s[:, i].sum() / max(int(s[:, 11].sum()), 1)), 1) for i, k in [(16, "pre"), (17, "chain_sums"), (18, "pad"), (13, "barrier"), (14, "tiles")]},
-           "per_iteration": {k: round(float(s[:, i].sum() / it), 1) for i, k in enumerate(PHASES) if i >= 2}}
+           "per_iteration": {k: round(float(s[:, i].sum() / it), 1) for i, k in enumerate(PHASES) if i >= 2},
+           # every slot: mean ticks per point (slots 10, 11, 14 are counts)
+           "slots_mean": [round(float(v), 1) for v in s[:, :24].mean(0)]}
     print(json.dumps(out, indent=1))
 
 
