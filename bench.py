@@ -301,15 +301,41 @@ def detection_extra(b):
     return head, loc, 1700.0
 
 
-def pinned_allocator():
+def pinned_allocator(kind="torch"):
+    """Pinned host buffers (uint8 numpy arrays): torch's pin_memory (default), or
+    (diagnostic --host-alloc) hipHostMalloc straight from the HIP runtime
+    ("hip", "hip-coherent") or page-aligned numpy memory registered with
+    hipHostRegister ("register")."""
     import torch
 
     keep = []
+    if kind == "torch":
+        def alloc(shape):
+            t = torch.empty(shape, dtype=torch.uint8).pin_memory()
+            keep.append(t)
+            return t.numpy()
+    else:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
 
-    def alloc(shape):
-        t = torch.empty(shape, dtype=torch.uint8).pin_memory()
-        keep.append(t)
-        return t.numpy()
+        def alloc(shape):
+            n = int(np.prod(shape))
+            if kind == "register":
+                raw = np.empty(n + 4096, np.uint8)
+                off = (-raw.ctypes.data) % 4096
+                a = raw[off:off + n]
+                if hip.hipHostRegister(a.ctypes.data, n, 0) != 0:
+                    raise RuntimeError("hipHostRegister failed")
+                keep.append(raw)
+                return a.reshape(shape)
+            p = ctypes.c_void_p()
+            flags = 0x40000000 if kind == "hip-coherent" else 0
+            if hip.hipHostMalloc(ctypes.byref(p), max(n, 1), flags) != 0:
+                raise RuntimeError("hipHostMalloc failed")
+            buf = (ctypes.c_uint8 * n).from_address(p.value)
+            keep.append(buf)
+            return np.ctypeslib.as_array(buf).reshape(shape)
 
     alloc.keep = keep
     return alloc
@@ -370,7 +396,7 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     C = len(cams)
     gridfast = args.features == "gridfast"
     L = _lib.load()
-    pinned = pinned_allocator()
+    pinned = pinned_allocator(args.host_alloc)
     feeds = [CameraFeed(c, args, pinned) for c in cams]
     max_obj = 2 * args.boxes
     group = t2d.Group(args.width, args.height, cams, device=local_rank, max_objects=max_obj)
@@ -449,8 +475,8 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         gathered = step(t, seq[j], seq[j + 1])
         ticks.append(time.perf_counter())
         t += 1
-        if i == args.diag_sync_at:  # diagnostic runs only: a device sync inside the timed region
-            torch.cuda.synchronize()
+        if i == args.diag_sync_at or (args.diag_sync_every and i % args.diag_sync_every == args.diag_sync_every - 1):
+            torch.cuda.synchronize()  # diagnostic runs only: a device sync inside the timed region
     g_last = drain()  # the last timed frame's hand-off
     gathered = g_last if g_last is not None else gathered
     torch.cuda.synchronize()
@@ -718,6 +744,14 @@ def tracker_roofline(args, r, C, profile):
                                "workload": f"the forward launch of one frame-set alone on the GPU: {C} cameras x "
                                            f"{args.points} points, median of {fw['launches']} launches"}
         out["isolated_backward"] = iso.get("backward")
+        # the same launches under rocprofv3 --kernel-trace (the round profile's
+        # `isolated` section: bench.py --mode isolated, this workload)
+        pi = ((profile or {}).get("isolated") or {}).get("kernels", {})
+        if fw and out.get("isolated") and fw.get("kernel") in pi:
+            pki = pi[fw["kernel"]]
+            a_p = launch_b / (pki["avg_us"] * 1e-6) / 1e9
+            out["isolated"].update({"profile_avg_us": pki["avg_us"], "profile_launches": pki["launches"],
+                                    "profile_achieved": round(a_p, 3), "profile_frac": round(a_p / HBM_PEAK_GBPS, 6)})
     lib_sha = file_sha16(_lib.LIB_PATH)
     if profile:
         pk = profile.get("kernels", {}).get(name, {})
@@ -775,6 +809,42 @@ def tracker_roofline(args, r, C, profile):
                                  f"{hbm_rate:.0f} GB/s; below 60 % of either peak the kernel is latency-bound"
                                  + (f"; waves wait {v['wait_any_frac']:.0%} of their cycles (SQ_WAIT_ANY)"
                                     if "wait_any_frac" in v else ""))
+    return out
+
+
+def mixed_roofline(args, line, profile):
+    """Roofline of the mixed-box leg's dominant kernel from the round profile's
+    `mixed_boxes` section (bench.py --box-dist pets under rocprofv3 --kernel-trace):
+    the kernel's BUSY time per frame-set (the union of its launches' intervals:
+    launches overlapping on several streams count once, so busy <= the frame-set
+    period) against the frame-set's SURVEY 8(d) LK bytes; traffic = PMC HBM bytes
+    of its launches per frame-set; wait_any_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES."""
+    mb = (profile or {}).get("mixed_boxes")
+    if not mb or not mb.get("kernels"):
+        return None
+    name, pk = max(mb["kernels"].items(), key=lambda kv: kv[1]["busy_us"] if kv[0].startswith("lk_kernel") else -1)
+    b = mb.get("bench") or {}
+    frames = (b.get("steps") or 0) + (b.get("warmup") or 0) + args.measure_steps + 1
+    if not frames or not pk.get("busy_us"):
+        return None
+    C = args.cameras
+    _, lk_b = algorithmic_bytes(args.width, args.height, 4, args.points)
+    busy_ms = pk["busy_us"] / frames / 1e3
+    ach = C * lk_b / (busy_ms * 1e-3) / 1e9
+    out = {"kernel": name, "bound": "latency", "achieved": round(ach, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBPS, 6), "bytes_per_frame_set": C * lk_b,
+           "busy_ms_per_frame_set": round(busy_ms, 4), "launches_per_frame_set": round(pk["launches"] / frames, 2),
+           "avg_launch_us": pk["avg_us"], "profile_ms_per_step": b.get("ms_per_step"),
+           "busy_within_step": b.get("ms_per_step") is not None and busy_ms <= b["ms_per_step"],
+           "frames_traced": frames, "profile": os.path.relpath(args.profile, ROOT),
+           "note": "busy time = union of the kernel's launch intervals in the profiled run, per frame-set; "
+                   "bytes = SURVEY 8(d) LK bytes 2*S_pyr + 21*N per camera-frame x cameras"}
+    if pk.get("hbm_bytes_per_launch") is not None:
+        out["traffic_per_frame_set"] = int(pk["hbm_bytes_per_launch"] * pk["launches"] / frames)
+    if pk.get("wait_any_frac") is not None:
+        out["wait_any_frac"] = pk["wait_any_frac"]
+    if line.get("compute"):
+        out["compute"] = line["compute"]
     return out
 
 
@@ -912,6 +982,7 @@ def tracker_legs(args, profile):
     lm = tracker_line(am, rm, 1, args.cameras, "weak", None)
     legs["mixed_boxes"] = {k: lm[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["mixed_boxes"]["lk_launches"] = {k: lm["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
+    legs["mixed_boxes"]["roofline"] = mixed_roofline(am, lm, profile)
     # the reference Run's real per-frame work together (PSNWhere_Tracker2D.cpp:735-757, 776-782,
     # 871-877): GridFAST per detection feeding PETS-sized box windows
     ar = argparse.Namespace(**{**vars(args), "features": "gridfast", "box_dist": "pets", "verify": False,
@@ -1207,7 +1278,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--mode", choices=["tracker", "kernel", "config4"], default="tracker")
+    ap.add_argument("--mode", choices=["tracker", "kernel", "config4", "isolated"], default="tracker")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--cameras", type=int, default=4, help="tracker mode: cameras per GPU (configs[2]: 4)")
@@ -1234,6 +1305,9 @@ def parse_args(argv=None):
     ap.add_argument("--measure-steps", type=int, default=20,
                     help="frames after the timed region with per-launch HIP-event timing (roofline)")
     ap.add_argument("--diag-sync-at", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--diag-sync-every", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--host-alloc", choices=["torch", "hip", "hip-coherent", "register"], default="torch",
+                    help=argparse.SUPPRESS)
     ap.add_argument("--push-last", action="store_true",
                     help="tracker mode: push frame t+ahead after complete_next(t+1) instead of before it")
     ap.add_argument("--step-profile", action="store_true", help="tracker mode: host ms of each slow step to stderr")
@@ -1261,6 +1335,9 @@ def main():
         sys.exit(launch_ranks(args, argv))
     if args.dry_run:
         return dry_main(args)
+    if args.mode == "isolated":  # the profile pass of roofline.isolated (tools/profile_round.sh)
+        print(json.dumps({"isolated": isolated_launches(args, args.cameras)}), flush=True)
+        return None
     if args.mode in ("kernel", "config4"):
         return kernel_main(args)
     return tracker_main(args)

@@ -34,7 +34,8 @@ def short(name):
     i = name.find("lk_kernel_bx<")
     if i >= 0:
         return name[i:name.index(">", i) + 1]
-    for k in ("lk_kernel_st", "lk_kernel", "pyramid_kernel", "read_u8", "read_x4", "write_u8", "write_x4"):
+    for k in ("lk_kernel_st", "lk_kernel_lg", "lk_kernel", "pyramid_kernel", "read_u8", "read_x4", "write_u8",
+              "write_x4"):
         if k in name:
             return k
     return name[:60]

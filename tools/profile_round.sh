@@ -22,6 +22,14 @@ timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU S
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY -d "$OUT/sq2" -o run --output-format csv -- python3 "$B" --steps 30 --warmup 3 $Q > "$OUT/sq2.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/cfetch" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cfetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/cwrite" -o run --output-format csv -- "$ROOT/tools/probes/probe_hbm_calib" > "$OUT/cwrite.log" 2>&1
+# isolated launches of the frame-set's windows (roofline.isolated) and the PETS-like
+# mixed-box leg (legs.mixed_boxes.roofline): kernel traces, PMC bytes, SQ_WAIT_ANY
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/iso" -o run --output-format csv -- python3 "$B" --mode isolated > "$OUT/iso_time.json" 2> "$OUT/iso.log"
+P="--box-dist pets --no-cpu-baseline --no-secondary --no-legs --no-isolated"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/pets" -o run --output-format csv -- python3 "$B" --steps 40 --warmup 5 $P > "$OUT/pets_bench.json" 2> "$OUT/pets.log"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pets_fetch" -o run --output-format csv -- python3 "$B" --steps 20 --warmup 3 $P > "$OUT/pets_fetch.log" 2>&1
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pets_write" -o run --output-format csv -- python3 "$B" --steps 20 --warmup 3 $P > "$OUT/pets_write.log" 2>&1
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY -d "$OUT/pets_sq2" -o run --output-format csv -- python3 "$B" --steps 20 --warmup 3 $P > "$OUT/pets_sq2.log" 2>&1
 python3 "$ROOT/tools/profile_summary.py" "$OUT" "$ROOT/mcmtt_opticalflow_amd/lib/libpsn_lk.so" "$OUT/profile.json" > "$OUT/profile_summary.log"
 find "$OUT/trace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 find "$OUT/ktrace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_mode_kernel_stats.csv" \;
