@@ -7,8 +7,11 @@
 // (:776-782, :871-877), which rebuilt both pyramids and the Scharr planes on
 // every call.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -203,6 +206,82 @@ int psn_lk_effective_max_level(int width, int height, int win_w, int win_h, int 
     return max_level;
 }
 
+// SDMA engine set-up. ROCr creates an SDMA engine's queue on the first copy that
+// engine runs: ~15 ms inside hsa_amd_memory_async_copy_on_engine, then ~0
+// (tools/probes/probe_sdma_engines: 16 engines on MI355X, H2D 6 MB). The HIP
+// runtime spreads async copies over the idle engines, so a frame upload that
+// lands on an engine for the first time stalls its caller (the bench's first
+// timed step after the device sync before the timed region: ~8 ms). Every
+// engine runs one 4-KB copy each way here, once per process and device.
+namespace {
+struct AgentPick {
+    uint32_t bdf = 0, domain = 0;
+    hsa_agent_t gpu{}, cpu{};
+    bool have_gpu = false, have_cpu = false;
+};
+hsa_status_t pick_agent(hsa_agent_t a, void *arg) {
+    AgentPick *p = (AgentPick *)arg;
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+    if (t == HSA_DEVICE_TYPE_CPU && !p->have_cpu) {
+        p->cpu = a;
+        p->have_cpu = true;
+    } else if (t == HSA_DEVICE_TYPE_GPU && !p->have_gpu) {
+        uint32_t bdf = 0, dom = 0;
+        if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS &&
+            hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS &&
+            bdf == p->bdf && dom == p->domain) {
+            p->gpu = a;
+            p->have_gpu = true;
+        }
+    }
+    return HSA_STATUS_SUCCESS;
+}
+void warm_sdma_engines(int device) {
+    int bus = 0, dev = 0, dom = 0;
+    if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+        hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+        hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess)
+        return;
+    if (hsa_init() != HSA_STATUS_SUCCESS) return;  // reference-counted: the HIP runtime's instance
+    AgentPick p;
+    p.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+    p.domain = (uint32_t)dom;
+    hsa_iterate_agents(pick_agent, &p);
+    void *h = nullptr, *d = nullptr;
+    hsa_signal_t sig{};
+    if (p.have_gpu && p.have_cpu && hipHostMalloc(&h, 4096, 0) == hipSuccess && hipMalloc(&d, 4096) == hipSuccess &&
+        hsa_signal_create(1, 0, nullptr, &sig) == HSA_STATUS_SUCCESS) {
+        for (int dir = 0; dir < 2; dir++) {
+            const hsa_agent_t da = dir == 0 ? p.gpu : p.cpu, sa = dir == 0 ? p.cpu : p.gpu;
+            void *dst = dir == 0 ? d : h;
+            const void *src = dir == 0 ? h : d;
+            uint32_t mask = 0;
+            if (hsa_amd_memory_copy_engine_status(da, sa, &mask) != HSA_STATUS_SUCCESS) continue;
+            for (int e = 0; e < 32; e++) {
+                if (!(mask & (1u << e))) continue;
+                hsa_signal_store_relaxed(sig, 1);
+                if (hsa_amd_memory_async_copy_on_engine(dst, da, src, sa, 4096, 0, nullptr, sig,
+                                                        (hsa_amd_sdma_engine_id_t)(1u << e), true) == HSA_STATUS_SUCCESS)
+                    hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+            }
+        }
+    }
+    if (sig.handle) hsa_signal_destroy(sig);
+    if (d) (void)hipFree(d);
+    if (h) (void)hipHostFree(h);
+    hsa_shut_down();
+}
+std::mutex g_warm_mu;
+std::vector<int> g_warmed;  // devices whose engines are set up
+void warm_sdma_once(int device) {
+    std::lock_guard<std::mutex> lk(g_warm_mu);
+    if (std::find(g_warmed.begin(), g_warmed.end(), device) != g_warmed.end()) return;
+    g_warmed.push_back(device);
+    warm_sdma_engines(device);
+}
+}  // namespace
+
 int psn_lk_create(int device, int width, int height, int ring_slots, int max_level_cap, psn_lk_ctx **out) {
     if (!out || width <= 0 || height <= 0 || ring_slots <= 0 || max_level_cap < 0 ||
         max_level_cap > psn::kPyrMaxTop)
@@ -231,6 +310,7 @@ int psn_lk_create(int device, int width, int height, int ring_slots, int max_lev
     };
     if (hipSetDevice(device) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     if (psn::lk_kernels_init() != hipSuccess) return fail(PSN_LK_ERR_HIP);
+    warm_sdma_once(device);  // (before any stream work: the engines' queues exist from here on)
     if (hipMalloc(&c->d_ctr, 2 * sizeof(unsigned)) != hipSuccess) return fail(PSN_LK_ERR_NOMEM);
     if (hipMemset(c->d_ctr, 0, 2 * sizeof(unsigned)) != hipSuccess) return fail(PSN_LK_ERR_HIP);
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) return fail(PSN_LK_ERR_HIP);

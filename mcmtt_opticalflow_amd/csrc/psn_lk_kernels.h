@@ -282,10 +282,25 @@ __host__ __device__ constexpr int lg_tiles_b_bytes(int tq) { return 2 * 2 * lg_p
 __host__ __device__ inline int lg_band_bytes(int w, int tr) { return align16((tr + 3) * 4 * bx_pm(w)); }
 // J region of the iterations (lg_jr): st_jreg_h(h) rows of bx_jrp(w) bytes, after the b tiles
 __host__ __device__ inline int lg_jr_bytes(int w, int h) { return align16(st_jreg_h(h) * bx_jrp(w)); }
+// b fallback by parity records (psn_lk_xb.h; build parameter PSN_LG_XB, off by
+// default: measured slower than the ordered tiles): 10
+// chains x 256 threads of 8-B run records in the b tile region, and a pool of
+// the HARD runs' terms after the J region
+#ifndef PSN_LG_XB
+#define PSN_LG_XB 0
+#endif
+constexpr int kXbRecBytes = 10 * 256 * 8;
+#ifndef PSN_LG_POOL_KB
+#define PSN_LG_POOL_KB 8
+#endif
+constexpr int kLgPoolBytes = PSN_LG_XB ? PSN_LG_POOL_KB * 1024 : 0;
+__host__ __device__ constexpr int lg_iter_region(int tq) {
+    return !PSN_LG_XB || lg_tiles_b_bytes(tq) > kXbRecBytes + 64 ? lg_tiles_b_bytes(tq) : kXbRecBytes + 64;
+}
 __host__ __device__ inline int lg_lds_bytes(int w, int h, int tr, bool jr, int tq) {
     int u = lg_band_bytes(w, tr);
     u = u > lg_tiles_a_bytes(tq) ? u : lg_tiles_a_bytes(tq);
-    const int it = lg_tiles_b_bytes(tq) + (jr ? lg_jr_bytes(w, h) : 0);
+    const int it = lg_iter_region(tq) + (jr ? lg_jr_bytes(w, h) : 0) + kLgPoolBytes;
     return lg_scr_bytes() + (u > it ? u : it);
 }
 #ifndef PSN_LG_JR_MAX_KB

@@ -24,7 +24,10 @@
 //
 // Bit-identical to oracle/lk_oracle.c (the SSE2 build's summation order, or the
 // scalar build's with PSN_LK_ACCUM_SCALAR).
-#include "psn_lk_bx.h"
+#include "psn_lk_xb.h"
+
+// (PSN_LG_XB, psn_lk_kernels.h: the b fallback by parity records before the
+// ordered tiles -- a build parameter, 0 = the tiles only)
 
 namespace psn {
 
@@ -259,9 +262,14 @@ __device__ __forceinline__ float lg_tiles(int qs, int NQ, float *buf, int nch, f
 
 constexpr int kLgMB = 4;  // quads per batch of slot loads in the passes over the window
 
+// Minimum waves per SIMD of the build (__launch_bounds__: k workgroups per CU of
+// 256 threads = k waves per SIMD; a build parameter for occupancy A/Bs)
+#ifndef PSN_LG_WAVES
+#define PSN_LG_WAVES 1
+#endif
 // TQ: quads per ordered-chain tile (kLgTQs; the planner's choice per query)
 template <int TQ>
-__global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
+__global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NT = kLgNT;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -270,7 +278,10 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
     int *EP = (int *)(RS + 16);
     uint8_t *U = smem + lg_scr_bytes();   // band staging | tile planes
     float *PL = (float *)U;
-    uint32_t *JR = (uint32_t *)(U + lg_tiles_b_bytes(TQ));  // J region (lg_jr), after the b tiles
+    uint32_t *JR = (uint32_t *)(U + lg_iter_region(TQ));  // J region (lg_jr), after the b tiles / run records
+#if PSN_LG_XB
+    int2 *XREC = (int2 *)U;  // b fallback run records [chain][thread]
+#endif
     uint8_t *const slot = (uint8_t *)A.lg_ws + (long long)blockIdx.x * A.lg_slot * 8;
     const float FLT_SCALE = 1.f / (1 << 20);
     int par = 0;
@@ -293,6 +304,9 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
         const int PM = bx_pm(w);  // I patch dwords per row
         const bool jrm = Q.lg_jr != 0;
         const int JRW = st_jreg_w(w), JRH = st_jreg_h(h), JRP4 = bx_jrp(w) >> 2;
+#if PSN_LG_XB
+        float *POOL = (float *)((uint8_t *)JR + (jrm ? lg_jr_bytes(w, h) : 0));  // HARD runs' terms
+#endif
         uint8_t *Pimg = U;
 
         const float hwx = __fmul_rn((float)(w - 1), 0.5f), hwy = __fmul_rn((float)(h - 1), 0.5f);
@@ -708,7 +722,182 @@ __global__ __launch_bounds__(kLgNT) void lk_kernel_lg(LkLaunchArgs A) {
                             LG_MARK(17);  // chain sums
                         }
                     };
+                    // ---- parity records (psn_lk_xb.h): every thread's run of every chain
+                    // as one record, the chain lanes walk them in order; the ordered
+                    // tiles when a term is past 2^24, a prefix past 2^30 or the pool of
+                    // HARD runs' terms overflows ----
+#if PSN_LG_XB
+                    auto xb_b = [&](float &acc_out) -> bool {
+                        const int wv = tid >> 6, fs = 32 * h0;
+                        // exact prefix at the run start per chain (the block scan's exclusive
+                        // prefix: wave-exclusive + the earlier waves' totals)
+                        int B[10];
+#pragma unroll
+                        for (int c = 0; c < 10; c++) {
+                            const int *r = rec + 8 * c;
+                            B[c] = T[c] + (wv > 0 ? r[0] : 0) + (wv > 1 ? r[1] : 0) + (wv > 2 ? r[2] : 0);
+                        }
+                        // guard (saturating sum of the runs' excursions: every prefix < 2^30,
+                        // no int wrap) and the largest |prefix| (the grid of the error bound)
+                        int gx = (long long)dmax * gmax > (long long)kExact || K > 64 ? (1 << 30) : 0, mx = 0;
+#pragma unroll
+                        for (int c = 0; c < 10; c++) {
+                            gx = max(gx, max(M[c], -m[c]));
+                            mx = max(mx, max(B[c] + M[c], -(B[c] + m[c])));
+                        }
+                        const unsigned gw = wave_sum_sat((unsigned)gx);
+                        const int mw = __builtin_amdgcn_readlane(wave_max_scan(mx), 63);
+                        if (lane == 0) {
+                            EP[4 + wv] = mw;
+                            EP[8 + wv] = (int)gw;
+                        }
+                        __syncthreads();
+                        const unsigned gsum = sat_add(sat_add((unsigned)EP[8], (unsigned)EP[9]), sat_add((unsigned)EP[10], (unsigned)EP[11]));
+                        if (gsum >= (1u << 30)) return false;
+                        const int MX = max(max(EP[4], EP[5]), max(EP[6], EP[7]));
+                        const int umax = MX + (MX >> 3) + 1024 <= (1 << 24) ? 1 : 1 << (31 - __builtin_clz((unsigned)(MX + (MX >> 3) + 1024)) - 23);
+                        // keys, term counts, HARD terms
+                        const bool mine = tid >= fs && cnt > 0;
+                        const int q1 = q0 + cnt, nq = mine ? q1 - fs * K : 0;
+                        const int nS = lg_sse_before(G, q1, G.nB2) - lg_sse_before(G, q0, G.nB2);
+                        const int nT = lg_tail_before(G, q1, G.nB2, G.tB) - lg_tail_before(G, q0, G.nB2, G.tB);
+                        const int ES = nq * (umax >> 1) + 2 * umax, ET = nq * 2 * umax + 2 * umax;
+                        int key[10], hard = 0;
+#pragma unroll
+                        for (int c = 0; c < 10; c++) {
+                            const int E = c % 5 == 4 ? ET : ES, n = c % 5 == 4 ? nT : nS;
+                            key[c] = mine && n > 0 ? xb_key(B[c] + m[c] - E, B[c] + M[c] + E) : 23;
+                            if (key[c] < 0) hard += n;
+                        }
+                        const int hs = wave_scan(hard);
+                        if (lane == 63) EP[12 + wv] = hs;
+                        if (tid == 0) EP[3] = 0;  // the replay's failure flag
+                        __syncthreads();
+                        const int pbase = (wv > 0 ? EP[12] : 0) + (wv > 1 ? EP[13] : 0) + (wv > 2 ? EP[14] : 0);
+                        const int ptotal = EP[12] + EP[13] + EP[14] + EP[15];
+                        if (ptotal > kLgPoolBytes / 4) return false;
+                        LG_MARK(19);  // xb: prefixes, guard, keys, pool scan
+                        // replay: each thread's run of every chain; first terms kept, the rest
+                        // from two representatives of either parity near B + first term (key
+                        // 23: one exact replay); HARD runs' terms into the pool
+                        float r0[10], r1[10];
+                        int f1[10], R0[10], poff[10];
+                        unsigned started = 0;
+                        {
+                            int o = pbase + hs - hard;
+#pragma unroll
+                            for (int c = 0; c < 10; c++) {
+                                poff[c] = o;
+                                if (key[c] < 0) o += c % 5 == 4 ? nT : nS;
+                                r0[c] = r1[c] = 0.f;
+                                f1[c] = R0[c] = 0;
+                            }
+                        }
+                        auto term = [&](int c, int t) {
+                            if (key[c] < 0) {
+                                POOL[poff[c]++] = (float)t;
+                                return;
+                            }
+                            const int ks = key[c] - 23, u = 1 << ks;
+                            if (!(started & (1u << c))) {
+                                started |= 1u << c;
+                                f1[c] = t;
+                                const int v = B[c] + t;
+                                R0[c] = ((v + u) >> (ks + 1)) << (ks + 1);
+                                r0[c] = (float)R0[c];
+                                r1[c] = (float)(R0[c] + u);
+                            } else {
+                                const float tf = (float)t;
+                                r0[c] = __fadd_rn(r0[c], tf);
+                                r1[c] = __fadd_rn(r1[c], tf);
+                            }
+                        };
+                        if (mine) {
+                            int y = y0, qx = x0;
+                            auto quad = [&](const uint2 &ip, const uint2 &xp, const uint2 &yp) {
+                                int d[4];
+                                lg_diffs(JJ, y, qx, ip, d);
+                                const int gxv[4] = {lo16(xp.x), hi16(xp.x), lo16(xp.y), hi16(xp.y)};
+                                const int gyv[4] = {lo16(yp.x), hi16(yp.x), lo16(yp.y), hi16(yp.y)};
+                                if (qx < G.nB2) {
+#pragma unroll
+                                    for (int i = 0; i < 4; i++) {
+                                        term(i, __mul24(d[i], gxv[i]));
+                                        term(5 + i, __mul24(d[i], gyv[i]));
+                                    }
+                                } else {
+#pragma unroll
+                                    for (int i = 0; i < 4; i++) {
+                                        if (4 * qx + i >= w) break;
+                                        term(4, __mul24(d[i], gxv[i]));
+                                        term(9, __mul24(d[i], gyv[i]));
+                                    }
+                                }
+                                if (++qx == QW) {
+                                    qx = 0;
+                                    y++;
+                                }
+                            };
+                            int k = 0;
+                            for (; k + kLgMB <= cnt; k += kLgMB) {
+                                uint2 ip[kLgMB], xp[kLgMB], yp[kLgMB];
+#pragma unroll
+                                for (int u = 0; u < kLgMB; u++) {
+                                    const int ix = (k + u) * NT + tid;
+                                    ip[u] = IPs[ix];
+                                    xp[u] = XPs[ix];
+                                    yp[u] = YPs[ix];
+                                }
+#pragma unroll
+                                for (int u = 0; u < kLgMB; u++) quad(ip[u], xp[u], yp[u]);
+                            }
+                            for (; k < cnt; k++) {
+                                const int ix = k * NT + tid;
+                                quad(IPs[ix], XPs[ix], YPs[ix]);
+                            }
+                        }
+                        LG_MARK(20);  // xb: replay
+                        // records (the b tiles region; its last readers passed a barrier)
+                        bool fail = false;
+                        if (tid >= fs) {
+#pragma unroll
+                            for (int c = 0; c < 10; c++) {
+                                const int n = c % 5 == 4 ? nT : nS;
+                                int2 rv;
+                                if (!mine || n == 0) {
+                                    rv = xb_rec_hard(0, 0);
+                                } else if (key[c] < 0) {
+                                    rv = xb_rec_hard(poff[c] - n, n);
+                                } else {
+                                    const int ks = key[c] - 23;
+                                    const int Q0 = ((int)r0[c] - R0[c]) >> ks;
+                                    const int D = (((int)r1[c] - R0[c] - (1 << ks)) >> ks) - Q0;
+                                    fail |= D < -1 || D > 1;
+                                    rv = xb_rec(Q0, f1[c], ks, D);
+                                }
+                                XREC[c * kXbRecThreads + tid] = rv;
+                            }
+                        }
+                        if (fail) EP[3] = 1;  // (no __syncthreads_or: it takes static LDS)
+                        __syncthreads();
+                        if (EP[3]) return false;
+                        LG_MARK(21);  // xb: records
+                        // the walk: chain lane c from the exact prefix before half wave h0
+                        if (tid < 10) {
+                            const int last = min(kXbRecThreads, (NQ + K - 1) / K);
+                            acc_out = xb_walk(XREC + tid * kXbRecThreads, POOL, fs, last, (float)base0);
+                        }
+                        LG_MARK(22);  // xb: walk
+                        return true;
+                    };
+                    float acc;
+                    if (!xb_b(acc)) {
+                        __syncthreads();  // every reader of the records / scratch is done
+                        acc = lg_tiles<2, TQ>(qs, NQ, PL, 10, (float)base0, loadB, storeB, geoB, markB);
+                    }
+#else
                     const float acc = lg_tiles<2, TQ>(qs, NQ, PL, 10, (float)base0, loadB, storeB, geoB, markB);
+#endif
                     LG_MARK(5);  // ordered b chains
                     if (tid < 64) {  // wave 0 combines in the SSE2 build's order
                         const int a = __float_as_int(acc);

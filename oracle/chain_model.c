@@ -183,3 +183,126 @@ float oracle_chain_binade(const float *f, int n, const int *seg_off, int nseg, i
     }
     return s;
 }
+
+/*
+ * Per-thread parity records with local HARD runs (the lk_kernel_lg b / A
+ * fallback of round 5): the chain from segment fs on,
+ * starting at the exact integer value `base` (every earlier prefix exact).
+ *   - B_t exact prefix at segment t, (m_t, M_t) its local prefix extremes (0
+ *     included), E_t = 8 * (terms from the start of segment fs to the end of t)
+ *     + 64: bounds |s - P| for every value of the segment and its representatives
+ *     while every |P| + E < 2^28 (ulp <= 16); past that the evaluation aborts
+ *     (returns NAN: the caller keeps its ordered tiles).
+ *   - key: 23 when [B + m - E, B + M + E] lies in [-2^24, 2^24] (no rounding: the
+ *     segment adds its exact total T), k >= 24 when it lies inside one binade of
+ *     |v| (grid u = 2^(k-23)), else HARD (its terms summed in order).
+ *   - a binade segment is a HEAD when the previous segment is not of key k (or
+ *     is HARD): its first term is added explicitly (s may sit on a finer grid),
+ *     the rest is a parity function (Q0, D): from a start s on the grid u, the
+ *     segment moves s by u * (Q0 + D * parity(s / u)), D in {-1, 0, 1}, found by
+ *     replaying it from two representatives of either parity near the start.
+ *   - the walk: per segment in order, s from the exact start.
+ * stats: [0] records walked, [1] HARD segments, [2] HARD terms, [3] heads,
+ * [4] 1 = aborted.
+ */
+static int key_abs(long long a) { /* a >= 0: 23 for a <= 2^24, else floor(log2 a) */
+    if (a <= (1LL << 24)) return 23;
+    int k = 63 - __builtin_clzll((unsigned long long)a);
+    return k;
+}
+float oracle_chain_runs(const float *f, const int *seg_off, int nseg, int fs, int base, int *stats) {
+    int recs = 0, hard = 0, hterms = 0, heads = 0;
+    if (stats) memset(stats, 0, 5 * sizeof(int));
+    enum { kMax = 4096 };
+    static __thread int key[kMax];
+    static __thread long long Bv[kMax + 1];
+    if (nseg > kMax) return NAN;
+    long long P = base;
+    const int a0 = seg_off[fs];
+    for (int t = fs; t < nseg; t++) {
+        const int a = seg_off[t], b = seg_off[t + 1];
+        Bv[t] = P;
+        long long m = 0, M = 0, q = 0;
+        for (int i = a; i < b; i++) {
+            if (fabsf(f[i]) > 16777216.f) {
+                if (stats) stats[4] = 1;
+                return NAN;
+            }
+            q += (long long)f[i];
+            if (q < m) m = q;
+            if (q > M) M = q;
+        }
+        P += q;
+        const long long E = 8LL * (b - a0) + 64;
+        const long long lo = Bv[t] + m - E, hi = Bv[t] + M + E;
+        if (hi >= (1LL << 28) || lo <= -(1LL << 28)) {
+            if (stats) stats[4] = 1;
+            return NAN;
+        }
+        int k;
+        if (lo >= -(1LL << 24) && hi <= (1LL << 24))
+            k = 23;
+        else if (lo > (1LL << 24)) {
+            k = key_abs(lo);
+            if (key_abs(hi) != k || hi >= (2LL << k)) k = -1;
+        } else if (hi < -(1LL << 24)) {
+            k = key_abs(-hi);
+            if (key_abs(-lo) != k || -lo >= (2LL << k)) k = -1;
+        } else
+            k = -1;
+        key[t] = b > a ? k : (t > fs ? key[t - 1] : 23);
+    }
+    float s = (float)base;
+    for (int t = fs; t < nseg; t++) {
+        const int a = seg_off[t], b = seg_off[t + 1];
+        if (b == a) continue;
+        const int k = key[t];
+        recs++;
+        if (k < 0) {
+            hard++;
+            hterms += b - a;
+            for (int i = a; i < b; i++) s = s + f[i];
+            continue;
+        }
+        if (k == 23) {
+            long long T = 0;
+            for (int i = a; i < b; i++) T += (long long)f[i];
+            s = (float)((long long)s + T);
+            continue;
+        }
+        const long long u = 1LL << (k - 23);
+        const int head = t == fs || key[t - 1] != k;
+        int i0 = a;
+        long long near = Bv[t];
+        if (head) {
+            heads++;
+            s = s + f[a];
+            near += (long long)f[a];
+            i0 = a + 1;
+        }
+        /* representatives: the multiple of 2u nearest `near`, and it + u */
+        const long long R0 = (long long)llround((double)near / (double)(2 * u)) * 2 * u;
+        float r0 = (float)R0, r1 = (float)(R0 + u);
+        for (int i = i0; i < b; i++) {
+            r0 = r0 + f[i];
+            r1 = r1 + f[i];
+        }
+        const long long Q0 = ((long long)r0 - R0) / u, Q1 = ((long long)r1 - (R0 + u)) / u;
+        const long long D = Q1 - Q0;
+        if (D < -1 || D > 1) {
+            if (stats) stats[4] = 2;
+            return NAN;
+        }
+        uint32_t bits;
+        memcpy(&bits, &s, 4);
+        const int p = (int)(bits & 1u);
+        s = (float)((long long)s + u * (Q0 + D * p));
+    }
+    if (stats) {
+        stats[0] = recs;
+        stats[1] = hard;
+        stats[2] = hterms;
+        stats[3] = heads;
+    }
+    return s;
+}

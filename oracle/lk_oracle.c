@@ -1,3 +1,4 @@
+#include <stdio.h>
 /*
  * oracle/lk_oracle.c -- TEST INFRASTRUCTURE ONLY (see lk_oracle.h).
  *
@@ -34,9 +35,18 @@ static long long *g_bsum_log = 0;
 void oracle_set_bsum_log(long long *buf) { g_bsum_log = buf; }
 static long long *g_chain_log = 0;
 static int g_chain_upt = 0;
+/* the per-thread parity-record model on every fallback evaluation (buf[16..21]:
+ * the caller's buffer holds 24 entries) */
+static int g_chain_log_ext = 0;
+static int g_chain_fs = 256;
+static float g_chain_ser[10];
+static float *g_chain_terms[10];
+static int g_chain_off[10][257];
+static size_t g_chain_cap = 0;
 void oracle_set_chain_log(long long *buf, int upt) {
     g_chain_log = buf;
     g_chain_upt = upt;
+    g_chain_log_ext = buf != 0;
 }
 /* lk_kernel_bx's chains of one b-sum evaluation through the binade-run model.
  * buf: [0] evaluations, [1] of them on the exact fast path (every prefix of every
@@ -50,6 +60,13 @@ static void chain_classify(const long long *t1, const long long *t2, int w, int 
     const int need = (U + 255) / 256;
     const int upt = g_chain_upt > 0 ? g_chain_upt : need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : 12;
     float *f = (float *)malloc(sizeof(float) * (size_t)w * h);
+    if (g_chain_log_ext && g_chain_cap < (size_t)w * h) {
+        for (int i = 0; i < 10; i++) {
+            free(g_chain_terms[i]);
+            g_chain_terms[i] = (float *)malloc(sizeof(float) * (size_t)w * h);
+        }
+        g_chain_cap = (size_t)w * h;
+    }
     int off[257];
     int exact = 1, walk_max = 0, st[5];
     long long recs = 0, hard = 0, hterms = 0;
@@ -81,6 +98,26 @@ static void chain_classify(const long long *t1, const long long *t2, int w, int 
         }
         const float ser = oracle_chain_serial(f, n);
         const float mod = oracle_chain_binade(f, n, off, 256, 64, st);
+        if (g_chain_log_ext) { /* [16] evaluations with a fallback, [17] sum of the longest chain walk
+                                * (records + HARD terms), [18] aborted, [19] mismatches, [20] serial
+                                * terms from the first failing thread (longest chain), [21] HARD terms */
+            int fs = 256;
+            long long Pq = 0;
+            for (int t = 0; t < 256 && fs == 256; t++) {
+                long long M = Pq, m = Pq;
+                for (int i = off[t]; i < off[t + 1]; i++) {
+                    Pq += (long long)f[i];
+                    if (Pq > M) M = Pq;
+                    if (Pq < m) m = Pq;
+                    if (fabsf(f[i]) > 16777216.f) M = 1LL << 30;
+                }
+                if (M > (1LL << 24) || m < -(1LL << 24)) fs = t;
+            }
+            if (fs < g_chain_fs) g_chain_fs = fs;
+            g_chain_ser[cc] = ser;
+            memcpy(g_chain_terms[cc], f, sizeof(float) * (size_t)n);
+            memcpy(g_chain_off[cc], off, sizeof(off));
+        }
         {   /* [11] terms after the chain's first inexact step, [12] of them the steps whose
              * accumulator stays below 2^24 - 2^16 in magnitude (exact integer additions),
              * [13] the same in blocks of 16 terms whose every step qualifies */
@@ -118,6 +155,41 @@ static void chain_classify(const long long *t1, const long long *t2, int w, int 
         if (st[4] > mhard) mhard = st[4];
     }
     (void)res;
+    if (g_chain_log_ext && g_chain_fs < 256) { /* the kernel's fallback: every chain from the first failing thread */
+        const int fs = g_chain_fs;
+        int walk_max = 0, ser_max = 0;
+        g_chain_log[16]++;
+        for (int cc = 0; cc < 10; cc++) {
+            const float *fc = g_chain_terms[cc];
+            const int *oc = g_chain_off[cc];
+            long long base = 0;
+            for (int i = 0; i < oc[fs]; i++) base += (long long)fc[i];
+            int st2[5];
+            const float r = oracle_chain_runs(fc, oc, 256, fs, (int)base, st2);
+            if (r != r) {
+                g_chain_log[18]++;
+                continue;
+            }
+            if (memcmp(&r, &g_chain_ser[cc], 4) != 0) {
+                if (g_chain_log[19]++ == 0 && getenv("CHAIN_DUMP")) {
+                    FILE *fp = fopen(getenv("CHAIN_DUMP"), "wb");
+                    if (fp) {
+                        int hdr[3] = {fs, (int)base, oc[256]};
+                        fwrite(hdr, 4, 3, fp);
+                        fwrite(oc, 4, 257, fp);
+                        fwrite(fc, 4, (size_t)oc[256], fp);
+                        fclose(fp);
+                    }
+                }
+            }
+            if (st2[0] + st2[2] > walk_max) walk_max = st2[0] + st2[2];
+            if (oc[256] - oc[fs] > ser_max) ser_max = oc[256] - oc[fs];
+            g_chain_log[21] += st2[2];
+        }
+        g_chain_log[17] += walk_max;
+        g_chain_log[20] += ser_max;
+    }
+    g_chain_fs = 256;
     free(f);
     g_chain_log[0]++;
     g_chain_log[2] += mismatch;

@@ -87,6 +87,9 @@ void oracle_set_chain_log(long long *buf, int upt);
 /* ---- Binade-run model of an ordered float chain (oracle/chain_model.c) ---- */
 float oracle_chain_serial(const float *f, int n);
 float oracle_chain_binade(const float *f, int n, const int *seg_off, int nseg, int wave, int *stats);
+/* Per-thread parity records with local HARD segments (lk_kernel_lg fallback): the
+ * chain from segment fs on, from the exact value base; NAN = aborted. */
+float oracle_chain_runs(const float *f, const int *seg_off, int nseg, int fs, int base, int *stats);
 
 /* ---- GridFAST feature extraction (oracle/gridfast_oracle.c) ----
  * FeatureDetector::create("GridFAST")->detect(gray, kps, mask(rect) = 255)

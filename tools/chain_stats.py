@@ -38,7 +38,7 @@ def main():
     W, H, npts, nboxes, period = 1920, 1080, 512, 8, 10
     sc = synth.make_scene(0, W, H, npts, nboxes=nboxes)
     L = oracle.lib()
-    buf = (ctypes.c_longlong * 16)()
+    buf = (ctypes.c_longlong * 24)()
     L.oracle_set_chain_log.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.oracle_set_chain_log(ctypes.addressof(buf), upt)
     T2.NTHREADS = 1
