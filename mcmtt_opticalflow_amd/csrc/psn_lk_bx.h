@@ -126,6 +126,47 @@ __device__ __forceinline__ bool bx_eval(const int *rec, int &total, int &h0, int
     if (h0 & 1) base0 += hw == 0 ? s.x : hw == 1 ? s.y : hw == 2 ? s.z : s.w;
     return h0 == 8;
 }
+// The same test at THREAD granularity (lk_kernel_lg: the ordered chains start at
+// the first failing thread's run, not at its half wave): bx_check_t records each
+// wave's first failing thread (256: none) and that thread's exact prefix of every
+// chain (the block-exclusive prefix: every earlier prefix passed the test, so it
+// is an exact integer); bx_eval_t returns the block's first failing thread f and,
+// on lane c, chain c's total and its exact prefix before thread f.
+constexpr int kBxThrRec = 128;  // [4 waves][16]: the first failing thread's prefixes
+template <int NC>
+__device__ __forceinline__ void bx_check_t(const int (&E)[NC], const int (&M)[NC], const int (&m)[NC], bool bad, int *rec,
+                                           bool no_tail) {
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    int p[NC];
+    int hi = 0, lo = 0;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const int *r = rec + 8 * c;
+        p[c] = E[c] + (wv > 0 ? r[0] : 0) + (wv > 1 ? r[1] : 0) + (wv > 2 ? r[2] : 0);
+        if (no_tail && c % 5 == 4) continue;
+        hi = max(hi, p[c] + M[c]);
+        lo = min(lo, p[c] + m[c]);
+    }
+    const unsigned long long f = __ballot((hi > kExact) | (lo < -kExact) | bad);
+    const int fl = f == 0ull ? 64 : __builtin_ctzll(f);
+    if (lane == 0) rec[kBxHalfRec + wv] = f == 0ull ? 256 : 64 * wv + fl;
+    if (lane == fl) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) rec[kBxThrRec + 16 * wv + c] = p[c];
+    }
+}
+template <int NC>
+__device__ __forceinline__ bool bx_eval_t(const int *rec, int &total, int &f, int &base0) {
+    const int lane = threadIdx.x & 63;
+    const int c = lane < NC ? lane : 0;
+    const int4 hh = *(const int4 *)(rec + kBxHalfRec);
+    f = min(min(hh.x, hh.y), min(hh.z, hh.w));
+    const int4 t = *(const int4 *)(rec + 8 * c);
+    total = t.x + t.y + t.z + t.w;
+    base0 = f < 256 ? rec[kBxThrRec + 16 * (f >> 6) + c] : 0;
+    return f == 256;
+}
 __device__ __forceinline__ float rl_f(int v, int lane) { return (float)__builtin_amdgcn_readlane(v, lane); }
 
 // chain-run update with one term

@@ -480,10 +480,10 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
                 par ^= 1;
                 bx_publish<15>(T, rec, G.tA == 0);
                 __syncthreads();
-                bx_check<15>(T, M, m, badA, rec, G.tA == 0);
+                bx_check_t<15>(T, M, m, badA, rec, G.tA == 0);
                 __syncthreads();
                 int tot, h0, base0;
-                const bool exact = bx_eval<15>(rec, tot, h0, base0);
+                const bool exact = bx_eval_t<15>(rec, tot, h0, base0);
                 float s3[3];
                 if (exact) {
 #pragma unroll
@@ -495,9 +495,9 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
                         s3[s] = t;
                     }
                 } else {
-                    // ordered chains from half wave h0 on (every earlier prefix is an exact
-                    // integer: the chain lanes start from base0)
-                    const int qs = min(h0 * 32 * K, NQ);
+                    // ordered chains from thread h0's run on (every earlier prefix is an
+                    // exact integer: the chain lanes start from base0)
+                    const int qs = min(h0 * K, NQ);
                     auto geoA = [&](int q, int &bs, int &bt) {
                         bs = lg_sse_before(G, q, G.nA);
                         bt = lg_tail_before(G, q, G.nA, G.tA);
@@ -653,10 +653,10 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
                 par ^= 1;
                 bx_publish<10>(T, rec, G.tB == 0);
                 __syncthreads();
-                bx_check<10>(T, M, m, bad, rec, G.tB == 0);
+                bx_check_t<10>(T, M, m, bad, rec, G.tB == 0);
                 __syncthreads();
                 int tot, h0, base0;
-                const bool bex = bx_eval<10>(rec, tot, h0, base0);
+                const bool bex = bx_eval_t<10>(rec, tot, h0, base0);
                 LG_MARK(3);  // publish / check / eval
                 float b1, b2;
                 if (bex) {
@@ -668,9 +668,9 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
                     }
                 } else {
                     LG_COUNT(11);
-                    // ordered float chains from half wave h0 on (chain lanes: wave 0, lanes
-                    // 0-9, from their exact prefixes base0), tiles of TQ quads
-                    const int qs = min(h0 * 32 * K, NQ);
+                    // ordered float chains from thread h0's run on (chain lanes: wave 0,
+                    // lanes 0-9, from their exact prefixes base0), tiles of TQ quads
+                    const int qs = min(h0 * K, NQ);
                     auto geoB = [&](int q, int &bs, int &bt) {
                         bs = lg_sse_before(G, q, G.nB2);
                         bt = lg_tail_before(G, q, G.nB2, G.tB);
@@ -728,7 +728,7 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
                     // HARD runs' terms overflows ----
 #if PSN_LG_XB
                     auto xb_b = [&](float &acc_out) -> bool {
-                        const int wv = tid >> 6, fs = 32 * h0;
+                        const int wv = tid >> 6, fs = h0;
                         // exact prefix at the run start per chain (the block scan's exclusive
                         // prefix: wave-exclusive + the earlier waves' totals)
                         int B[10];
