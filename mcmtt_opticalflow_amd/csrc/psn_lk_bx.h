@@ -127,7 +127,9 @@ __device__ __forceinline__ bool bx_eval(const int *rec, int &total, int &h0, int
     return h0 == 8;
 }
 // The same test at THREAD granularity (lk_kernel_lg: the ordered chains start at
-// the first failing thread's run, not at its half wave): bx_check_t records each
+// the first failing thread's run, not at its half wave; lk_kernel_bx keeps the
+// half waves: the failing lane's prefixes kept live past the test spilled
+// registers in every build of it): bx_check_t records each
 // wave's first failing thread (256: none) and that thread's exact prefix of every
 // chain (the block-exclusive prefix: every earlier prefix passed the test, so it
 // is an exact integer); bx_eval_t returns the block's first failing thread f and,
