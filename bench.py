@@ -1074,6 +1074,9 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     torch.cuda.set_stream(stream)
     ctx = lk.LKContext(W, H, ring_slots=R * C, max_level_cap=levels - 1, device=local_rank)
     ctx.set_stream(stream.cuda_stream)
+    for kv in getattr(args, "lk_variant", None) or []:  # experiments: psn_lk_debug_set_variant
+        k, v = kv.split("=")
+        ctx.set_variant(k, int(v))
     mode = 2 if C == 1 else 1
     ctx.set_ingest_overlap(mode)
     sb = pdist.slot_bytes(N, C)
@@ -1279,6 +1282,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mode", choices=["tracker", "kernel", "config4", "isolated"], default="tracker")
+    ap.add_argument("--lk-variant", action="append", metavar="KEY=VALUE",
+                    help="kernel-variant override of --mode kernel/config4 (A/B experiments; _lib.VARIANTS keys)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--cameras", type=int, default=4, help="tracker mode: cameras per GPU (configs[2]: 4)")

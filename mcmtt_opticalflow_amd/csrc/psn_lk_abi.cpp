@@ -101,6 +101,7 @@ struct psn_lk_ctx {
     int force_threads = 0;
     bool force_generic = false;
     bool onewave = true;  // ONEWAVE 0: multi-wave iterations in the single-tile kernel
+    bool st_ovl = true;   // ST_OVL 0: every level's A phase in the single-tile prologue
     bool box = true;      // BOX 0: box windows run the row-tiled kernel instead of lk_kernel_bx
     // TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
     // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
@@ -780,6 +781,7 @@ struct PlannedQuery {
     bool single = false;        // single-tile kernel (window <= 1024 px, LDS plan fits)
     int st_lds = 0;             // its LDS
     int ow_rows = 1 << 30, ow_lds = 0;  // its one-wave mode
+    int ovl_lds = 0;                    // the one-wave mode with the overlapped A phase (0: does not fit)
     int bx_upt = 0, bx_lds = 0;  // box kernel units per thread (0: does not fit)
     int tiled_tr = 0;           // row-tiled kernel: tile rows (0: window not LDS-resident)
     int lg_tr = 0;              // large-window kernel: band rows
@@ -858,6 +860,8 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
             if (psn::ow_rows(w, h) <= psn::kOwMaxRows && so.total <= psn::kStMaxLds) {
                 pq.ow_rows = psn::ow_rows(w, h);
                 pq.ow_lds = so.total;
+                const psn::LkStLayout sv(w, h, sse, ml + 1, true, true);
+                if (sv.total <= psn::kStMaxLds) pq.ovl_lds = sv.total;
             }
         }
     }
@@ -1018,7 +1022,18 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
             lds = lds_ow;
             // more points than two workgroups per CU hold, and LDS for three:
             // the 168-VGPR variant (three per CU; one-camera launches fit at two)
-            if (oept == 2 && E <= 8 && lds_ow <= 53 * 1024 && wgs > 2 * c->num_cus) threads += 200000;
+            if (oept == 2 && E <= 8 && lds_ow <= 53 * 1024 && wgs > 2 * c->num_cus) {
+                threads += 200000;
+            } else if (c->st_ovl && E > 4) {
+                // two workgroups per CU: the finer levels' A phase beside the
+                // iterations, per query whose overlapped layout fits
+                lds = 0;
+                for (int i = 0; i < a.nq; i++) {
+                    const PlannedQuery &pq = *grp[i];
+                    a.q[i].st_ovl = pq.ovl_lds > 0 ? 1 : 0;
+                    lds = std::max(lds, pq.ovl_lds > 0 ? pq.ovl_lds : pq.ow_lds);
+                }
+            }
         }
         bool builds = false;
         if (c->pend && fused_slot < 0 && !d_counts) {  // fuse the deferred build into this launch's tail
@@ -1304,6 +1319,7 @@ int psn_lk_debug_set_variant(psn_lk_ctx *c, int key, int value) {
     case PSN_LK_VARIANT_LARGE: c->force_large = value != 0; return PSN_LK_OK;
     case PSN_LK_VARIANT_LG_LDS: c->lg_lds = std::max(4 * 1024, std::min(value, 160 * 1024 - 1024)); return PSN_LK_OK;
     case PSN_LK_VARIANT_LG_JR: c->lg_jr = value != 0; return PSN_LK_OK;
+    case PSN_LK_VARIANT_ST_OVL: c->st_ovl = value != 0; return PSN_LK_OK;
     default: return PSN_LK_ERR_ARG;
     }
 }

@@ -336,12 +336,13 @@ __device__ __forceinline__ void dma_region(uint32_t *dst, const LevelDev &L, int
 // chunk of dwords c0.. is contiguous in LDS); patches crossing the image border
 // reflect their rows, move the dwords that lie inside the image the same way and
 // gather the others' bytes through reflect-101.
+// NT threads t = 0..NT-1 of the caller's group (the workgroup, or one wave).
 template <int NT>
-__device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m,
-                                          unsigned dv_m) {
+__device__ __forceinline__ void dma_patch_t(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m,
+                                            unsigned dv_m, int t) {
     const int ax = gx0 & ~3;
     const int n = PH * m;
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wid = t >> 6, lane = t & 63;
     if (gy0 >= 0 && gx0 >= 0 && gy0 + PH <= L.h && gx0 + PW <= L.w) {
         // the row's last dword may read up to 6 bytes past the image width:
         // inside the 256-B pitch, the next row, or the ring's slack
@@ -374,6 +375,11 @@ __device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int g
             }
         }
     }
+}
+template <int NT>
+__device__ __forceinline__ void dma_patch(uint8_t *dst, const LevelDev &L, int gy0, int gx0, int PW, int PH, int m,
+                                          unsigned dv_m) {
+    dma_patch_t<NT>(dst, L, gy0, gx0, PW, PH, m, dv_m, (int)threadIdx.x);
 }
 // dma_patch for rows of any width (no division magic): each thread's (row,
 // dword) by a Walk over the PH x m dword grid.

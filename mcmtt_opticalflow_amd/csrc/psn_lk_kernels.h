@@ -53,6 +53,7 @@ struct LkQueryDev {
     union {
         int bx_hw;  // box kernel: half waves per fallback tile
         int lg_jr;  // large-window kernel: 1 = the iterations read J from an LDS copy of its region
+        int st_ovl; // single-tile one-wave kernel: 1 = the finer levels' A phase runs beside the iterations
     };
     unsigned dv_bxpm, dv_bxjr;
 };
@@ -174,9 +175,14 @@ __host__ __device__ inline int lk_pat_rs(int w) { return 4 * lk_pat_m(w); }
 //     float chain planes RA) and what only the iterations use (the two J
 //     regions JP, the b chain planes / err row R) -- 49.6 KB at 21x21 with 4
 //     levels: three workgroups per CU.
+//   overlapped one-wave layout (ow + ovl): no union -- the prologue computes only
+//     the coarsest level's A phase; waves 1-3 compute the finer levels' (I
+//     patch, Scharr, window values, A chains) while wave 0 iterates, so the I
+//     patches, Scharr planes and A planes of every level stay beside the J
+//     regions and b planes: 66.6 KB at 21x21 with 4 levels.
 struct LkStLayout {
     int tbl, ri, lv, jp, pim, pim_stride, dg, dg_stride, iw, iw_stride, r, ra, total;
-    __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev, bool ow = false) {
+    __host__ __device__ LkStLayout(int w, int h, bool sse, int nlev, bool ow = false, bool ovl = false) {
         const int wh = w * h;
         tbl = 0;
         ri = tbl + 2 * kMaxLevels * 8 * 4;
@@ -187,7 +193,15 @@ struct LkStLayout {
         const int rb_a = 12 * nlev * lk_st_planeA(w, h, sse);
         const int pb = 16 * lk_st_planeB(w, h, sse);
         const int eb = 4 * round16i(wh);
-        if (ow) {
+        if (ow && ovl) {
+            iw = kStScratchBytes;
+            pim = iw + nlev * iw_stride;
+            dg = pim + nlev * pim_stride;
+            ra = dg + nlev * dg_stride;
+            jp = ra + rb_a;
+            r = jp + 8 * st_jp_cm_dw(w, h);
+            total = r + (pb > eb ? pb : eb);
+        } else if (ow) {
             iw = kStScratchBytes;  // fused builds use LDS from kStScratchBytes, after the LK work
             const int u = iw + nlev * iw_stride;
             pim = u;  // prologue view

@@ -1021,6 +1021,43 @@ __device__ __forceinline__ void pyr_tail(const LkLaunchArgs &A, uint8_t *smem) {
     }
 }
 
+// Solver table of one level from the A sums (a11, a22 saturating, s12 wrapping)
+// and the 15 ordered chain sums c (sum s = 0..2: chains 5s..5s+3 the SSE2 lanes,
+// 5s+4 the tail; used only when the sum is not exact as an integer):
+// {A11, A12, A22, 1/D, minEig, ok} as LKTrackerInvoker computes them.
+__device__ __forceinline__ void st_level_table(float *lv, unsigned a11, int s12, unsigned a22, float c0, float c1,
+                                               float c2, float c3, float c4, float c5, float c6, float c7, float c8,
+                                               float c9, float c10, float c11, float c12, float c13, float c14,
+                                               bool sse, int wh, float min_eig) {
+    // a sum whose every term and every partial sum (in any order) is an
+    // integer <= 2^24 is exact in float: its integer value; otherwise the
+    // ordered chains, combined in the SSE2 build's order
+    float s0 = c4, s1 = c9, s2 = c14;
+    if (sse) {
+        s0 = __fadd_rn(s0, __fadd_rn(__fadd_rn(__fadd_rn(c0, c1), c2), c3));
+        s1 = __fadd_rn(s1, __fadd_rn(__fadd_rn(__fadd_rn(c5, c6), c7), c8));
+        s2 = __fadd_rn(s2, __fadd_rn(__fadd_rn(__fadd_rn(c10, c11), c12), c13));
+    }
+    float A11 = a11 <= (unsigned)kExact ? (float)a11 : s0;
+    float A12 = ((a11 + a22) >> 1) <= (unsigned)kExact ? (float)s12 : s1;
+    float A22 = a22 <= (unsigned)kExact ? (float)a22 : s2;
+    const float FLT_SCALE = 1.f / (1 << 20);
+    A11 = __fmul_rn(A11, FLT_SCALE);
+    A12 = __fmul_rn(A12, FLT_SCALE);
+    A22 = __fmul_rn(A22, FLT_SCALE);
+    const float D = __fsub_rn(__fmul_rn(A11, A22), __fmul_rn(A12, A12));
+    const float dd = __fsub_rn(A11, A22);
+    const float t = __fadd_rn(__fmul_rn(dd, dd), __fmul_rn(__fmul_rn(4.f, A12), A12));
+    const float minEig = __fdiv_rn(__fsub_rn(__fadd_rn(A22, A11), sqrtf(t)), (float)(2 * wh));
+    const bool ok = !(minEig < min_eig || D < FLT_EPSILON);
+    lv[0] = A11;
+    lv[1] = A12;
+    lv[2] = A22;
+    lv[3] = ok ? __fdiv_rn(1.f, D) : 0.f;
+    lv[4] = minEig;
+    lv[5] = ok ? 1.f : 0.f;
+}
+
 // Diagnostic stamps of the single-tile kernel (PSN_LK_STAMPS): 60 start, 50
 // prologue landed, 51 Scharr of all levels, 52 A products + reduction, 53
 // solver table; per level L*10+0 start, +1 J staged, +2 window loaded, +7
@@ -1048,7 +1085,13 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
     const int PW = w + 3, DW = w + 1;
     const int RS = lk_pat_rs(w);  // I patch row stride (bytes)
 
-    const LkStLayout lay(w, h, sse, nlev, E > 0);
+    // overlapped A phase (one-wave builds at two workgroups per CU): the prologue
+    // computes the coarsest level only; waves 1-3 compute the finer levels while
+    // wave 0 iterates (the per-level barriers order their tables before use)
+    // (not the 4-row build: its VGPRs would pass 170, one workgroup less per CU)
+    const bool ovl = E > 4 && OCC == 1 && Q.st_ovl != 0;
+    const int lo = ovl ? maxL : 0;  // the prologue's levels: lo..maxL
+    const LkStLayout lay(w, h, sse, nlev, E > 0, ovl);
     int *RI = (int *)(smem + lay.ri);
     float *LV = (float *)(smem + lay.lv);
     uint32_t *JP = (uint32_t *)(smem + lay.jp);
@@ -1100,6 +1143,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
 #pragma unroll
     for (int l = 0; l < kStMaxLev; l++) {
         if (l > maxL) break;
+        if (l < lo) continue;
         const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
         const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
         if (!gg.valid) continue;
@@ -1140,6 +1184,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
 #pragma unroll
     for (int l = 0; l < kStMaxLev; l++) {
         if (l > maxL) break;
+        if (l < lo) continue;
         const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
         const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
         if (!gg.valid) continue;
@@ -1166,6 +1211,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
 #pragma unroll
     for (int l = 0; l < kStMaxLev; l++) {
         if (l > maxL) break;
+        if (l < lo) continue;
         const LevelDev I = ring_level(A.ring, Q.prev_slot, l);
         const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
         // Per-sum exactness: A11 (terms >= 0) is exact when s11 <= 2^24, A22 when
@@ -1220,7 +1266,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
         for (int half = 0; half < 2; half++) {
             const int q = lane + 64 * half;
             const int l = q / 15, r = q - 15 * (q / 15);
-            if (l <= maxL) {
+            if (l <= maxL && l >= lo) {
                 unsigned a11 = 0, a22 = 0;
 #pragma unroll
                 for (int ww = 0; ww < NW; ww++) {
@@ -1241,7 +1287,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
         // CH written by other lanes of this wave: LDS executes a wave's accesses in
         // order; the clobber keeps the compiler from hoisting the reads
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane <= maxL) {
+        if (lane <= maxL && lane >= lo) {
             const int l = lane;
             unsigned a11 = 0, a22 = 0;
             int s12 = 0;
@@ -1252,37 +1298,9 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
                 s12 += ra[8];
                 a22 = sat_add(a22, (unsigned)ra[16]);
             }
-            // a sum whose every term and every partial sum (in any order) is an
-            // integer <= 2^24 is exact in float: its integer value; otherwise the
-            // ordered chains
-            float s3[3];
-#pragma unroll
-            for (int s = 0; s < 3; s++) {
-                const float *c = CH + l * 15 + s * 5;
-                float tail = c[4];
-                if (sse) tail = __fadd_rn(tail, __fadd_rn(__fadd_rn(__fadd_rn(c[0], c[1]), c[2]), c[3]));
-                s3[s] = tail;
-            }
-            const float A11_ = a11 <= (unsigned)kExact ? (float)a11 : s3[0];
-            const float A12_ = ((a11 + a22) >> 1) <= (unsigned)kExact ? (float)s12 : s3[1];
-            const float A22_ = a22 <= (unsigned)kExact ? (float)a22 : s3[2];
-            float A11 = A11_, A12 = A12_, A22 = A22_;
-            const float FLT_SCALE = 1.f / (1 << 20);
-            A11 = __fmul_rn(A11, FLT_SCALE);
-            A12 = __fmul_rn(A12, FLT_SCALE);
-            A22 = __fmul_rn(A22, FLT_SCALE);
-            const float D = __fsub_rn(__fmul_rn(A11, A22), __fmul_rn(A12, A12));
-            const float dd = __fsub_rn(A11, A22);
-            const float t = __fadd_rn(__fmul_rn(dd, dd), __fmul_rn(__fmul_rn(4.f, A12), A12));
-            const float minEig = __fdiv_rn(__fsub_rn(__fadd_rn(A22, A11), sqrtf(t)), (float)(2 * wh));
-            const bool ok = !(minEig < Q.min_eig || D < FLT_EPSILON);
-            float *lv = LV + l * kStLvFloats;
-            lv[0] = A11;
-            lv[1] = A12;
-            lv[2] = A22;
-            lv[3] = ok ? __fdiv_rn(1.f, D) : 0.f;
-            lv[4] = minEig;
-            lv[5] = ok ? 1.f : 0.f;
+            const float *c = CH + l * 15;
+            st_level_table(LV + l * kStLvFloats, a11, s12, a22, c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8],
+                           c[9], c[10], c[11], c[12], c[13], c[14], sse, wh, Q.min_eig);
         }
     }
     __syncthreads();  // LV published; the A planes in R are dead from here
@@ -1353,6 +1371,87 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
         const JWalk wkh_int = jwalk_t(th, JRW >> 2, NT - 64, Q.dv_jrw4), wkh_bord = jwalk_t(th, JRW, NT - 64, Q.dv_jrw);
         const JWalk wk0_int = jwalk_t(lane, JRW >> 2, 64, Q.dv_jrw4), wk0_bord = jwalk_t(lane, JRW, 64, Q.dv_jrw);
         pf.cs = JRHc;
+        // overlapped A phase of level l by ONE wave (no barrier: a wave's LDS
+        // accesses complete in order): I patch by LDS-DMA, Scharr plane, window
+        // values and A products, the 15 ordered chains when a sum is inexact, and
+        // the level's solver table -- the prologue's arithmetic, one wave wide
+        auto a_level_wave = [&](int l) {
+            const LevelDev I = tbl_get(TBL, 0, l);
+            const IGeo gg = i_geo(px0, py0, hwx, hwy, l, w, h, I.w, I.h);
+            if (!gg.valid) return;
+            uint8_t *const pim = smem + lay.pim + l * lay.pim_stride;
+            dma_patch_t<64>(pim, I, gg.ipy - 1, gg.ipx - 1, PW, h + 3, lk_pat_m(w), Q.dv_pm, lane);
+            dma_wait();
+            const uint8_t *P = pim + ((gg.ipx - 1) & 3);
+            short2 *Dg = (short2 *)(smem + lay.dg + l * lay.dg_stride);
+            {
+                Walk wk;
+                wk.init_m(lane, 64, DW, Q.dv_dw);
+                for (int idx = lane; idx < (h + 1) * DW; idx += 64, wk.step()) {
+                    const int gy = gg.ipy + wk.y, gx = gg.ipx + wk.x;
+                    short2 d = make_short2(0, 0);
+                    if ((unsigned)gy < (unsigned)I.h && (unsigned)gx < (unsigned)I.w) {
+                        const uint8_t *p = P + wk.y * RS + wk.x;
+                        const int a0 = p[0], a1 = p[1], a2 = p[2];
+                        const int b0 = p[RS], b2 = p[RS + 2];
+                        const int c0 = p[2 * RS], c1 = p[2 * RS + 1], c2 = p[2 * RS + 2];
+                        d.x = (short)(3 * (a2 + c2) + 10 * b2 - 3 * (a0 + c0) - 10 * b0);
+                        d.y = (short)(3 * ((c0 - a0) + (c2 - a2)) + 10 * (c1 - a1));
+                    }
+                    Dg[idx] = d;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            int2 *IW = (int2 *)(smem + lay.iw + l * lay.iw_stride);
+            float *PA = RA + l * 3 * GA.P;
+            unsigned s11 = 0, s22 = 0;  // per lane <= 16 * 4080^2 < 2^30
+            int s12 = 0;
+            for (int i0 = 0; i0 < wh; i0 += 64) {
+                const int idx = i0 + lane;
+                const bool v = idx < wh;
+                const int i = v ? idx : 0;
+                const int y = qdiv(i, Q.dv_w), x = i - y * w;
+                const uint8_t *p = P + (y + 1) * RS + x + 1;
+                const int iw = PSN_DESCALE(__mul24((int)p[0], gg.w00) + __mul24((int)p[1], gg.w01) +
+                                               __mul24((int)p[RS], gg.w10) + __mul24((int)p[RS + 1], gg.w11), 9);
+                const short2 *d = Dg + y * DW + x;
+                const short2 d00 = d[0], d01 = d[1], d10 = d[DW], d11 = d[DW + 1];
+                int ix = PSN_DESCALE(__mul24((int)d00.x, gg.w00) + __mul24((int)d01.x, gg.w01) +
+                                         __mul24((int)d10.x, gg.w10) + __mul24((int)d11.x, gg.w11), 14);
+                int iy = PSN_DESCALE(__mul24((int)d00.y, gg.w00) + __mul24((int)d01.y, gg.w01) +
+                                         __mul24((int)d10.y, gg.w10) + __mul24((int)d11.y, gg.w11), 14);
+                if (v) IW[i] = make_int2(iw, (ix & 0xffff) | (iy << 16));
+                ix = v ? ix : 0;
+                iy = v ? iy : 0;
+                const int xx2 = __mul24(ix, ix), xy = __mul24(ix, iy), yy2 = __mul24(iy, iy);
+                const int pos = v ? posA(GA, y, x) : 4 * GA.S + GA.lenT;
+                PA[pos] = (float)xx2;
+                PA[GA.P + pos] = (float)xy;
+                PA[2 * GA.P + pos] = (float)yy2;
+                s11 += (unsigned)xx2;
+                s12 += xy;
+                s22 += (unsigned)yy2;
+            }
+            s11 = wave_sum_sat(s11);
+            s12 = wave_sum(s12);
+            s22 = wave_sum_sat(s22);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            float acc = 0.f;
+            if (lane < 15) {
+                const int sm = lane / 5, ch = lane - 5 * sm;
+                const unsigned bound = sm == 0 ? s11 : sm == 2 ? s22 : (s11 + s22) >> 1;
+                if (bound > (unsigned)kExact) {
+                    const int base = sm * GA.P + (ch < 4 ? ch * GA.S : 4 * GA.S);
+                    acc = chain_sum16(PA + base, (ch < 4 ? GA.S : GA.T) >> 4);
+                }
+            }
+            float c[15];
+#pragma unroll
+            for (int k = 0; k < 15; k++) c[k] = readlane_f(acc, k);
+            if (lane == 0)
+                st_level_table(LV + l * kStLvFloats, s11, s12, s22, c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7],
+                               c[8], c[9], c[10], c[11], c[12], c[13], c[14], sse, wh, Q.min_eig);
+        };
         LK_STAMP(54);
         bool pf_regs = true;  // the prefetched region is still in registers (prologue) vs already in LDS
         int buf = 0;
@@ -1423,6 +1522,14 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
             pf_y0 = __builtin_amdgcn_readfirstlane(cv_floor(__fsub_rn(__fmul_rn(NPy, 2.f), hwy)) - kStJMargin);
 
             if (wid != 0) {
+                if (ovl && level == maxL) {  // the finer levels' A phase: wave k takes levels maxL - k, maxL - k - 3, ...
+                    for (int l = maxL - wid; l >= 0; l -= NW - 1) a_level_wave(l);
+#ifdef PSN_LK_STAMPS
+                    unsigned long long t_s;  // wave k's A phase done: slot 59 - 10 k
+                    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_s) : : "memory");
+                    if (lane == 0 && wid < 4 && A.stamps) A.stamps[(size_t)blockIdx.x * 64 + 59 - 10 * wid] = t_s;
+#endif
+                }
                 if (level > 0) {
                     JPStage<NT> cp;
                     cp.cs = JRHc;

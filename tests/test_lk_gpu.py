@@ -283,6 +283,20 @@ def test_lk_fused_ingest_pipeline(oracle_mod, env, win):
                     np.testing.assert_array_equal(ctx.read_level((t + 1) % R, lvl), ref_l, f"pyr {t + 1} level {lvl}")
 
 
+@pytest.mark.parametrize("ml", [0, 1, 4, 5])
+def test_lk_st_overlapped_a_phase_levels(oracle_mod, ml):
+    """One-wave single-tile launches at two workgroups per CU compute the finer
+    levels' A phase on waves 1-3 beside the iterations (wave 1 takes two levels
+    from 5 levels on); bit-identical to the oracle and to the prologue-only
+    variant (st_ovl 0) at every level count."""
+    sc, f0, f1 = scene_pair(13, 3840, 2160, 200)
+    pts = sc.points_at(0)
+    ref = oracle_ref(oracle_mod, f0, f1, pts, (21, 21), ml)
+    for env in [{}, {"st_ovl": 0}]:
+        gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, (21, 21), ml, variants=env)
+        assert_same(gpu, ref, f"maxLevel {ml} {env}")
+
+
 def test_lk_config5_4k_5level(oracle_mod):
     """configs[4] shape on one GPU: 3840x2160, 4096 points, 5-level pyramid."""
     sc, f0, f1 = scene_pair(7, 3840, 2160, 4096)
@@ -292,7 +306,7 @@ def test_lk_config5_4k_5level(oracle_mod):
     assert_same(gpu, ref, "4k")
 
 
-@pytest.mark.parametrize("env", [{}, {"onewave": 0}, {"generic": 1}, {"threads": 64},
+@pytest.mark.parametrize("env", [{}, {"st_ovl": 0}, {"onewave": 0}, {"generic": 1}, {"threads": 64},
                                  {"threads": 128}, {"threads": 512},
                                  {"generic": 1, "threads": 64}])
 @pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])

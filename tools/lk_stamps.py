@@ -37,6 +37,8 @@ def main():
         ctx.push_frame(1, f1)
         rc = L.psn_lk_debug_set_stamps(ctx.handle, st.addr)
         assert rc == 0, "not a stamps build"
+        ovl = int(os.environ.get("ST_OVL", "1"))
+        L.psn_lk_debug_set_variant(ctx.handle, _lib.VARIANTS["st_ovl"], ovl)
         q = lk.make_query(0, 1, 0, npts, lk.make_params((win, win), 3))
         for _ in range(3):
             ctx.track([q], pts)
@@ -56,6 +58,10 @@ def main():
                               "j_prefetch": float((s[:, 59] - s[:, 63]).mean())}
     out["prologue_split"] = {"point_load": float((s[:, 58] - s[:, 60]).mean()), "dma_issue": float((s[:, 59] - s[:, 58]).mean()),
                              "dma_wait_barrier": float((s[:, 50] - s[:, 59]).mean())}
+    if ovl:  # waves 1-3's overlapped A phase done (slots 49, 39, 29), from the level-3 iteration start
+        out["ovl_a_done_after_l3_start"] = {f"wave{k}": round(float((s[:, 59 - 10 * k] - s[:, 31]).mean()), 1)
+                                            for k in (1, 2, 3)}
+        out["ovl_l3_iters_cycles"] = round(float((s[:, 37] - s[:, 32]).mean()), 1)
     prev_end = s[:, 53]
     for lev in range(3, -1, -1):
         b = lev * 10
