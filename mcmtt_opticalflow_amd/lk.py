@@ -30,6 +30,11 @@ def make_params(win_size=(21, 21), max_level=3, criteria=(3, 30, 0.01), flags=0,
     return p
 
 
+def query_array(queries: list[LkQuery]):
+    """The ctypes array psn_lk_track_device takes (at least one element)."""
+    return (LkQuery * max(len(queries), 1))(*queries)
+
+
 def make_query(prev_slot, next_slot, first_pt, num_pts, params: LkParams) -> LkQuery:
     q = LkQuery()
     q.prev_slot, q.next_slot, q.first_pt, q.num_pts = prev_slot, next_slot, first_pt, num_pts
@@ -148,10 +153,12 @@ class LKContext:
                                          st.ctypes.data, er.ctypes.data if er is not None else None), "track")
         return nxt, st, er
 
-    def track_device(self, queries: list[LkQuery], d_prev: int, d_next: int, d_status: int, d_err: int | None):
-        arr = (LkQuery * max(len(queries), 1))(*queries)
-        self._check(self._L.psn_lk_track_device(self._h, arr, len(queries), d_prev, d_next, d_status, d_err),
-                    "track_device")
+    def track_device(self, queries, d_prev: int, d_next: int, d_status: int, d_err: int | None):
+        """`queries`: a list of LkQuery, or a ctypes LkQuery array built once by the
+        caller (query_array) for a launch it repeats."""
+        arr = queries if isinstance(queries, ctypes.Array) else query_array(queries)
+        self._check(self._L.psn_lk_track_device(self._h, arr, len(arr) if len(queries) else 0, d_prev, d_next,
+                                                d_status, d_err), "track_device")
 
     def gridfast_detect(self, slot: int, rois, params: GridFastParams | None = None, seed: int = 0):
         """GridFAST keypoints of slot's frame masked by each roi (x, y, w, h),
