@@ -1,9 +1,9 @@
 #!/bin/bash
-# bench.py harness A/B: this tree's bench.py vs the previous one (tools/bench_prev.py.txt), same library.
+# bench.py harness A/B: this tree's bench.py vs bench_prev.py (copy an earlier bench.py there first), same library.
 set -e -o pipefail
 O=gpurun_out/bab
 mkdir -p $O
-cp tools/bench_prev.py.txt bench_prev.py
+test -f bench_prev.py
 for r in 1 2 3; do
   for V in bench bench_prev; do
     timeout -k 10 200 python $V.py --mode kernel --steps 300 --no-cpu-baseline --no-secondary --no-legs > $O/${V}_$r.json 2>$O/${V}_$r.err
