@@ -228,6 +228,8 @@ int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *
  *   PSN_LK_VARIANT_ST_OVL      0 = the single-tile kernel computes every level's A phase
  *                              in its prologue (1: waves 1-3 compute the finer levels'
  *                              beside wave 0's iterations when the layout fits)
+ *   PSN_LK_VARIANT_POISON_LDS  1 = single-tile launches fill their LDS with pseudo-random
+ *                              words first (tests: a read of unwritten LDS shows up)
  * Queries are split into one launch per window class (single-tile / box kernel
  * per units-per-thread and tail build / row-tiled / large), each sized for its
  * own windows. */
@@ -241,6 +243,7 @@ int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *
 #define PSN_LK_VARIANT_LG_LDS 8
 #define PSN_LK_VARIANT_LG_JR 9
 #define PSN_LK_VARIANT_ST_OVL 10
+#define PSN_LK_VARIANT_POISON_LDS 11
 int psn_lk_debug_set_variant(psn_lk_ctx *ctx, int key, int value);
 
 /* Window-sample counter (SURVEY 8(d)'s compute figure): while on, every box-

@@ -40,7 +40,7 @@ MAX_WIN_WIDTH = 6400  # PSN_LK_MAX_WIN_WIDTH (any window height)
 COMM_UNIQUE_ID_BYTES = 128
 # psn_lk_debug_set_variant keys (tests / experiments; never read from the environment)
 VARIANTS = {"threads": 1, "generic": 2, "onewave": 3, "box": 4, "tiled_lds": 5, "fused_helpers": 6,
-            "large": 7, "lg_lds": 8, "lg_jr": 9, "st_ovl": 10}
+            "large": 7, "lg_lds": 8, "lg_jr": 9, "st_ovl": 10, "poison_lds": 11}
 
 
 class PsnLkError(RuntimeError):

@@ -101,7 +101,11 @@ struct psn_lk_ctx {
     int force_threads = 0;
     bool force_generic = false;
     bool onewave = true;  // ONEWAVE 0: multi-wave iterations in the single-tile kernel
-    bool st_ovl = true;   // ST_OVL 0: every level's A phase in the single-tile prologue
+#ifndef PSN_ST_OVL_DEFAULT
+#define PSN_ST_OVL_DEFAULT 1
+#endif
+    bool st_ovl = PSN_ST_OVL_DEFAULT != 0;  // ST_OVL 0: every level's A phase in the single-tile prologue
+    bool poison_lds = false;                 // POISON_LDS 1: single-tile launches fill their LDS with a pattern first
     bool box = true;      // BOX 0: box windows run the row-tiled kernel instead of lk_kernel_bx
     // TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
     // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
@@ -1054,6 +1058,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
             fused_slot = c->pend_slot;
             builds = true;
         }
+        a.poison_lds = c->poison_lds ? lds : 0;
         HIPCHK(c, psn::launch_lk(a, wgs, threads, lds, true, c->stream));
         return builds ? mark_fused_build(c, fused_slot) : PSN_LK_OK;
     }
@@ -1320,6 +1325,7 @@ int psn_lk_debug_set_variant(psn_lk_ctx *c, int key, int value) {
     case PSN_LK_VARIANT_LG_LDS: c->lg_lds = std::max(4 * 1024, std::min(value, 160 * 1024 - 1024)); return PSN_LK_OK;
     case PSN_LK_VARIANT_LG_JR: c->lg_jr = value != 0; return PSN_LK_OK;
     case PSN_LK_VARIANT_ST_OVL: c->st_ovl = value != 0; return PSN_LK_OK;
+    case PSN_LK_VARIANT_POISON_LDS: c->poison_lds = value != 0; return PSN_LK_OK;
     default: return PSN_LK_ERR_ARG;
     }
 }

@@ -78,7 +78,7 @@ struct LkLaunchArgs {
     unsigned long long *stamps;  // diagnostic build only (PSN_LK_STAMPS): [wg][64] s_memtime
     unsigned long long *samples; // optional: += sum over levels of w*h*(1 + iterations) per point
     int nq;
-    int pad_;
+    int poison_lds;          // debug (PSN_LK_VARIANT_POISON_LDS): bytes of dynamic LDS the kernel fills with a pattern first
     // optional per-query point counts on the device (<= num_pts, the grid
     // capacity): workgroups past a query's count exit at once (device-side
     // chains whose counts come from a previous kernel)

@@ -1021,6 +1021,17 @@ __device__ __forceinline__ void pyr_tail(const LkLaunchArgs &A, uint8_t *smem) {
     }
 }
 
+// Debug (PSN_LK_VARIANT_POISON_LDS): fill `bytes` of dynamic LDS with 24-bit
+// pseudo-random words before the kernel uses it, so a read of LDS the kernel never
+// wrote sees the same adversarial values on every run instead of what earlier
+// kernels left there.
+template <int NT>
+__device__ __forceinline__ void lds_poison(uint8_t *smem, int bytes) {
+    unsigned *p = (unsigned *)smem;
+    for (int i = threadIdx.x; i < bytes / 4; i += NT) p[i] = ((unsigned)i * 2654435761u) >> 8;
+    __syncthreads();
+}
+
 // Solver table of one level from the A sums (a11, a22 saturating, s12 wrapping)
 // and the 15 ordered chain sums c (sum s = 0..2: chains 5s..5s+3 the SSE2 lanes,
 // 5s+4 the tail; used only when the sum is not exact as an integer):
@@ -1068,6 +1079,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = blockIdx.x;
+    if (A.poison_lds) lds_poison<NT>(smem, A.poison_lds);
     if (A.pyr_ntiles > 0 && g >= A.lk_wgs) {  // fused-build helper: tiles only
         pyr_tail<NT>(A, smem);
         return;
@@ -1355,9 +1367,15 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
         const int lane_off = colx * JRHc + oy0;
         // class c occupies lanes (last[c-1], last[c]]; empty classes repeat the previous bound
         const int last4 = w * G - 1;
-        // this lane ends class cls_end (it publishes the class's scans), or -1
+        // this lane ends class cls_end (it publishes the class's scans), or -1; with
+        // no tail columns (w % 8 == 0) the last lane ends class 3 and the empty class
+        // 4 alike and publishes both (class 4's sums are then 0)
         int cls_end = -1;
-        if (lane == last4) cls_end = 4;
+        bool end3 = false;
+        if (lane == last4) {
+            cls_end = 4;
+            end3 = n8 > 0 && n8 == w;
+        }
         if (n8 > 0)
             for (int c = 0; c < 4; c++)
                 if (lane == (c + 1) * cw * G - 1 && lane != last4) cls_end = c;
@@ -1650,6 +1668,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
                         a1 = (unsigned)wave_scan((int)a1);
                         a2 = (unsigned)wave_scan((int)a2);
                         if (cls_end >= 0) CSX[cls_end] = make_int4(c1, c2, (int)a1, (int)a2);
+                        if (end3) CSX[3] = make_int4(c1, c2, (int)a1, (int)a2);
                         int S1[5], S2[5];
                         bool exact = true;
                         int4 pv = make_int4(0, 0, 0, 0);

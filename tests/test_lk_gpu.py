@@ -292,9 +292,23 @@ def test_lk_st_overlapped_a_phase_levels(oracle_mod, ml):
     sc, f0, f1 = scene_pair(13, 3840, 2160, 200)
     pts = sc.points_at(0)
     ref = oracle_ref(oracle_mod, f0, f1, pts, (21, 21), ml)
-    for env in [{}, {"st_ovl": 0}]:
+    for env in [{}, {"st_ovl": 0}, {"poison_lds": 1}]:
         gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, (21, 21), ml, variants=env)
         assert_same(gpu, ref, f"maxLevel {ml} {env}")
+
+
+@pytest.mark.parametrize("win", [(24, 24), (16, 40), (32, 32), (24, 16), (21, 21), (9, 15)])
+def test_lk_st_unwritten_lds_never_read(oracle_mod, win):
+    """With the single-tile launch's LDS filled with pseudo-random words first
+    (PSN_LK_VARIANT_POISON_LDS), every window shape -- widths that are multiples
+    of 8 (no SSE2 tail class) included -- gives the oracle's bits in both A-phase
+    modes: no path reads LDS it did not write."""
+    sc, f0, f1 = scene_pair(14, 640, 480, 160)
+    pts = sc.points_at(0)
+    ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3)
+    for env in [{"poison_lds": 1}, {"poison_lds": 1, "st_ovl": 0}]:
+        gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, variants=env)
+        assert_same(gpu, ref, f"{win} {env}")
 
 
 def test_lk_config5_4k_5level(oracle_mod):
@@ -306,7 +320,8 @@ def test_lk_config5_4k_5level(oracle_mod):
     assert_same(gpu, ref, "4k")
 
 
-@pytest.mark.parametrize("env", [{}, {"st_ovl": 0}, {"onewave": 0}, {"generic": 1}, {"threads": 64},
+@pytest.mark.parametrize("env", [{}, {"st_ovl": 0}, {"poison_lds": 1}, {"poison_lds": 1, "st_ovl": 0},
+                                 {"poison_lds": 1, "onewave": 0}, {"onewave": 0}, {"generic": 1}, {"threads": 64},
                                  {"threads": 128}, {"threads": 512},
                                  {"generic": 1, "threads": 64}])
 @pytest.mark.parametrize("flags", [0, ACCUM_SCALAR])
