@@ -228,8 +228,9 @@ int psn_lk_timing_launches(psn_lk_ctx *ctx, int cap, double *ms, int *tag, int *
  *   PSN_LK_VARIANT_ST_OVL      0 = the single-tile kernel computes every level's A phase
  *                              in its prologue (1: waves 1-3 compute the finer levels'
  *                              beside wave 0's iterations when the layout fits)
- *   PSN_LK_VARIANT_POISON_LDS  1 = single-tile launches fill their LDS with pseudo-random
- *                              words first (tests: a read of unwritten LDS shows up)
+ *   PSN_LK_VARIANT_POISON_LDS  1 = LK launches (single-tile, box, large) fill their LDS
+ *                              with pseudo-random words first (tests: a read of unwritten
+ *                              LDS shows up)
  * Queries are split into one launch per window class (single-tile / box kernel
  * per units-per-thread and tail build / row-tiled / large), each sized for its
  * own windows. */

@@ -105,7 +105,7 @@ struct psn_lk_ctx {
 #define PSN_ST_OVL_DEFAULT 1
 #endif
     bool st_ovl = PSN_ST_OVL_DEFAULT != 0;  // ST_OVL 0: every level's A phase in the single-tile prologue
-    bool poison_lds = false;                 // POISON_LDS 1: single-tile launches fill their LDS with a pattern first
+    bool poison_lds = false;                 // POISON_LDS 1: LK launches fill their LDS with a pattern first
     bool box = true;      // BOX 0: box windows run the row-tiled kernel instead of lk_kernel_bx
     // TILED_LDS: LDS budget of a tiled-kernel workgroup (bytes); 76 KB keeps two
     // workgroups per CU (Tracker2D box windows: 64x64 backward, 64x160 forward at 1080p)
@@ -1075,6 +1075,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
                 d.bx_hw++;
             lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt, d.bx_hw).total);
         }
+        a.poison_lds = c->poison_lds ? lds_bx : 0;
         HIPCHK(c, psn::launch_lk_bx(a, wgs, upt, notail, lds_bx, c->stream));
         return PSN_LK_OK;
     }
@@ -1105,6 +1106,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
     a.lg_slot = slot;
     a.lk_wgs = wgs;
     a.total_wgs = wgs;
+    a.poison_lds = c->poison_lds ? lds : 0;
     HIPCHK(c, psn::launch_lk_lg(a, grid, lds, key, c->stream));
     for (auto &e : c->lg_ws)
         if (e.s == c->stream) {

@@ -411,6 +411,15 @@ __device__ __forceinline__ void dma_rows(uint8_t *dst, const LevelDev &L, int gy
     }
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Debug (PSN_LK_VARIANT_POISON_LDS): fill `bytes` of dynamic LDS with 24-bit
+// pseudo-random words before the kernel uses it, so a read of LDS the kernel never
+// wrote sees the same values on every run instead of what earlier kernels left.
+template <int NT>
+__device__ __forceinline__ void lds_poison(uint8_t *smem, int bytes) {
+    unsigned *p = (unsigned *)smem;
+    for (int i = threadIdx.x; i < bytes / 4; i += NT) p[i] = ((unsigned)i * 2654435761u) >> 8;
+    __syncthreads();
+}
 // A workgroup barrier that leaves vector-memory loads in flight (__syncthreads'
 // fence would wait for them): every thread's LDS data it orders was already
 // waited for (dma_wait / lgkmcnt) by the thread that wrote it. The empty asm

@@ -1021,17 +1021,6 @@ __device__ __forceinline__ void pyr_tail(const LkLaunchArgs &A, uint8_t *smem) {
     }
 }
 
-// Debug (PSN_LK_VARIANT_POISON_LDS): fill `bytes` of dynamic LDS with 24-bit
-// pseudo-random words before the kernel uses it, so a read of LDS the kernel never
-// wrote sees the same adversarial values on every run instead of what earlier
-// kernels left there.
-template <int NT>
-__device__ __forceinline__ void lds_poison(uint8_t *smem, int bytes) {
-    unsigned *p = (unsigned *)smem;
-    for (int i = threadIdx.x; i < bytes / 4; i += NT) p[i] = ((unsigned)i * 2654435761u) >> 8;
-    __syncthreads();
-}
-
 // Solver table of one level from the A sums (a11, a22 saturating, s12 wrapping)
 // and the 15 ordered chain sums c (sum s = 0..2: chains 5s..5s+3 the SSE2 lanes,
 // 5s+4 the tail; used only when the sum is not exact as an integer):
@@ -2087,6 +2076,7 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
     static_assert(UPT % 2 == 0, "units are processed in pairs");
     constexpr int NT = kBxNT;
     const int tid = threadIdx.x, lane = tid & 63;
+    if (A.poison_lds) lds_poison<NT>(smem, A.poison_lds);
     const int g = xcd_remap((int)blockIdx.x, (int)gridDim.x);
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;

@@ -273,6 +273,7 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int NT = kLgNT;
     const int tid = threadIdx.x, lane = tid & 63;
+    if (A.poison_lds) lds_poison<NT>(smem, A.poison_lds);
     int *X = (int *)smem;                 // chain-check records, two parities
     float *RS = (float *)(X + kBxXInts);  // results (wave 0 -> all), err partials
     int *EP = (int *)(RS + 16);

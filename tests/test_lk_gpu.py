@@ -483,6 +483,21 @@ def test_lk_large_kernel_all_shapes(oracle_mod, lg_lds, jr, flags):
         assert_same(gpu, ref, f"{env} {win}")
 
 
+@pytest.mark.parametrize("win,flags,env", [((37, 50), 0, {}), ((64, 160), 0, {}), ((64, 64), ACCUM_SCALAR, {}),
+                                           ((45, 120), 0, {}), ((100, 250), 0, {}), ((130, 130), 0, {"lg_jr": 0}),
+                                           ((111, 277), GET_MIN_EIGENVALS, {}), ((64, 64), 0, {"large": 1}),
+                                           ((33, 33), ACCUM_SCALAR, {"large": 1})])
+def test_lk_box_and_large_unwritten_lds_never_read(oracle_mod, win, flags, env):
+    """The box and large-window kernels with their LDS filled with pseudo-random
+    words first (PSN_LK_VARIANT_POISON_LDS): the oracle's bits -- no path reads
+    LDS it did not write (pads, tile ends, record slots, J regions)."""
+    sc, f0, f1 = scene_pair(17, 1920, 1080, 24, box_w=win[0], box_h=win[1])
+    pts = np.concatenate([sc.points_at(0), BORDER_PTS_1080])
+    ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
+    gpu = glk.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags, variants={"poison_lds": 1, **env})
+    assert_same(gpu, ref, f"poisoned LDS win {win} flags {flags} {env}")
+
+
 def test_lk_large_err_sequential_path(oracle_mod):
     """Uncorrelated frames and a 160 x 160 window: sum|diff| > 2^24, so err takes
     the ordered chain of the large-window kernel; b and A chains as well."""
