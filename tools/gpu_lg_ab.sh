@@ -1,24 +1,22 @@
 #!/bin/bash
-# Large-window kernel build variants (var_libs/<name>/): isolated launches of
-# PETS-scale windows at 128 and 512 points, then the PETS-box bench line.
+# large-window kernel A/B: parity (large-window + poison tests), isolated launch times and
+# the PETS leg of this tree vs var_libs/$1, alternating twice
 set -e -o pipefail
+B=${1:-head}
 R=$(pwd)
-Q="--no-cpu-baseline --no-secondary --no-legs --no-isolated"
-O=gpurun_out/lg_ab
+O=gpurun_out/lgab
 mkdir -p $O
-for V in base ${VARIANTS:-jr100 tq192 tq64}; do
-  L=mcmtt_opticalflow_amd/lib/libpsn_lk.so
-  [ $V != base ] && L=var_libs/$V/libpsn_lk.so
-  for P in 128 512; do
-    timeout -k 10 200 python tools/bx_time.py --points $P --reps 8 --shapes 100x250,130x130,150x375,140x357 --lib $L > $O/t_${V}_$P.json
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_lk_gpu.py -m gpu \
+  -k "large or unwritten" > $O/test.log 2>&1
+tail -1 $O/test.log
+D=/tmp/v_$B; rm -rf $D; mkdir -p $D
+tar --exclude=./gpurun_out --exclude=./build --exclude=./var_libs -cf - . | tar -xf - -C $D
+cp var_libs/$B/libpsn_lk.so $D/mcmtt_opticalflow_amd/lib/
+for r in 1 2; do
+  for V in new $B; do
+    if [ $V = new ]; then W=$R; else W=$D; fi
+    (cd $W && timeout -k 10 200 python tools/bx_time.py --points 512 --reps 8 --shapes 100x250,130x130,150x375,140x357 > $R/$O/t_${V}_$r.json 2>$R/$O/t_${V}_$r.err)
+    (cd $W && timeout -k 10 300 python bench.py --box-dist pets --steps 40 --warmup 5 --no-cpu-baseline --no-secondary --no-legs --no-isolated > $R/$O/p_${V}_$r.json 2>$R/$O/p_${V}_$r.err)
+    echo "$V run $r: pets $(python -c "import json;d=json.loads(open('$O/p_${V}_$r.json').read().strip().splitlines()[-1]);print(d['value'])") lg $(python -c "import json;d=json.load(open('$O/t_${V}_$r.json'));print({k:v['median_us'] for k,v in d.items() if isinstance(v,dict) and 'median_us' in v})")"
   done
-  echo "variant $V timed"
 done
-for V in base ${VARIANTS:-jr100 tq192 tq64}; do
-  D=/tmp/v_$V; rm -rf $D; mkdir -p $D
-  tar --exclude=./gpurun_out --exclude=./build -cf - . | tar -xf - -C $D
-  [ $V != base ] && cp var_libs/$V/*.so $D/mcmtt_opticalflow_amd/lib/
-  (cd $D && timeout -k 10 200 python bench.py --steps 40 --box-dist pets $Q > $R/$O/pets_$V.json 2>/dev/null)
-  echo "variant $V benched"
-done
-echo done
