@@ -38,7 +38,7 @@ static int g_chain_upt = 0;
 /* the per-thread parity-record model on every fallback evaluation (buf[16..21]:
  * the caller's buffer holds 24 entries) */
 static int g_chain_log_ext = 0;
-static int g_chain_fs = 256;
+static int g_chain_fs = 256, g_chain_ls = -1;
 static float g_chain_ser[10];
 static float *g_chain_terms[10];
 static int g_chain_off[10][257];
@@ -114,6 +114,21 @@ static void chain_classify(const long long *t1, const long long *t2, int w, int 
                 if (M > (1LL << 24) || m < -(1LL << 24)) fs = t;
             }
             if (fs < g_chain_fs) g_chain_fs = fs;
+            {   /* [22] last thread whose run leaves |prefix| <= 2^24 - 2^16 (max over chains) */
+                int ls = -1;
+                long long Pr = 0;
+                for (int t = 0; t < 256; t++) {
+                    long long M = Pr, m = Pr;
+                    for (int i = off[t]; i < off[t + 1]; i++) {
+                        Pr += (long long)f[i];
+                        if (Pr > M) M = Pr;
+                        if (Pr < m) m = Pr;
+                        if (fabsf(f[i]) > 16777216.f) M = 1LL << 30;
+                    }
+                    if (M > (1LL << 24) - (1LL << 16) || m < -((1LL << 24) - (1LL << 16))) ls = t;
+                }
+                if (ls > g_chain_ls) g_chain_ls = ls;
+            }
             g_chain_ser[cc] = ser;
             memcpy(g_chain_terms[cc], f, sizeof(float) * (size_t)n);
             memcpy(g_chain_off[cc], off, sizeof(off));
@@ -188,8 +203,22 @@ static void chain_classify(const long long *t1, const long long *t2, int w, int 
         }
         g_chain_log[17] += walk_max;
         g_chain_log[20] += ser_max;
+        {   /* [22] serial terms of the longest chain from the first failing thread to the
+             * end of the last one whose run leaves a prefix above 2^24 - 2^16, [23] threads
+             * from the first to that last failing one, [24] threads from the first to the end */
+            int cut_max = 0;
+            for (int cc = 0; cc < 10; cc++) {
+                const int *oc = g_chain_off[cc];
+                const int e = g_chain_ls + 1 > fs ? g_chain_ls + 1 : fs;
+                if (oc[e] - oc[fs] > cut_max) cut_max = oc[e] - oc[fs];
+            }
+            g_chain_log[22] += cut_max;
+            g_chain_log[23] += g_chain_ls + 1 - fs;
+            g_chain_log[24] += 256 - fs;
+        }
     }
     g_chain_fs = 256;
+    g_chain_ls = -1;
     free(f);
     g_chain_log[0]++;
     g_chain_log[2] += mismatch;

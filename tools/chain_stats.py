@@ -29,7 +29,9 @@ from mcmtt_opticalflow_amd import synth  # noqa: E402
 
 KEYS = ["evals", "fast_path", "mismatch", "walk_sum", "walk_max", "records", "hard_segs", "hard_terms",
         "max_wave_records", "max_wave_hard", "fallback_evals",
-        "suffix_terms", "suffix_exact_steps", "suffix_exact_in_blocks16"]
+        "suffix_terms", "suffix_exact_steps", "suffix_exact_in_blocks16",
+        "u14", "u15", "fb_evals", "walk_sum2", "walk_abort", "walk_mismatch", "serial_from_first", "hard_terms2",
+        "serial_first_to_last", "threads_first_to_last", "threads_first_to_end"]
 
 
 def main():
@@ -38,7 +40,7 @@ def main():
     W, H, npts, nboxes, period = 1920, 1080, 512, 8, 10
     sc = synth.make_scene(0, W, H, npts, nboxes=nboxes)
     L = oracle.lib()
-    buf = (ctypes.c_longlong * 24)()
+    buf = (ctypes.c_longlong * 32)()
     L.oracle_set_chain_log.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.oracle_set_chain_log(ctypes.addressof(buf), upt)
     T2.NTHREADS = 1
