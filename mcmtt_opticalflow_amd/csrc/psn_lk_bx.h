@@ -237,16 +237,22 @@ __device__ __forceinline__ int cw_dot(unsigned ip, unsigned k, int c) {
 // bilinear with the diff folded into the accumulator constant 256 - 512 I
 // (I = the unit's window values, packed pairs ip; one v_dot2 each with the
 // selector pairs (-512, 0) / (0, -512) and c256 = 256).
-__device__ __forceinline__ void bx_diffs(const uint32_t *jp, int JRP4, unsigned W0, unsigned W1, unsigned s0,
-                                         unsigned s1, unsigned s2, unsigned s3, const unsigned (&ip)[2], int (&d)[4],
-                                         int c256) {
-    const uint32_t a0 = jp[0], a1 = jp[1], b0 = jp[JRP4], b1 = jp[JRP4 + 1];
+// (rows as two pointers: jp and jq = jp + JRP4)
+__device__ __forceinline__ void bx_diffs2(const uint32_t *jp, const uint32_t *jq, unsigned W0, unsigned W1, unsigned s0,
+                                          unsigned s1, unsigned s2, unsigned s3, const unsigned (&ip)[2], int (&d)[4],
+                                          int c256) {
+    const uint32_t a0 = jp[0], a1 = jp[1], b0 = jq[0], b1 = jq[1];
     const unsigned kl = 0x0000fe00u, kh = 0xfe000000u;  // (-512, 0), (0, -512)
     const int cw[4] = {cw_dot(ip[0], kl, c256), cw_dot(ip[0], kh, c256), cw_dot(ip[1], kl, c256), cw_dot(ip[1], kh, c256)};
     d[0] = sdot2(__builtin_amdgcn_perm(b1, b0, s0), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s0), W0, cw[0])) >> 9;
     d[1] = sdot2(__builtin_amdgcn_perm(b1, b0, s1), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s1), W0, cw[1])) >> 9;
     d[2] = sdot2(__builtin_amdgcn_perm(b1, b0, s2), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s2), W0, cw[2])) >> 9;
     d[3] = sdot2(__builtin_amdgcn_perm(b1, b0, s3), W1, sdot2(__builtin_amdgcn_perm(a1, a0, s3), W0, cw[3])) >> 9;
+}
+__device__ __forceinline__ void bx_diffs(const uint32_t *jp, int JRP4, unsigned W0, unsigned W1, unsigned s0,
+                                         unsigned s1, unsigned s2, unsigned s3, const unsigned (&ip)[2], int (&d)[4],
+                                         int c256) {
+    bx_diffs2(jp, jp + JRP4, W0, W1, s0, s1, s2, s3, ip, d, c256);
 }
 // pair selector: bytes (sj + i, sj + i + 1) of a row's 8-byte window -> J[x] | J[x+1] << 16
 __device__ __forceinline__ unsigned bx_sel(int sj, int i) {

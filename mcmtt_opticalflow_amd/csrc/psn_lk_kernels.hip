@@ -2374,7 +2374,49 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
                     return first ? r[0] : r[1];
                 };
+                // no-tail build: the tile's half picked at compile time, the unit's plane
+                // slot from its index in the tile (as the b fallback's write_tile_nt)
+                auto writeA_nt = [&](int g, float *buf, auto lowerT) {
+                    constexpr bool lower = decltype(lowerT)::value;
+                    if ((ftid >> 6) != (g >> 1)) return;
+                    int sa, ta, nsse, ntail;
+                    geoA(g, sa, ta, nsse, ntail);
+                    const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                    const bool up = (ftid & 32) != 0;
+                    const int ub = lower ? (up ? (ftid ^ 32) * UPT + K1 : ftid * UPT) : (up ? ftid * UPT + K1 : (ftid ^ 32) * UPT);
+                    const int rel = ub - 32 * UPT * g;
+                    auto pick = [](unsigned a, unsigned b) {
+                        auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+                        return lower ? r[0] : r[1];
+                    };
+#pragma unroll
+                    for (int k = 0; k < K1; k++) {
+                        unsigned xp[2] = {pick(XP[k][0], XP[K1 + k][0]), pick(XP[k][1], XP[K1 + k][1])};
+                        unsigned yp[2] = {pick(YP[k][0], YP[K1 + k][0]), pick(YP[k][1], YP[K1 + k][1])};
+                        if (ub + k < U) {
+                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
+                            float *d1 = buf + rel + k;
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                                const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                                d1[i * S] = (float)__mul24(gx, gx);
+                                d1[i * S + P] = (float)__mul24(gx, gy);
+                                d1[i * S + 2 * P] = (float)__mul24(gy, gy);
+                            }
+                        }
+                    }
+                };
                 auto writeA = [&](int g, float *buf) {
+                    if constexpr (NOTAIL) {
+                        if (HW == 1) {  // (split: UPT is even)
+                            if (g & 1)
+                                writeA_nt(g, buf, std::false_type());
+                            else
+                                writeA_nt(g, buf, std::true_type());
+                            return;
+                        }
+                    }
                     int sa, ta, nsse, ntail;
                     if (split) {
                         if ((ftid >> 6) != (g >> 1)) return;
@@ -2508,7 +2550,12 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
             // below that in the whole wave, the pass keeps no max |d|
             const bool dtrack = __ballot(gmax > kExact / 8160) != 0ull;
             auto bmain = [&](auto trk) {
-                const uint8_t *jb = (const uint8_t *)(JR32 + oy * JRP4 + (ox >> 2));  // the iteration's base
+                // the iteration's byte offsets of rows oy and oy + 1 in LDS, opaque
+                // scalars (the J region's constant offset stays inside them: one
+                // SDWA add per row and unit, not two adds and a constant)
+                unsigned jo0 = (unsigned)((const uint8_t *)(JR32 + oy * JRP4 + (ox >> 2)) - smem);
+                unsigned jo1 = jo0 + 4u * (unsigned)JRP4;
+                asm volatile("" : "+s"(jo0), "+s"(jo1));
                 // units in pairs (UPT is even): each chain takes its two terms by
                 // v_mad_i32_i16 (gradient half, product and sum in one) and one
                 // v_max3 / v_min3 of the two new prefixes
@@ -2519,7 +2566,8 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
 #pragma unroll
                     for (int u = 0; u < 2; u++) {
                         const unsigned o = u ? UB[k >> 1] >> 16 : UB[k >> 1] & 0xffffu;
-                        bx_diffs((const uint32_t *)(jb + o), JRP4, W0, W1, s0, s1, s2, s3, IP[k + u], d[u], c256);
+                        bx_diffs2((const uint32_t *)(smem + jo0 + o), (const uint32_t *)(smem + jo1 + o), W0, W1, s0, s1, s2,
+                                  s3, IP[k + u], d[u], c256);
                         ms[u] = -(int)((sseB >> (k + u)) & 1u);  // SSE2 unit -> lane chains 0-3, else the tail chain
                     }
                     if constexpr (decltype(trk)::value) {
@@ -2727,6 +2775,50 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                         }
                     }
                 };
+                // No-tail build, half-wave tiles: the unit's J dwords from its packed
+                // offset (UB, swapped like the window values) and its plane slot from its
+                // index in the tile (every quad is an SSE2 quad, every pixel inside the
+                // window); the tile's half picked at compile time (no select per value)
+                unsigned fo0 = (unsigned)((const uint8_t *)(JR32 + oy * JRP4 + (ox >> 2)) - smem);
+                unsigned fo1 = fo0 + 4u * (unsigned)JRP4;
+                asm volatile("" : "+s"(fo0), "+s"(fo1));
+                auto write_tile_nt = [&](int g, float *buf, auto lowerT) {
+                    constexpr bool lower = decltype(lowerT)::value;
+                    const int zf = opaque256();
+                    int sa, ta, nsse, ntail;
+                    tile_geo(g, sa, ta, nsse, ntail);
+                    const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                    const bool up = (ftid & 32) != 0;
+                    // lower tile: lane l < 32 its unit k, lane l + 32 lane l's unit K1 + k;
+                    // upper tile: lane l < 32 lane l + 32's unit k, lane l + 32 its unit K1 + k
+                    const int ub = lower ? (up ? (ftid ^ 32) * UPT + K1 : ftid * UPT) : (up ? ftid * UPT + K1 : (ftid ^ 32) * UPT);
+                    const int rel = ub - 32 * UPT * g;
+                    auto pick = [](unsigned a, unsigned b) {
+                        auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+                        return lower ? r[0] : r[1];
+                    };
+                    auto uoff = [&](int k) { return (k & 1) ? UB[k >> 1] >> 16 : UB[k >> 1] & 0xffffu; };
+#pragma unroll
+                    for (int k = 0; k < K1; k++) {
+                        const unsigned ip[2] = {pick(IP[k][0], IP[K1 + k][0]), pick(IP[k][1], IP[K1 + k][1])};
+                        const unsigned xp[2] = {pick(XP[k][0], XP[K1 + k][0]), pick(XP[k][1], XP[K1 + k][1])};
+                        const unsigned yp[2] = {pick(YP[k][0], YP[K1 + k][0]), pick(YP[k][1], YP[K1 + k][1])};
+                        const unsigned off = pick(uoff(k), uoff(K1 + k));
+                        if (ub + k < U) {
+                            int d[4];
+                            bx_diffs2((const uint32_t *)(smem + fo0 + off), (const uint32_t *)(smem + fo1 + off), W0, W1, s0,
+                                      s1, s2, s3, ip, d, zf);
+                            float *d1 = buf + rel + k;
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                                const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                                d1[i * S] = (float)__mul24(d[i], gx);
+                                d1[i * S + P] = (float)__mul24(d[i], gy);
+                            }
+                        }
+                    }
+                };
                 auto pad_tile = [&](int g, float *buf) {  // chain lanes: zero their region's pad
                     if (!chl) return;
                     int sa, ta, nsse, ntail;
@@ -2758,7 +2850,14 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     for (int g = max(h0, 2 * wv); g <= min(2 * wv + 1, g_last); g++) {
                         const int b = (g - h0) % 3;
                         if (g - h0 >= 3) spin(3 + b, tag(g - 3));
-                        write_tile(g, PL + b * 2 * PC);
+                        if constexpr (NOTAIL) {
+                            if (g & 1)
+                                write_tile_nt(g, PL + b * 2 * PC, std::false_type());
+                            else
+                                write_tile_nt(g, PL + b * 2 * PC, std::true_type());
+                        } else {
+                            write_tile(g, PL + b * 2 * PC);
+                        }
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                         if (fl == 0) FLG[b] = tag(g);
                     }
