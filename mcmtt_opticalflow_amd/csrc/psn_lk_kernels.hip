@@ -2440,6 +2440,25 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     if ((ftid >> 5) < g || (ftid >> 5) >= g + HW) return;
                     geoA(g, sa, ta, nsse, ntail);
                     const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                    if constexpr (NOTAIL && UPT <= 8) {  // the thread's own units, slots from their index
+                        const int rel = u0 - 32 * UPT * g;
+#pragma unroll
+                        for (int k = 0; k < UPT; k++) {
+                            if (u0 + k >= U) break;
+                            unsigned xp[2] = {XP[k][0], XP[k][1]}, yp[2] = {YP[k][0], YP[k][1]};
+                            asm volatile("" : "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]), "+v"(yp[1]));
+                            float *d1 = buf + rel + k;
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                                const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                                d1[i * S] = (float)__mul24(gx, gx);
+                                d1[i * S + P] = (float)__mul24(gx, gy);
+                                d1[i * S + 2 * P] = (float)__mul24(gy, gy);
+                            }
+                        }
+                        return;
+                    }
                     int yk = y0, qk = q0;
                     asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
@@ -2764,6 +2783,34 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunc
                     if ((ftid >> 5) < g || (ftid >> 5) >= g + HW) return;
                     tile_geo(g, sa, ta, nsse, ntail);
                     const int S = bx_region(nsse), P = 4 * S + bx_region(ntail);
+                    if constexpr (NOTAIL && UPT <= 8) {  // the thread's own units: offsets from UB, slots from their index
+                        unsigned fo0 = (unsigned)((const uint8_t *)(JR32 + oy * JRP4 + (ox >> 2)) - smem);
+                        unsigned fo1 = fo0 + 4u * (unsigned)JRP4;
+                        asm volatile("" : "+s"(fo0), "+s"(fo1));
+                        const int rel = u0 - 32 * UPT * g;
+#pragma unroll
+                        for (int k = 0; k < UPT; k++) {
+                            if (u0 + k >= U) break;
+                            // opaque copies: nothing of the unit is hoisted out of the tile loop
+                            unsigned ubk = UB[k >> 1], ip[2] = {IP[k][0], IP[k][1]}, xp[2] = {XP[k][0], XP[k][1]},
+                                     yp[2] = {YP[k][0], YP[k][1]};
+                            asm volatile("" : "+v"(ubk), "+v"(ip[0]), "+v"(ip[1]), "+v"(xp[0]), "+v"(xp[1]), "+v"(yp[0]),
+                                         "+v"(yp[1]));
+                            const unsigned off = (k & 1) ? ubk >> 16 : ubk & 0xffffu;
+                            int d[4];
+                            bx_diffs2((const uint32_t *)(smem + fo0 + off), (const uint32_t *)(smem + fo1 + off), W0, W1, s0,
+                                      s1, s2, s3, ip, d, zf);
+                            float *d1 = buf + rel + k;
+#pragma unroll
+                            for (int i = 0; i < 4; i++) {
+                                const int gx = (i & 1) ? hi16(xp[i >> 1]) : lo16(xp[i >> 1]);
+                                const int gy = (i & 1) ? hi16(yp[i >> 1]) : lo16(yp[i >> 1]);
+                                d1[i * S] = (float)__mul24(d[i], gx);
+                                d1[i * S + P] = (float)__mul24(d[i], gy);
+                            }
+                        }
+                        return;
+                    }
                     int yk = y0, qk = q0;
                     asm volatile("" : "+v"(yk), "+v"(qk));
 #pragma unroll
