@@ -301,44 +301,30 @@ def detection_extra(b):
     return head, loc, 1700.0
 
 
-def pinned_allocator(kind="torch"):
-    """Pinned host buffers (uint8 numpy arrays): torch's pin_memory (default), or
-    (diagnostic --host-alloc) hipHostMalloc straight from the HIP runtime
-    ("hip", "hip-coherent") or page-aligned numpy memory registered with
-    hipHostRegister ("register")."""
-    import torch
+def pinned_allocator(kind="hip"):
+    """Pinned host buffers (uint8 numpy arrays) from the library's HIP runtime
+    (mcmtt_opticalflow_amd/hip.py): hipHostMalloc (default, "hip"; coherent with
+    "hip-coherent"), or (diagnostic --host-alloc register) page-aligned numpy
+    memory registered with hipHostRegister."""
+    from mcmtt_opticalflow_amd import hip
 
-    keep = []
-    if kind == "torch":
-        def alloc(shape):
-            t = torch.empty(shape, dtype=torch.uint8).pin_memory()
-            keep.append(t)
-            return t.numpy()
-    else:
-        hip = ctypes.CDLL("libamdhip64.so")
-        hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
-        hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    if kind == "register":
+        keep = []
+        H = hip.rt()
+        H.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
 
         def alloc(shape):
             n = int(np.prod(shape))
-            if kind == "register":
-                raw = np.empty(n + 4096, np.uint8)
-                off = (-raw.ctypes.data) % 4096
-                a = raw[off:off + n]
-                if hip.hipHostRegister(a.ctypes.data, n, 0) != 0:
-                    raise RuntimeError("hipHostRegister failed")
-                keep.append(raw)
-                return a.reshape(shape)
-            p = ctypes.c_void_p()
-            flags = 0x40000000 if kind == "hip-coherent" else 0
-            if hip.hipHostMalloc(ctypes.byref(p), max(n, 1), flags) != 0:
-                raise RuntimeError("hipHostMalloc failed")
-            buf = (ctypes.c_uint8 * n).from_address(p.value)
-            keep.append(buf)
-            return np.ctypeslib.as_array(buf).reshape(shape)
+            raw = np.empty(n + 4096, np.uint8)
+            off = (-raw.ctypes.data) % 4096
+            a = raw[off:off + n]
+            hip.check(H.hipHostRegister(a.ctypes.data, n, 0), "hipHostRegister")
+            keep.append(raw)
+            return a.reshape(shape)
 
-    alloc.keep = keep
-    return alloc
+        alloc.keep = keep
+        return alloc
+    return hip.PinnedAllocator(coherent=(kind == "hip-coherent"))
 
 
 class LaunchTimes:
@@ -382,16 +368,14 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     """The Tracker2D workload on this rank: warm-up, `steps` timed frames. Returns
     the measurements (rank 0: with the gathered results of every frame when
     args.verify)."""
-    import torch
-
-    from mcmtt_opticalflow_amd import _lib
+    from mcmtt_opticalflow_amd import _lib, hip
     from mcmtt_opticalflow_amd import dist as pdist
     from mcmtt_opticalflow_amd import tracker2d as t2d
 
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
     warmup = max(warmup, 1)  # the first step launches the frame the next one completes
-    torch.cuda.set_device(local_rank)
+    hip.set_device(local_rank)
     cams = cameras_of_rank(args, world, rank)
     C = len(cams)
     gridfast = args.features == "gridfast"
@@ -402,7 +386,9 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     group = t2d.Group(args.width, args.height, cams, device=local_rank, max_objects=max_obj)
     slot_bytes = t2d.result_slot_bytes(max_obj, 1)
     send = pinned((C, slot_bytes))
-    exch = pdist.ResultExchange(world, rank, C * slot_bytes, device=local_rank) if world > 1 else None
+    # N > 1 always; N = 1 with --exchange (what the RCCL hand-off costs on one rank)
+    exch = (pdist.ResultExchange(world, rank, C * slot_bytes, device=local_rank)
+            if world > 1 or args.exchange else None)
     T = t2d.load()
     recorded = [] if args.verify else None
 
@@ -467,7 +453,7 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         t += 1
     drain()
     barrier(world)
-    torch.cuda.synchronize()
+    hip.synchronize()
     t0 = time.perf_counter()
     ticks = []  # host time after each step (its frame's results are in host memory): no sync added
     for i in range(steps):
@@ -476,10 +462,10 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
         ticks.append(time.perf_counter())
         t += 1
         if i == args.diag_sync_at or (args.diag_sync_every and i % args.diag_sync_every == args.diag_sync_every - 1):
-            torch.cuda.synchronize()  # diagnostic runs only: a device sync inside the timed region
+            hip.synchronize()  # diagnostic runs only: a device sync inside the timed region
     g_last = drain()  # the last timed frame's hand-off
     gathered = g_last if g_last is not None else gathered
-    torch.cuda.synchronize()
+    hip.synchronize()
     barrier(world)
     elapsed = time.perf_counter() - t0
     elapsed = pdist.max_over_ranks(elapsed)
@@ -501,7 +487,7 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
             t += 1
         g_last = drain()
         gathered = g_last if g_last is not None else gathered
-        torch.cuda.synchronize()
+        hip.synchronize()
         per_kernel, ts = launches.read()
         samples = sampler.read()
     # feature points of the last completed frame (GridFAST mode: what GridFAST kept)
@@ -517,6 +503,8 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     group.close()
     if exch:
         exch.close()
+    if hasattr(pinned, "close"):
+        pinned.close()
     isolated = None
     if args.isolated and world == 1:
         isolated = isolated_launches(args, C)
@@ -597,21 +585,34 @@ def verify_tracker(args, r):
                         "bit for bit against oracle/tracker2d_oracle.py CameraTracker.run"}
 
 
-def tracker_cpu_baseline(args, n_frames_cap=400):
+def tracker_cpu_baseline(args, n_frames_cap=400, legs=("share", "single", "all", "shared")):
     """The oracle Tracker2D (oracle/tracker2d_oracle.py CameraTracker + oracle/lk_oracle.c)
-    on this host: the same synthetic cameras, detections and points, the
-    reference call schedule (every calcOpticalFlowPyrLK rebuilds both pyramids),
-    OpenMP over points and over the rows of the full-frame passes. Legs: the
-    cores allotted to this GPU, 1 thread, all cores, and the shared-pyramid
-    schedule at the allotted cores."""
+    on this host: the same synthetic cameras, detections and points (or, with
+    --features gridfast, the oracle's GridFAST per detection with the run's seeds,
+    PSNWhere_Tracker2D.cpp:735-757), the reference call schedule (every
+    calcOpticalFlowPyrLK rebuilds both pyramids), OpenMP over points and over the
+    rows of the full-frame passes. Legs: the cores allotted to this GPU, 1 thread,
+    all cores, and the shared-pyramid schedule at the allotted cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # cpu_baseline leg only
     import tracker2d_oracle as T2  # cpu_baseline leg only
     from mcmtt_opticalflow_amd import synth
 
     W, H, C = args.width, args.height, args.cameras
+    gridfast = args.features == "gridfast"
     scenes = [synth.make_scene(c, W, H, args.points, nboxes=args.boxes, box_dist=args.box_dist) for c in range(C)]
     grays = [[oracle.bgr2gray(synth.to_bgr(sc.frame(t))) for t in range(args.period)] for sc in scenes]
+
+    def features(gray, boxes, sc, f, t):
+        if not gridfast:
+            pts = sc.points_at(f)
+            return [pts[sc.pt_box == k] for k in range(args.boxes)]
+        rois = []  # the detection boxes clipped as the reference clips its masks
+        for b in boxes:
+            x, y = max(0.0, b[0]), max(0.0, b[1])
+            rois.append((int(x), int(y), int(min(W - x - 1, b[2])), int(min(H - y - 1, b[3]))))
+        feats, _ = oracle.gridfast_detect(gray, rois, seed=t)
+        return feats
 
     def leg(threads, shared, budget, ncams=C):
         T2.NTHREADS, T2.SHARED_PYRAMIDS = threads, shared
@@ -626,8 +627,7 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
                 progress(f"  frame {t}")
             for c, sc in enumerate(scenes[:ncams]):
                 boxes = detection_boxes(sc, f)
-                pts = sc.points_at(f)
-                feats = [pts[sc.pt_box == k] for k in range(args.boxes)]
+                feats = features(grays[c][f], boxes, sc, f, t)
                 extra = [(T2.Rect(*h), loc, hh) for h, loc, hh in (detection_extra(b) for b in boxes)]
                 cams[c].run(grays[c][f], [T2.Rect(*b) for b in boxes], feats, t, extra)
                 if t >= 2:
@@ -642,22 +642,31 @@ def tracker_cpu_baseline(args, n_frames_cap=400):
     # capped by the cgroup's CPU quota), the thread count set explicitly
     share, allc = cpu_share_threads(), cpu_quota_cores()
     v, n, dt = leg(share, False, args.cpu_budget)
-    v1, n1, dt1 = leg(1, False, args.cpu_budget / 2, ncams=1)  # one camera: bounded warm-up
-    va, na, dta = leg(allc, False, args.cpu_budget / 2)
-    vs, ns, dts = leg(share, True, args.cpu_budget / 2)
-    return {"value": round(v, 4), "unit": "frames/s", "cores": share, "kind": "port",
-            "sample": f"{n} camera-frames ({C} cameras x {n // C} frames, {dt:.1f} s) of the same workload "
-                      "(1080p BGR->gray, 8 detections x 64 points, box windows, backward chains + forward + "
-                      "Munkres matching) through oracle/tracker2d_oracle.py + oracle/lk_oracle.c, OpenMP over "
-                      "points and over the rows of every pyramid/border/Scharr pass, reference call schedule "
-                      "(both pyramids rebuilt in every calcOpticalFlowPyrLK)",
-            "single_thread": round(v1, 4), "single_thread_sample": f"{n1} camera-frames (camera 0), {dt1:.1f} s",
-            "all_cores": round(va, 4), "all_cores_threads": allc, "all_cores_sample": f"{na} camera-frames, {dta:.1f} s",
-            "shared_pyramid": round(vs, 4), "shared_pyramid_sample": f"{ns} camera-frames, {dts:.1f} s, {share} threads",
-            "cores_note": "cores = the host cores this GPU's job is allotted (the box sets OMP_NUM_THREADS to its "
-                          "per-GPU CPU share); all_cores = every core this process may run on at once (the affinity "
-                          f"set of {len(os.sched_getaffinity(0))} CPUs capped by the cgroup CPU quota)",
-            **host_info()}
+    feat_txt = ("GridFAST per detection (oracle/gridfast_oracle.c, the run's seeds)" if gridfast else
+                f"{args.points // args.boxes} given points")
+    box_txt = "PETS-like box sizes (synth.pets_box_sizes)" if args.box_dist == "pets" else "64x160 boxes"
+    out = {"value": round(v, 4), "unit": "frames/s", "cores": share, "kind": "port",
+           "sample": f"{n} camera-frames ({C} cameras x {n // C} frames, {dt:.1f} s) of the same workload "
+                     f"({W}x{H} BGR->gray, {args.boxes} detections ({box_txt}) x {feat_txt}, box windows, backward "
+                     "chains + forward + Munkres matching) through oracle/tracker2d_oracle.py + oracle/lk_oracle.c, "
+                     "OpenMP over points and over the rows of every pyramid/border/Scharr pass, reference call "
+                     "schedule (both pyramids rebuilt in every calcOpticalFlowPyrLK)"}
+    if "single" in legs:
+        v1, n1, dt1 = leg(1, False, args.cpu_budget / 2, ncams=1)  # one camera: bounded warm-up
+        out.update({"single_thread": round(v1, 4), "single_thread_sample": f"{n1} camera-frames (camera 0), {dt1:.1f} s"})
+    if "all" in legs:
+        va, na, dta = leg(allc, False, args.cpu_budget / 2)
+        out.update({"all_cores": round(va, 4), "all_cores_threads": allc,
+                    "all_cores_sample": f"{na} camera-frames, {dta:.1f} s"})
+    if "shared" in legs:
+        vs, ns, dts = leg(share, True, args.cpu_budget / 2)
+        out.update({"shared_pyramid": round(vs, 4),
+                    "shared_pyramid_sample": f"{ns} camera-frames, {dts:.1f} s, {share} threads"})
+    out.update({"cores_note": "cores = the host cores this GPU's job is allotted (the box sets OMP_NUM_THREADS to its "
+                              "per-GPU CPU share); all_cores = every core this process may run on at once (the "
+                              f"affinity set of {len(os.sched_getaffinity(0))} CPUs capped by the cgroup CPU quota)",
+                **host_info()})
+    return out
 
 
 def load_profile(path):
@@ -702,7 +711,8 @@ def isolated_launches(args, C, reps=20):
             ms = np.array([m for m, _ in _lib.timing_launches(L, ctx.handle, reps + 1)])
             tags = {t for _, t in _lib.timing_launches(L, ctx.handle, reps + 1)}
             L.psn_lk_enable_timing(ctx.handle, 0, 1)
-            out[name] = {"window": list(win), "median_us": round(1e3 * float(np.median(ms)), 2),
+            out[name] = {"window": list(win), "mean_us": round(1e3 * float(ms.mean()), 2),
+                         "median_us": round(1e3 * float(np.median(ms)), 2),
                          "min_us": round(1e3 * float(ms.min()), 2), "launches": int(ms.size),
                          "kernel": ",".join(sorted(_lib.kernel_of_tag(t) for t in tags))}
     return out
@@ -720,38 +730,52 @@ def tracker_roofline(args, r, C, profile):
     if not per:
         return None
     name, (n, tot) = max(per.items(), key=lambda kv: kv[1][1])
-    avg_ms = tot / n
+    pipe_ms = tot / n  # wall time of the launch in the running pipeline (overlapping launches)
     launch_b = C * lk_b
+    iso = r.get("isolated") or {}
+    fw = iso.get("forward")
+    # the contract's achieved / frac: the dominant launch's own duration, timed
+    # alone on the GPU (HIP events on its stream, mean of the launches), so the
+    # kernel's time per step is its cost and not the overlap of two streams;
+    # the in-pipeline wall time is reported beside it
+    if fw and fw.get("mean_us") and fw.get("kernel") == name:
+        avg_ms, timing = fw["mean_us"] * 1e-3, "isolated"
+    else:
+        avg_ms, timing = pipe_ms, "in_pipeline"
     ach = launch_b / (avg_ms * 1e-3) / 1e9
+    ms_step = r["elapsed"] / r["steps"] * 1e3
+    per_step = {k: v[1] / max(r["measure_steps"], 1) for k, v in per.items()}
     out = {"kernel": name, "bound": "latency",
            "achieved": round(ach, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 6),
            "traffic": None, "bytes_per_launch": launch_b, "avg_launch_us": round(1e3 * avg_ms, 2),
-           "launches_timed": n,
+           "timing": timing,
+           "launches_per_step": round(n / max(r["measure_steps"], 1), 3),
+           "kernel_ms_per_step": round(avg_ms * n / max(r["measure_steps"], 1), 4),
+           "kernel_within_step": avg_ms * n / max(r["measure_steps"], 1) <= ms_step,
+           "in_pipeline": {"avg_launch_us": round(1e3 * pipe_ms, 2), "launches_timed": n,
+                           "achieved": round(launch_b / (pipe_ms * 1e-3) / 1e9, 3),
+                           "note": "the launch's wall time inside the running pipeline (HIP events on its stream; "
+                                   "consecutive forward launches overlap on two streams and share the CUs with the "
+                                   "backward chains), so it exceeds the launch's own cost"},
            "bytes_note": f"SURVEY 8(d) LK bytes 2*S_pyr + 21*N = {lk_b} per camera-frame x {C} camera-frames per "
-                         "launch; achieved/peak/frac are the HBM roofline of this kernel (contract fields)",
+                         "launch; achieved/peak/frac are the HBM roofline of this kernel (contract fields) over "
+                         "avg_launch_us (timing: isolated = the frame-set's launch alone on the GPU)",
            "per_kernel_us": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
-                                 "ms_per_step": round(v[1] / max(r["measure_steps"], 1), 4)} for k, v in sorted(per.items())},
-           "avg_launch_note": "avg_launch_us = the launch's wall time in the running pipeline (HIP events on its "
-                              "stream; consecutive launches overlap on their streams); isolated = the same launch "
-                              "alone on the GPU"}
-    iso = r.get("isolated")
-    if iso:
-        fw = iso["forward"] if "forward" in iso else None
-        if fw and fw.get("median_us"):
-            a_iso = launch_b / (fw["median_us"] * 1e-6) / 1e9
-            out["isolated"] = {**fw, "achieved": round(a_iso, 3), "frac": round(a_iso / HBM_PEAK_GBPS, 6),
-                               "bytes_per_launch": launch_b,
-                               "workload": f"the forward launch of one frame-set alone on the GPU: {C} cameras x "
-                                           f"{args.points} points, median of {fw['launches']} launches"}
+                                 "ms_per_step": round(per_step[k], 4)} for k, v in sorted(per.items())}}
+    if fw:
+        out["isolated"] = {**fw, "bytes_per_launch": launch_b,
+                           "workload": f"the forward launch of one frame-set alone on the GPU: {C} cameras x "
+                                       f"{args.points} points, {fw['launches']} launches"}
         out["isolated_backward"] = iso.get("backward")
         # the same launches under rocprofv3 --kernel-trace (the round profile's
         # `isolated` section: bench.py --mode isolated, this workload)
         pi = ((profile or {}).get("isolated") or {}).get("kernels", {})
-        if fw and out.get("isolated") and fw.get("kernel") in pi:
+        if fw.get("kernel") in pi:
             pki = pi[fw["kernel"]]
             a_p = launch_b / (pki["avg_us"] * 1e-6) / 1e9
             out["isolated"].update({"profile_avg_us": pki["avg_us"], "profile_launches": pki["launches"],
-                                    "profile_achieved": round(a_p, 3), "profile_frac": round(a_p / HBM_PEAK_GBPS, 6)})
+                                    "profile_achieved": round(a_p, 3), "profile_frac": round(a_p / HBM_PEAK_GBPS, 6),
+                                    "profile_vs_live": round(pki["avg_us"] / (1e3 * avg_ms), 4)})
     lib_sha = file_sha16(_lib.LIB_PATH)
     if profile:
         pk = profile.get("kernels", {}).get(name, {})
@@ -924,9 +948,20 @@ def tracker_line(args, r, world, C, scaling, profile):
         "frames_per_set_per_s": round(r["steps"] / r["elapsed"], 2),
         "segments": segment_rates(r, world * C),
         "result_objects_last_frame": r["objs_last"],
+        "runtime": runtime_record(),
         "cpu_baseline": None,
     }
     return out
+
+
+def runtime_record():
+    """The ROCm runtime files this process runs on (psn_lk_runtime_info + /proc/self/maps)."""
+    from mcmtt_opticalflow_amd import _lib
+
+    info = _lib.runtime_info()
+    return {k: info.get(k) for k in ("libamdhip64", "libhsa-runtime64", "librccl", "libamd_comgr",
+                                     "hip_runtime_version", "rccl_version", "built_against_hip", "one_runtime",
+                                     "mapped")}
 
 
 def tracker_main(args):
@@ -991,6 +1026,12 @@ def tracker_legs(args, profile):
     lr = tracker_line(ar, rr, 1, args.cameras, "weak", None)
     legs["realistic"] = {k: lr[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["realistic"]["lk_launches"] = {k: lr["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
+    if not args.no_cpu_baseline:  # the reference's real per-frame work on the host cores (oracle restatement)
+        progress("realistic leg: cpu baseline")
+        cb = tracker_cpu_baseline(ar, legs=("share", "single"))
+        legs["realistic"]["cpu_baseline"] = cb
+        legs["realistic"]["speedup_vs_cpu"] = round(lr["value"] / cb["value"], 1)
+        legs["realistic"]["speedup_vs_cpu_single_thread"] = round(lr["value"] / cb["single_thread"], 1)
     legs["config4"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3)["line"]
     legs["config4_frames_in_hbm"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3,
                                                 ingest="hbm")["line"]
@@ -1044,17 +1085,16 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     psn_lk_push_frame_async, copy engines, as the Tracker2D headline does);
     sg: SG(9, 1) Insert of every tracked point's position per frame (status as
     the active mask), on the same stream."""
-    import torch
-
     from mcmtt_opticalflow_amd import dist as pdist
-    from mcmtt_opticalflow_amd import lk, synth
+    from mcmtt_opticalflow_amd import hip, lk, synth
 
-    device = torch.device("cuda", local_rank)
+    hip.set_device(local_rank)
     cams = [rank * C + k for k in range(C)]
     win, R = 21, 4
     scenes = [synth.make_scene(c, W, H, N) for c in cams]
     frames = []
     period = args.period if ingest == "hbm" else min(args.period, 4)  # pinned 4K BGR: 25 MB a frame
+    pinned = None
     if ingest == "host":
         pinned = pinned_allocator()
         for sc in scenes:
@@ -1064,39 +1104,38 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
                 b[...] = synth.to_bgr(sc.frame(t))
                 fr.append(b)
             frames.append(fr)
-    else:
+    else:  # gray frames resident in HBM (device buffers of the library's runtime)
         for sc in scenes:
-            f = torch.empty((period, H, W), dtype=torch.uint8, device=device)
-            for t in range(period):
-                f[t].copy_(torch.from_numpy(sc.frame(t)))
-            frames.append(f)
-    stream = torch.cuda.Stream(device)
-    torch.cuda.set_stream(stream)
+            frames.append([hip.DeviceBuffer.from_array(sc.frame(t)) for t in range(period)])
+    stream = hip.Stream()
     ctx = lk.LKContext(W, H, ring_slots=R * C, max_level_cap=levels - 1, device=local_rank)
-    ctx.set_stream(stream.cuda_stream)
+    ctx.set_stream(stream.handle)
     for kv in getattr(args, "lk_variant", None) or []:  # experiments: psn_lk_debug_set_variant
         k, v = kv.split("=")
         ctx.set_variant(k, int(v))
     mode = 2 if C == 1 else 1
     ctx.set_ingest_overlap(mode)
     sb = pdist.slot_bytes(N, C)
-    slots = [torch.zeros(sb, dtype=torch.uint8, device=device) for _ in range(2)]
-    views = [pdist.slot_views(s, N, C) for s in slots]
-    for hdr, nxt, _, _ in views:
-        hdr.copy_(torch.tensor([[c, 0, N, 0] for c in cams], dtype=torch.int32).view(hdr.shape))
-    views[0][1].copy_(torch.from_numpy(np.concatenate([sc.points_at(0) for sc in scenes])))
-    gathered = torch.empty((world, sb), dtype=torch.uint8, device=device)
+    offs = pdist.slot_offsets(N, C)  # header, next_xy, err, status
+    hdr0 = np.array([[c, 0, N, 0] for c in cams], np.int32)
+    slot_host = np.zeros(sb, np.uint8)
+    slot_host[:hdr0.nbytes] = hdr0.view(np.uint8).reshape(-1)
+    slot_host[offs[1]:offs[2]] = np.concatenate([sc.points_at(0) for sc in scenes]).astype(np.float32).view(
+        np.uint8).reshape(-1)
+    slots = [hip.DeviceBuffer.from_array(slot_host) for _ in range(2)]
+    gathered = hip.DeviceBuffer(world * sb)
+    comm = pdist.init_comm(world, rank, local_rank) if world > 1 else None
     params = lk.make_params((win, win), levels - 1)
     smoother = None
     if sg:
         smoother = lk.SGSmoother(C * N, 2, 9, 1, device=local_rank)
-        smoother.set_stream(stream.cuda_stream)
-        sg_ref = torch.empty(C * N, dtype=torch.int32, device=device)
-        sg_out = torch.empty((C * N, 9, 2), dtype=torch.float64, device=device)
+        smoother.set_stream(stream.handle)
+        sg_ref = hip.DeviceBuffer(4 * C * N)
+        sg_out = hip.DeviceBuffer(8 * C * N * 9 * 2)
 
     # the harness's per-step host work kept to the calls themselves: frame
-    # pointers, query arrays, slot views and their device pointers built once
-    fptr = [[int(frames[k][i].data_ptr()) for i in range(period)] for k in range(C)] if ingest != "host" else None
+    # pointers, query arrays and slot pointers built once
+    fptr = [[frames[k][i].addr for i in range(period)] for k in range(C)] if ingest != "host" else None
 
     def push(t):
         for k in range(C):
@@ -1110,9 +1149,8 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     ctx.sync()
     queries = [lk.query_array([lk.make_query(k * R + (t - 1) % R, k * R + t % R, k * N, N, params) for k in range(C)])
                for t in range(R)]
-    ptrs = [tuple(int(v.data_ptr()) for v in vw) for vw in views]  # (header, next, err, status) per parity
-    hdr_t = [vw[0][:, 1] if C > 1 else vw[0][1] for vw in views]
-    sg_ptrs = (int(sg_ref.data_ptr()), int(sg_out.data_ptr())) if sg else None
+    ptrs = [tuple(sl.addr + o for o in offs) for sl in slots]  # (header, next, err, status) per parity
+    sg_ptrs = (sg_ref.addr, sg_out.addr) if sg else None
 
     def step(t):
         cur, prv = ptrs[t % 2], ptrs[(t - 1) % 2]
@@ -1120,20 +1158,21 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
         ctx.track_device(queries[t % R], prv[1], cur[1], cur[3], cur[2])
         if smoother is not None:  # lost points (status 0) are not inserted
             smoother.insert_device(cur[1], 2, cur[3], sg_ptrs[0], sg_ptrs[1])
-        hdr_t[t % 2].fill_(t)
-        if world > 1:
-            pdist.allgather_slots(slots[t % 2], world, out=gathered)
+        for k in range(C):  # header.frame of every camera
+            hip.memset_d32_async(cur[0] + 16 * k + 4, t, 1, stream)
+        if comm is not None:
+            pdist.comm_allgather(comm, slots[t % 2].addr, gathered.addr, sb, stream.handle)
 
     t = 1
     for _ in range(warmup):
         step(t)
         t += 1
-    torch.cuda.synchronize(device)
+    hip.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         step(t)
         t += 1
-    torch.cuda.synchronize(device)
+    hip.synchronize()
     elapsed = time.perf_counter() - t0
     # launch durations after the timed region (HIP events on the LK stream)
     measure = max(1, min(steps, 50))
@@ -1141,12 +1180,16 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     for _ in range(measure):
         step(t)
         t += 1
-    torch.cuda.synchronize(device)
+    hip.synchronize()
     ts = ctx.timing_stats()
     ctx.close()
     if smoother is not None:
         smoother.close()
-    torch.cuda.set_stream(torch.cuda.default_stream(device))
+    if comm is not None:
+        pdist.comm_destroy(comm)
+    stream.destroy()
+    if pinned is not None:
+        pinned.close()
     pyr_b, lk_b = algorithmic_bytes(W, H, levels, N)
     lk_us = 1e3 * ts["track_ms"] / max(ts["n_track"], 1)
     launch_b = C * lk_b + (pyr_b if mode == 2 else 0)
@@ -1179,11 +1222,9 @@ def config4_run(args, world, rank, local_rank, steps, warmup, ingest="host"):
     W, H, N, levels = 3840, 2160, 4096, 5
     r = kernel_run(args, steps, warmup, world, rank, local_rank, C=C, W=W, H=H, N=N, levels=levels, sg=True,
                    ingest=ingest)
-    import torch
-
     from mcmtt_opticalflow_amd import dist as pdist
 
-    elapsed = pdist.max_over_ranks(r["elapsed"], torch.device("cuda", local_rank))
+    elapsed = pdist.max_over_ranks(r["elapsed"])
     fps_all = total * steps / elapsed
     ach = r["launch_bytes"] / (r["lk_us"] * 1e-6) / 1e9
     src = ("BGR in pinned host memory, uploaded every frame (psn_lk_push_frame_async)" if ingest == "host"
@@ -1202,12 +1243,9 @@ def config4_run(args, world, rank, local_rank, steps, warmup, ingest="host"):
 
 def kernel_main(args):
     world, rank, local_rank = dist_env()
-    import torch
-    import torch.distributed as dist
-
-    torch.cuda.set_device(local_rank)
-    if world > 1:  # the slots are device tensors: RCCL (nccl backend) for the all-gather and the timing max
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    # control plane (barriers, the RCCL id, the timing max) on gloo; the slots'
+    # all-gather is the library's RCCL communicator (psn_comm)
+    init_control_plane(world)
     if args.mode == "config4":
         res = config4_run(args, world, rank, local_rank, args.steps, args.warmup)
         if rank == 0:
@@ -1219,13 +1257,15 @@ def kernel_main(args):
                    "roofline": line["roofline"], "cpu_baseline": None}
             print(json.dumps(out), flush=True)
         if world > 1:
+            import torch.distributed as dist
+
             dist.destroy_process_group()
         return
     C = max(1, args.kcameras)
     r = kernel_run(args, args.steps, args.warmup, world, rank, local_rank, C=C, N=args.kpoints)
     from mcmtt_opticalflow_amd import dist as pdist
 
-    elapsed = pdist.max_over_ranks(r["elapsed"], torch.device("cuda", local_rank))
+    elapsed = pdist.max_over_ranks(r["elapsed"])
     fps_all = world * C * args.steps / elapsed
     if rank == 0:
         ach = r["launch_bytes"] / (r["lk_us"] * 1e-6) / 1e9
@@ -1246,6 +1286,8 @@ def kernel_main(args):
             out["speedup_vs_cpu"] = round(fps_all / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
     if world > 1:
+        import torch.distributed as dist
+
         dist.destroy_process_group()
 
 
@@ -1318,8 +1360,11 @@ def parse_args(argv=None):
                     help="frames after the timed region with per-launch HIP-event timing (roofline)")
     ap.add_argument("--diag-sync-at", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--diag-sync-every", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--host-alloc", choices=["torch", "hip", "hip-coherent", "register"], default="torch",
+    ap.add_argument("--host-alloc", choices=["hip", "hip-coherent", "register"], default="hip",
                     help=argparse.SUPPRESS)
+    ap.add_argument("--exchange", action="store_true",
+                    help="tracker mode, N = 1: run the RCCL result exchange (psn_comm, one rank) every frame as N > 1 "
+                         "does")
     ap.add_argument("--push-last", action="store_true",
                     help="tracker mode: push frame t+ahead after complete_next(t+1) instead of before it")
     ap.add_argument("--step-profile", action="store_true", help="tracker mode: host ms of each slow step to stderr")
@@ -1347,6 +1392,11 @@ def main():
         sys.exit(launch_ranks(args, argv))
     if args.dry_run:
         return dry_main(args)
+    # the product library before anything imports torch (the gloo control
+    # plane): one HIP/HSA/RCCL runtime in this process, ROCm's (psn_runtime.cpp)
+    from mcmtt_opticalflow_amd import _lib
+
+    _lib.load()
     if args.mode == "isolated":  # the profile pass of roofline.isolated (tools/profile_round.sh)
         print(json.dumps({"isolated": isolated_launches(args, args.cameras)}), flush=True)
         return None

@@ -306,6 +306,17 @@ void psn_comm_destroy(psn_comm *comm);
 
 int psn_lk_abi_version(void);
 
+/* ---- runtime binding (no reference counterpart: process plumbing) ----
+ * libpsn_lk binds the ROCm runtime by soname (libamdhip64.so.7,
+ * libhsa-runtime64.so.1, librccl.so.1 from its RUNPATH /opt/rocm/lib). When it
+ * loads, it also gives those objects their unversioned names (and maps
+ * libamd_comgr.so.3 from the same directory), so a library loaded later that
+ * asks for "libamdhip64.so" (PyTorch-ROCm's do) binds to the same runtime
+ * instead of mapping a second HIP/HSA runtime. Writes a JSON object into buf:
+ * the file each runtime symbol resolves to, the HIP runtime / RCCL versions, a
+ * bit mask of the unversioned names bound, and the HIP version built against. */
+int psn_lk_runtime_info(char *buf, int len);
+
 #ifdef __cplusplus
 }
 #endif

@@ -121,6 +121,25 @@ def kernel_of_tag(tag: int) -> str:
     return f"lk_kernel_bx<{tag // 10}, {'true' if tag % 10 else 'false'}>"
 
 
+def runtime_info() -> dict:
+    """The ROCm runtime this process runs the library on: psn_lk_runtime_info
+    (the file each HIP / HSA / RCCL / comgr symbol resolves to, versions) plus
+    every runtime file mapped (`mapped`: one path per library = one runtime)."""
+    import json
+
+    from . import hip
+
+    L = load()
+    buf = ctypes.create_string_buffer(4096)
+    rc = L.psn_lk_runtime_info(buf, len(buf))
+    if rc != 0:
+        raise PsnLkError(rc, "psn_lk_runtime_info")
+    info = json.loads(buf.value.decode())
+    info["mapped"] = hip.mapped_runtimes()
+    info["one_runtime"] = all(len(v) <= 1 for v in info["mapped"].values())
+    return info
+
+
 def load(path: str | None = None):
     """The product library (mcmtt_opticalflow_amd/lib/libpsn_lk.so). Only the
     profiling tools pass path (STAMPS_LIB_PATH), before anything else loads it."""
@@ -197,6 +216,7 @@ def load(path: str | None = None):
     L.psn_comm_allgather.argtypes = [vp, vp, vp, ctypes.c_size_t, vp]
     L.psn_comm_destroy.argtypes = [vp]
     L.psn_comm_destroy.restype = None
+    L.psn_lk_runtime_info.argtypes = [ctypes.c_char_p, ip]
     _lib, _lib_path = L, path
     return L
 

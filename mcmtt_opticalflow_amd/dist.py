@@ -60,8 +60,21 @@ def allgather_slots(slot, world_size: int, out=None):
     return out
 
 
+def slot_offsets(npts: int, ncam: int = 1):
+    """Byte offsets of (header, next_xy, err, status) in a slot of
+    slot_bytes(npts, ncam) bytes (device pointers = slot base + offset)."""
+    m = npts * ncam
+    o = HEADER_BYTES * ncam
+    return 0, o, o + 8 * m, o + 12 * m
+
+
 def max_over_ranks(value: float, device=None) -> float:
-    """Max of a float over all ranks (the bench's max-over-ranks timing)."""
+    """Max of a float over all ranks (the bench's max-over-ranks timing; CPU
+    tensors on the gloo control plane unless `device` names another)."""
+    import sys
+
+    if "torch.distributed" not in sys.modules:  # no control plane in this process: one rank
+        return float(value)
     import torch
     import torch.distributed as dist
 
@@ -70,6 +83,45 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def init_comm(world: int, rank: int, device: int):
+    """The library's RCCL communicator over all ranks (psn_comm_init); the unique
+    id travels over the torch.distributed control group (gloo) when world > 1."""
+    import ctypes
+
+    from . import _lib
+
+    L = _lib.load()
+    uid = (ctypes.c_uint8 * _lib.COMM_UNIQUE_ID_BYTES)()
+    if rank == 0 and L.psn_comm_get_unique_id(uid) != 0:
+        raise RuntimeError("psn_comm_get_unique_id failed")
+    if world > 1:
+        import torch.distributed as dist
+
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)
+        ctypes.memmove(uid, box[0], len(box[0]))
+    comm = ctypes.c_void_p()
+    rc = L.psn_comm_init(world, rank, device, uid, ctypes.byref(comm))
+    if rc != 0:
+        raise RuntimeError(f"psn_comm_init failed ({rc})")
+    return comm
+
+
+def comm_allgather(comm, d_send: int, d_recv: int, nbytes: int, stream: int):
+    """psn_comm_allgather of one slot per rank, device to device, enqueued on `stream`."""
+    from . import _lib
+
+    rc = _lib.load().psn_comm_allgather(comm, d_send, d_recv, nbytes, stream)
+    if rc != 0:
+        raise RuntimeError(f"psn_comm_allgather failed ({rc})")
+
+
+def comm_destroy(comm):
+    from . import _lib
+
+    _lib.load().psn_comm_destroy(comm)
 
 
 class ResultExchange:
@@ -90,75 +142,75 @@ class ResultExchange:
 
     backend "psn_comm": the library's RCCL communicator (psn_comm_init /
     psn_comm_allgather over xGMI; the unique id travels over the
-    torch.distributed control group): staging pinned host -> device -> all-gather
-    -> pinned host, enqueued on one HIP stream with an event per ticket. backend
+    torch.distributed control group when world > 1): staging pinned host ->
+    device -> all-gather -> pinned host, enqueued on one HIP stream of the
+    library's runtime (hip.py, no torch.cuda) with an event per ticket. backend
     "torch": the same exchange with torch.distributed on CPU tensors (gloo,
     async_op), for the CPU tests."""
 
     def __init__(self, world: int, rank: int, bytes_per_rank: int, device: int = 0, backend: str = "psn_comm",
                  depth: int = 3):
-        import ctypes
-
-        import torch
-        import torch.distributed as dist
-
         self.world, self.rank, self.nbytes, self.backend, self.depth = world, rank, bytes_per_rank, backend, depth
         self._comm = None
         self._next = 0        # ring entry of the next start
-        self._inflight = []   # tickets started, not yet waited (start order)
+        self._inflight = []   # ring entries started, not yet waited (start order)
         if backend == "torch":
+            import torch
+
             self._send = [torch.empty(bytes_per_rank, dtype=torch.uint8) for _ in range(depth)]
             self._recv = [torch.empty(world * bytes_per_rank, dtype=torch.uint8) for _ in range(depth)]
             self._work = [None] * depth
             return
-        from . import _lib
+        from . import _lib, hip
 
         self._L = _lib.load()
-        uid = (ctypes.c_uint8 * _lib.COMM_UNIQUE_ID_BYTES)()
-        if rank == 0 and self._L.psn_comm_get_unique_id(uid) != 0:
-            raise RuntimeError("psn_comm_get_unique_id failed")
-        box = [bytes(uid)]
-        dist.broadcast_object_list(box, src=0)
-        ctypes.memmove(uid, box[0], len(box[0]))
-        comm = ctypes.c_void_p()
-        rc = self._L.psn_comm_init(world, rank, device, uid, ctypes.byref(comm))
-        if rc != 0:
-            raise RuntimeError(f"psn_comm_init failed ({rc})")
+        self._hip = hip
+        comm = init_comm(world, rank, device)
         self._comm = comm
-        dev = torch.device("cuda", device)
-        self._stream = torch.cuda.Stream(dev)
-        self._send_h = [torch.empty(bytes_per_rank, dtype=torch.uint8).pin_memory() for _ in range(depth)]
-        self._send = [torch.empty(bytes_per_rank, dtype=torch.uint8, device=dev) for _ in range(depth)]
-        self._recv_d = [torch.empty(world * bytes_per_rank, dtype=torch.uint8, device=dev) for _ in range(depth)]
-        self._recv_h = [torch.empty(world * bytes_per_rank, dtype=torch.uint8).pin_memory() for _ in range(depth)]
-        self._done = [torch.cuda.Event() for _ in range(depth)]
+        hip.set_device(device)
+        # the library's HIP runtime (mcmtt_opticalflow_amd/hip.py): pinned staging,
+        # device buffers, one exchange stream, an event per ring entry
+        self._stream = hip.Stream()
+        self._pinned = hip.PinnedAllocator()
+        self._send_h = [self._pinned((bytes_per_rank,)) for _ in range(depth)]
+        self._recv_h = [self._pinned((world * bytes_per_rank,)) for _ in range(depth)]
+        self._send = [hip.DeviceBuffer(bytes_per_rank) for _ in range(depth)]
+        self._recv_d = [hip.DeviceBuffer(world * bytes_per_rank) for _ in range(depth)]
+        self._done = [hip.Event() for _ in range(depth)]
 
     def start(self, send) -> int:
         """Enqueue the exchange of `send` (uint8, bytes_per_rank bytes; copied
-        before return, so the caller may refill it) and return its ticket."""
+        before return, so the caller may refill it) and return its ticket. A
+        failed start leaves every ticket in flight intact."""
         import numpy as np
-        import torch
-        import torch.distributed as dist
 
         if len(self._inflight) >= self.depth:
             raise RuntimeError(f"ResultExchange: {self.depth} exchanges in flight; wait for the oldest first")
+        src = np.ascontiguousarray(send).reshape(-1)
+        if src.dtype != np.uint8 or src.size != self.nbytes:
+            raise ValueError(f"ResultExchange.start: {src.size} {src.dtype} values, expected {self.nbytes} uint8")
+        # the in-flight entries are the run just before _next (waited in start
+        # order), so with fewer than `depth` in flight entry _next is free
         i = self._next
-        self._next = (i + 1) % self.depth
-        src = torch.from_numpy(np.ascontiguousarray(send).reshape(-1))
         if self.backend == "torch":
-            self._send[i].copy_(src)
+            import torch
+            import torch.distributed as dist
+
+            self._send[i].copy_(torch.from_numpy(src))
             self._work[i] = dist.all_gather_into_tensor(self._recv[i], self._send[i], async_op=True)
         else:
-            self._send_h[i].copy_(src)  # a few KB: the caller's buffer is free again
-            with torch.cuda.stream(self._stream):
-                self._send[i].copy_(self._send_h[i], non_blocking=True)
-                rc = self._L.psn_comm_allgather(self._comm, self._send[i].data_ptr(), self._recv_d[i].data_ptr(),
-                                                self.nbytes, self._stream.cuda_stream)
-                if rc != 0:
-                    raise RuntimeError(f"psn_comm_allgather failed ({rc})")
-                self._recv_h[i].copy_(self._recv_d[i], non_blocking=True)
-                self._done[i].record(self._stream)
-        self._inflight.append(i)
+            h = self._hip
+            self._send_h[i][:] = src  # a few KB: the caller's buffer is free again
+            h.memcpy_async(self._send[i].addr, self._send_h[i].ctypes.data, self.nbytes, h.H2D, self._stream)
+            rc = self._L.psn_comm_allgather(self._comm, self._send[i].addr, self._recv_d[i].addr, self.nbytes,
+                                            self._stream.handle)
+            if rc != 0:
+                raise RuntimeError(f"psn_comm_allgather failed ({rc})")
+            h.memcpy_async(self._recv_h[i].ctypes.data, self._recv_d[i].addr, self.world * self.nbytes, h.D2H,
+                           self._stream)
+            self._done[i].record(self._stream)
+        self._inflight.append(i)  # only once the exchange is enqueued
+        self._next = (i + 1) % self.depth
         return i
 
     def wait(self, ticket: int):
@@ -173,7 +225,7 @@ class ResultExchange:
             self._work[ticket] = None
             return self._recv[ticket].numpy()
         self._done[ticket].synchronize()
-        return self._recv_h[ticket].numpy()
+        return self._recv_h[ticket]
 
     def pending(self) -> int:
         return len(self._inflight)
@@ -189,3 +241,9 @@ class ResultExchange:
             self._stream.synchronize()
             self._L.psn_comm_destroy(self._comm)
             self._comm = None
+            for e in self._done:
+                e.destroy()
+            for b in self._send + self._recv_d:
+                b.free()
+            self._pinned.close()
+            self._stream.destroy()
