@@ -383,7 +383,11 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     pinned = pinned_allocator(args.host_alloc)
     feeds = [CameraFeed(c, args, pinned) for c in cams]
     max_obj = 2 * args.boxes
+    c_t0 = time.perf_counter()
     group = t2d.Group(args.width, args.height, cams, device=local_rank, max_objects=max_obj)
+    create_ms = 1e3 * (time.perf_counter() - c_t0)
+    warm = ctypes.c_double()
+    warm_ms = warm.value if L.psn_lk_sdma_warmup_ms(local_rank, ctypes.byref(warm)) == 0 else None
     slot_bytes = t2d.result_slot_bytes(max_obj, 1)
     send = pinned((C, slot_bytes))
     # N > 1 always; N = 1 with --exchange (what the RCCL hand-off costs on one rank)
@@ -515,7 +519,11 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
             "box_sizes": box_sizes, "isolated": isolated,
             "measure_steps": measure,
             "per_kernel": per_kernel, "ts": ts, "samples": samples, "objs_last": objs_last,
-            "points_per_camera": pts_last, "recorded": recorded, "slot_bytes": slot_bytes, "max_obj": max_obj}
+            "points_per_camera": pts_last, "recorded": recorded, "slot_bytes": slot_bytes, "max_obj": max_obj,
+            "setup": {"group_create_ms": round(create_ms, 3),
+                      "sdma_warmup_ms": None if warm_ms is None else round(warm_ms, 3),
+                      "note": "outside the timed region: psn_t2d_group creation, of which the process's first "
+                              "psn_lk_create sets up every SDMA engine (psn_lk_sdma_warmup_ms)"}}
 
 
 def verify_tracker(args, r):
@@ -729,19 +737,31 @@ def tracker_roofline(args, r, C, profile):
     per = r["per_kernel"]
     if not per:
         return None
-    name, (n, tot) = max(per.items(), key=lambda kv: kv[1][1])
-    pipe_ms = tot / n  # wall time of the launch in the running pipeline (overlapping launches)
     launch_b = C * lk_b
     iso = r.get("isolated") or {}
-    fw = iso.get("forward")
+    meas = max(r["measure_steps"], 1)
+    # the dominant kernel: the largest cost per frame-set when each launch runs
+    # alone on the GPU (isolated mean x launches per step); without isolated
+    # timings, the largest in-pipeline time per step
+    cand = [(v["mean_us"] * per[v["kernel"]][0] / meas, v) for v in iso.values()
+            if v and v.get("mean_us") and v.get("kernel") in per]
+    if cand:
+        _, dom = max(cand, key=lambda c: c[0])
+        name = dom["kernel"]
+    else:
+        dom = None
+        name = max(per.items(), key=lambda kv: kv[1][1])[0]
+    n, tot = per[name]
+    pipe_ms = tot / n  # wall time of the launch in the running pipeline (overlapping launches)
     # the contract's achieved / frac: the dominant launch's own duration, timed
     # alone on the GPU (HIP events on its stream, mean of the launches), so the
-    # kernel's time per step is its cost and not the overlap of two streams;
+    # kernel's time per step is its cost and not the overlap of several streams;
     # the in-pipeline wall time is reported beside it
-    if fw and fw.get("mean_us") and fw.get("kernel") == name:
-        avg_ms, timing = fw["mean_us"] * 1e-3, "isolated"
+    if dom is not None:
+        avg_ms, timing = dom["mean_us"] * 1e-3, "isolated"
     else:
         avg_ms, timing = pipe_ms, "in_pipeline"
+    fw = dom
     ach = launch_b / (avg_ms * 1e-3) / 1e9
     ms_step = r["elapsed"] / r["steps"] * 1e3
     per_step = {k: v[1] / max(r["measure_steps"], 1) for k, v in per.items()}
@@ -763,10 +783,11 @@ def tracker_roofline(args, r, C, profile):
            "per_kernel_us": {k: {"launches": v[0], "avg_us": round(1e3 * v[1] / v[0], 2),
                                  "ms_per_step": round(per_step[k], 4)} for k, v in sorted(per.items())}}
     if fw:
-        out["isolated"] = {**fw, "bytes_per_launch": launch_b,
-                           "workload": f"the forward launch of one frame-set alone on the GPU: {C} cameras x "
+        which = [k for k, v in iso.items() if v is fw][0]
+        out["isolated"] = {**fw, "call": which, "bytes_per_launch": launch_b,
+                           "workload": f"the {which} launch of one frame-set alone on the GPU: {C} cameras x "
                                        f"{args.points} points, {fw['launches']} launches"}
-        out["isolated_backward"] = iso.get("backward")
+        out["isolated_all"] = iso
         # the same launches under rocprofv3 --kernel-trace (the round profile's
         # `isolated` section: bench.py --mode isolated, this workload)
         pi = ((profile or {}).get("isolated") or {}).get("kernels", {})
@@ -949,6 +970,7 @@ def tracker_line(args, r, world, C, scaling, profile):
         "segments": segment_rates(r, world * C),
         "result_objects_last_frame": r["objs_last"],
         "runtime": runtime_record(),
+        "setup": r.get("setup"),
         "cpu_baseline": None,
     }
     return out
@@ -1151,6 +1173,18 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
                for t in range(R)]
     ptrs = [tuple(sl.addr + o for o in offs) for sl in slots]  # (header, next, err, status) per parity
     sg_ptrs = (sg_ref.addr, sg_out.addr) if sg else None
+    # every step's slot headers (cam, frame, npts, 0), prepared in pinned host
+    # memory before the timed region and written by one small copy kernel per
+    # step (psn_t2d_upload_device), the frame index of the slot the LK fills
+    measure = max(1, min(steps, 50))
+    t_end = warmup + steps + measure + 2
+    hdr_alloc = pinned_allocator("hip-coherent")
+    hdr_pin = hdr_alloc((t_end, C * 16))
+    hdr_tab = hdr_pin.view(np.int32).reshape(t_end, C, 4)
+    hdr_tab[:] = hdr0[None]
+    hdr_tab[:, :, 1] = np.arange(t_end, dtype=np.int32)[:, None]
+    L = ctx._L
+    L.psn_t2d_upload_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
 
     def step(t):
         cur, prv = ptrs[t % 2], ptrs[(t - 1) % 2]
@@ -1158,8 +1192,9 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
         ctx.track_device(queries[t % R], prv[1], cur[1], cur[3], cur[2])
         if smoother is not None:  # lost points (status 0) are not inserted
             smoother.insert_device(cur[1], 2, cur[3], sg_ptrs[0], sg_ptrs[1])
-        for k in range(C):  # header.frame of every camera
-            hip.memset_d32_async(cur[0] + 16 * k + 4, t, 1, stream)
+        rc = L.psn_t2d_upload_device(cur[0], hdr_pin[t].ctypes.data, 16 * C, stream.handle)
+        if rc:
+            raise RuntimeError(f"psn_t2d_upload_device failed ({rc})")
         if comm is not None:
             pdist.comm_allgather(comm, slots[t % 2].addr, gathered.addr, sb, stream.handle)
 
@@ -1175,7 +1210,6 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     hip.synchronize()
     elapsed = time.perf_counter() - t0
     # launch durations after the timed region (HIP events on the LK stream)
-    measure = max(1, min(steps, 50))
     ctx.enable_timing(measure + 1, 1)
     for _ in range(measure):
         step(t)
@@ -1190,6 +1224,7 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     stream.destroy()
     if pinned is not None:
         pinned.close()
+    hdr_alloc.close()
     pyr_b, lk_b = algorithmic_bytes(W, H, levels, N)
     lk_us = 1e3 * ts["track_ms"] / max(ts["n_track"], 1)
     launch_b = C * lk_b + (pyr_b if mode == 2 else 0)
@@ -1374,6 +1409,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-legs", action="store_true")
     ap.add_argument("--dry-run", action="store_true")
+    ap.add_argument("--lib-dir", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--profile", default=DEFAULT_PROFILE,
                     help="round profile summary (tools/profile_summary.py) for roofline.traffic / valu")
     args = ap.parse_args(argv)
@@ -1396,6 +1432,11 @@ def main():
     # plane): one HIP/HSA/RCCL runtime in this process, ROCm's (psn_runtime.cpp)
     from mcmtt_opticalflow_amd import _lib
 
+    if args.lib_dir:  # A/B experiments: another build of both libraries (tools/gpu_ab.sh)
+        from mcmtt_opticalflow_amd import tracker2d
+
+        _lib.LIB_PATH = os.path.abspath(os.path.join(args.lib_dir, "libpsn_lk.so"))
+        tracker2d.LIB_PATH = os.path.abspath(os.path.join(args.lib_dir, "libpsn_tracker2d.so"))
     _lib.load()
     if args.mode == "isolated":  # the profile pass of roofline.isolated (tools/profile_round.sh)
         print(json.dumps({"isolated": isolated_launches(args, args.cameras)}), flush=True)

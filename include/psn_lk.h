@@ -53,13 +53,16 @@ extern "C" {
 #define PSN_LK_MAX_LEVELS 8
 /* Window limits: widths up to PSN_LK_MAX_WIN_WIDTH (one window row band of the
  * large-window kernel in LDS) and h * ceil(w/4) < 2^22 quads (about 2^24 px);
- * psn_lk_window_supported() is the whole predicate, what psn_lk_track checks
- * after winSize > 2 (else PSN_LK_ERR_UNSUPPORTED). Tracker2D passes box.w x box.h
- * (PSNWhere_Tracker2D.cpp:871-877) and box.w x box.w (:776-782) uncapped: a
- * forward window of a box inside a frame of < 2^24 px is always supported, but a
- * backward box.w x box.w window is not when box.w > 4096 (4097^2 > 2^24): the
- * Tracker2D host checks the same predicate per chain / forward call and flags
- * such a box instead of failing the frame. */
+ * psn_lk_window_supported() is the window predicate psn_lk_track checks after
+ * winSize > 2 (else PSN_LK_ERR_UNSUPPORTED); the only other UNSUPPORTED exit, the
+ * large-window planner's 160-KB LDS guard, is unreachable for a supported window.
+ * Tracker2D passes box.w x box.h (PSNWhere_Tracker2D.cpp:871-877) and box.w x
+ * box.w (:776-782) uncapped: a forward window of a box inside a frame of < 2^24 px
+ * is always supported, but a backward box.w x box.w window is not when box.w >
+ * 4096 (4097^2 > 2^24): the Tracker2D host checks the same predicate up front and
+ * flags such a box; the frame then fails (PSN_LK_ERR_UNSUPPORTED, before any
+ * launch) only when that box's backward chain would actually run, i.e. it holds
+ * at least the chain's minimum of 4 features. */
 #define PSN_LK_MAX_WIN_WIDTH 6400
 #define PSN_LK_MAX_WIN_QUADS (1L << 22)
 
@@ -316,6 +319,12 @@ int psn_lk_abi_version(void);
  * the file each runtime symbol resolves to, the HIP runtime / RCCL versions, a
  * bit mask of the unversioned names bound, and the HIP version built against. */
 int psn_lk_runtime_info(char *buf, int len);
+
+/* Wall time (ms) the first psn_lk_create on `device` spent setting up the
+ * device's SDMA engines (one 4-KB copy per engine each way, so a later frame
+ * upload never lands on an engine whose queue ROCr has yet to create);
+ * PSN_LK_ERR_ARG when no context was created on the device yet. */
+int psn_lk_sdma_warmup_ms(int device, double *ms);
 
 #ifdef __cplusplus
 }

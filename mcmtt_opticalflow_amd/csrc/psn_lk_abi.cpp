@@ -11,6 +11,7 @@
 #include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <cstdarg>
 #include <cstdio>
@@ -221,8 +222,10 @@ int psn_lk_effective_max_level(int width, int height, int win_w, int win_h, int 
 namespace {
 struct AgentPick {
     uint32_t bdf = 0, domain = 0;
+    char uuid[17] = {};  // the HIP device's UUID (16 characters), empty when HIP has none
     hsa_agent_t gpu{}, cpu{};
-    bool have_gpu = false, have_cpu = false;
+    int n_bdf = 0;  // GPU agents on the device's PCI function (> 1: a partitioned device)
+    bool have_gpu = false, have_cpu = false, uuid_match = false;
 };
 hsa_status_t pick_agent(hsa_agent_t a, void *arg) {
     AgentPick *p = (AgentPick *)arg;
@@ -231,13 +234,23 @@ hsa_status_t pick_agent(hsa_agent_t a, void *arg) {
     if (t == HSA_DEVICE_TYPE_CPU && !p->have_cpu) {
         p->cpu = a;
         p->have_cpu = true;
-    } else if (t == HSA_DEVICE_TYPE_GPU && !p->have_gpu) {
+    } else if (t == HSA_DEVICE_TYPE_GPU) {
         uint32_t bdf = 0, dom = 0;
-        if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS &&
-            hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS &&
-            bdf == p->bdf && dom == p->domain) {
+        if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS ||
+            hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) != HSA_STATUS_SUCCESS ||
+            bdf != p->bdf || dom != p->domain)
+            return HSA_STATUS_SUCCESS;
+        p->n_bdf++;
+        // the agent's UUID ("GPU-" + 16 characters) against the HIP device's: on a
+        // partitioned device several agents share the PCI function
+        char u[32] = {};
+        const bool um = p->uuid[0] &&
+                        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_UUID, u) == HSA_STATUS_SUCCESS &&
+                        strncmp(u + 4, p->uuid, 16) == 0;
+        if (!p->have_gpu || (um && !p->uuid_match)) {
             p->gpu = a;
             p->have_gpu = true;
+            p->uuid_match = um;
         }
     }
     return HSA_STATUS_SUCCESS;
@@ -252,7 +265,14 @@ void warm_sdma_engines(int device) {
     AgentPick p;
     p.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
     p.domain = (uint32_t)dom;
+    {
+        hipUUID hu{};
+        if (hipDeviceGetUuid(&hu, device) == hipSuccess) memcpy(p.uuid, hu.bytes, 16);
+    }
     hsa_iterate_agents(pick_agent, &p);
+    // several agents on the PCI function and none with the HIP device's UUID: the
+    // engines of an unknown partition are not warmed (no stall fix, no harm)
+    if (p.n_bdf > 1 && !p.uuid_match) p.have_gpu = false;
     void *h = nullptr, *d = nullptr;
     hsa_signal_t sig{};
     if (p.have_gpu && p.have_cpu && hipHostMalloc(&h, 4096, 0) == hipSuccess && hipMalloc(&d, 4096) == hipSuccess &&
@@ -278,14 +298,28 @@ void warm_sdma_engines(int device) {
     hsa_shut_down();
 }
 std::mutex g_warm_mu;
-std::vector<int> g_warmed;  // devices whose engines are set up
+std::vector<std::pair<int, double>> g_warmed;  // devices whose engines are set up, with the wall ms it took
 void warm_sdma_once(int device) {
     std::lock_guard<std::mutex> lk(g_warm_mu);
-    if (std::find(g_warmed.begin(), g_warmed.end(), device) != g_warmed.end()) return;
-    g_warmed.push_back(device);
+    for (const auto &w : g_warmed)
+        if (w.first == device) return;
+    const auto t0 = std::chrono::steady_clock::now();
     warm_sdma_engines(device);
+    g_warmed.push_back({device, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count()});
 }
 }  // namespace
+
+int psn_lk_sdma_warmup_ms(int device, double *ms) {
+    if (!ms) return PSN_LK_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_warm_mu);
+    for (const auto &w : g_warmed)
+        if (w.first == device) {
+            *ms = w.second;
+            return PSN_LK_OK;
+        }
+    *ms = 0.0;
+    return PSN_LK_ERR_ARG;  // no context was created on this device yet
+}
 
 int psn_lk_create(int device, int width, int height, int ring_slots, int max_level_cap, psn_lk_ctx **out) {
     if (!out || width <= 0 || height <= 0 || ring_slots <= 0 || max_level_cap < 0 ||
@@ -1071,7 +1105,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
         for (int i = 0; i < a.nq; i++) {
             psn::LkQueryDev &d = a.q[i];
             d.bx_hw = 1;
-            while (d.bx_hw < 8 && psn::BxLayout(d.win_w, d.win_h, upt, d.bx_hw + 1).total <= psn::bx_lds_target(upt))
+            while (d.bx_hw < 8 && psn::BxLayout(d.win_w, d.win_h, upt, d.bx_hw + 1).total <= psn::bx_lds_target(upt, notail))
                 d.bx_hw++;
             lds_bx = std::max(lds_bx, psn::BxLayout(d.win_w, d.win_h, upt, d.bx_hw).total);
         }

@@ -239,10 +239,16 @@ constexpr int kBxXInts = 2 * 4 * kBxRecInts;           // two parities x 4 waves
 constexpr int kBxScrBytes = (kBxXInts + 32) * 4 + 64;  // + results / err partials
 constexpr int kBxMaxLds = 64 * 1024;
 constexpr int kBxLdsTarget = 53 * 1024;  // three workgroups per CU
-// workgroups per CU of lk_kernel_bx<upt> (its __launch_bounds__): the 4-unit
-// build fits 128 VGPRs, so four per CU when the LDS plan allows it
-__host__ __device__ constexpr int bx_occupancy(int upt) { return upt <= 4 ? 4 : 3; }
-__host__ __device__ constexpr int bx_lds_target(int upt) { return upt <= 4 ? 40 * 1024 : kBxLdsTarget; }
+// workgroups per CU of lk_kernel_bx<upt, notail> (its __launch_bounds__): the
+// 4-unit build fits 128 VGPRs, so four per CU when the LDS plan allows it; the
+// builds whose registers do not fit 168 VGPRs at three per CU (12 units, and 10
+// units with the scalar-tail chain: 8-33 spilled VGPRs) run two per CU
+__host__ __device__ constexpr int bx_occupancy(int upt, bool notail) {
+    return upt <= 4 ? 4 : (upt >= 12 || (!notail && upt >= 10)) ? 2 : 3;
+}
+__host__ __device__ constexpr int bx_lds_target(int upt, bool notail) {
+    return bx_occupancy(upt, notail) == 4 ? 40 * 1024 : bx_occupancy(upt, notail) == 3 ? kBxLdsTarget : kBxMaxLds;
+}
 __host__ __device__ inline int bx_qw(int w) { return (w + 3) >> 2; }
 __host__ __device__ inline int bx_pm(int w) { return bx_qw(w) + 2; }      // I patch dwords per row
 __host__ __device__ inline int bx_jrp(int w) { return st_jreg_w(w) + 8; }  // J region row pitch (bytes)

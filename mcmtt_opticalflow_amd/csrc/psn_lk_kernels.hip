@@ -2071,7 +2071,7 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
     } while (0)
 #endif
 template <int UPT, bool NOTAIL>
-__global__ __launch_bounds__(kBxNT, bx_occupancy(UPT)) void lk_kernel_bx(LkLaunchArgs A) {
+__global__ __launch_bounds__(kBxNT, bx_occupancy(UPT, NOTAIL)) void lk_kernel_bx(LkLaunchArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     static_assert(UPT % 2 == 0, "units are processed in pairs");
     constexpr int NT = kBxNT;

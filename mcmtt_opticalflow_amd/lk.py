@@ -31,8 +31,11 @@ def make_params(win_size=(21, 21), max_level=3, criteria=(3, 30, 0.01), flags=0,
 
 
 def query_array(queries: list[LkQuery]):
-    """The ctypes array psn_lk_track_device takes (at least one element)."""
-    return (LkQuery * max(len(queries), 1))(*queries)
+    """The ctypes array psn_lk_track_device takes (at least one element; the
+    number of real queries rides along as `nq`, 0 for an empty list)."""
+    arr = (LkQuery * max(len(queries), 1))(*queries)
+    arr.nq = len(queries)
+    return arr
 
 
 def make_query(prev_slot, next_slot, first_pt, num_pts, params: LkParams) -> LkQuery:
@@ -157,8 +160,8 @@ class LKContext:
         """`queries`: a list of LkQuery, or a ctypes LkQuery array built once by the
         caller (query_array) for a launch it repeats."""
         arr = queries if isinstance(queries, ctypes.Array) else query_array(queries)
-        self._check(self._L.psn_lk_track_device(self._h, arr, len(arr) if len(queries) else 0, d_prev, d_next,
-                                                d_status, d_err), "track_device")
+        nq = getattr(arr, "nq", len(arr))
+        self._check(self._L.psn_lk_track_device(self._h, arr, nq, d_prev, d_next, d_status, d_err), "track_device")
 
     def gridfast_detect(self, slot: int, rois, params: GridFastParams | None = None, seed: int = 0):
         """GridFAST keypoints of slot's frame masked by each roi (x, y, w, h),

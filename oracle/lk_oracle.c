@@ -35,8 +35,8 @@ static long long *g_bsum_log = 0;
 void oracle_set_bsum_log(long long *buf) { g_bsum_log = buf; }
 static long long *g_chain_log = 0;
 static int g_chain_upt = 0;
-/* the per-thread parity-record model on every fallback evaluation (buf[16..21]:
- * the caller's buffer holds 24 entries) */
+/* the per-thread parity-record model on every fallback evaluation (buf[16..24]:
+ * the caller's buffer holds ORACLE_CHAIN_LOG_ENTRIES = 25 entries, lk_oracle.h) */
 static int g_chain_log_ext = 0;
 static int g_chain_fs = 256, g_chain_ls = -1;
 static float g_chain_ser[10];

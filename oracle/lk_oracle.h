@@ -81,7 +81,10 @@ void oracle_set_bsum_log(long long *buf);
 /* Analysis hook: every b-sum evaluation is cut into lk_kernel_bx's chains
  * (units of 4 px, `upt` units per thread, 256 threads) and evaluated with the
  * binade-run model (chain_model.c); buf[0..15] collects statistics (see
- * chain_classify in lk_oracle.c). upt = 0 picks the kernel's UPT. */
+ * chain_classify in lk_oracle.c) and buf[16..24] the per-thread parity-record
+ * model, so buf holds at least ORACLE_CHAIN_LOG_ENTRIES entries. upt = 0 picks
+ * the kernel's UPT. */
+#define ORACLE_CHAIN_LOG_ENTRIES 25
 void oracle_set_chain_log(long long *buf, int upt);
 
 /* ---- Binade-run model of an ordered float chain (oracle/chain_model.c) ---- */

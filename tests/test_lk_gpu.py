@@ -245,6 +245,26 @@ def test_lk_device_pointer_path(oracle_mod, overlap):
     assert_same(gpu, ref, "device path")
 
 
+def test_lk_device_empty_query_forms_agree():
+    """No queries: the list [] and a prebuilt query_array([]) (one zeroed
+    placeholder element, nq = 0) are both a no-op, and the outputs stay untouched."""
+    import hiprt
+
+    sc, f0, f1 = scene_pair(9, 640, 480, 16)
+    d_f0, d_f1 = hiprt.DeviceBuffer.from_array(f0), hiprt.DeviceBuffer.from_array(f1)
+    sentinel = np.full((16, 2), -7.0, np.float32)
+    d_p, d_n = hiprt.DeviceBuffer.from_array(sc.points_at(0)), hiprt.DeviceBuffer.from_array(sentinel)
+    d_s, d_e = hiprt.DeviceBuffer.from_array(np.full(16, 9, np.uint8)), hiprt.DeviceBuffer(64)
+    with glk.LKContext(640, 480, ring_slots=2, max_level_cap=3) as ctx:
+        ctx.push_frame_device(0, d_f0.addr, 640, 1)
+        ctx.push_frame_device(1, d_f1.addr, 640, 1)
+        for qs in ([], glk.query_array([])):
+            ctx.track_device(qs, d_p.addr, d_n.addr, d_s.addr, d_e.addr)
+        ctx.sync()
+    assert np.array_equal(d_n.to_array((16, 2), np.float32), sentinel)
+    assert np.all(d_s.to_array(16, np.uint8) == 9)
+
+
 @pytest.mark.parametrize("env", [{}, {"threads": 128}, {"threads": 64}, {"threads": 512}])
 @pytest.mark.parametrize("win", [(21, 21), (9, 9), (64, 64)])
 def test_lk_fused_ingest_pipeline(oracle_mod, env, win):

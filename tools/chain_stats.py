@@ -13,6 +13,8 @@ LK calls goes through the binade-run model (oracle/chain_model.c):
   FRAMES=6 python tools/chain_stats.py
 """
 import ctypes
+
+CHAIN_LOG_ENTRIES = 25  # ORACLE_CHAIN_LOG_ENTRIES (oracle/lk_oracle.h)
 import json
 import os
 import sys
@@ -40,7 +42,7 @@ def main():
     W, H, npts, nboxes, period = 1920, 1080, 512, 8, 10
     sc = synth.make_scene(0, W, H, npts, nboxes=nboxes)
     L = oracle.lib()
-    buf = (ctypes.c_longlong * 32)()
+    buf = (ctypes.c_longlong * CHAIN_LOG_ENTRIES)()
     L.oracle_set_chain_log.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.oracle_set_chain_log(ctypes.addressof(buf), upt)
     T2.NTHREADS = 1
