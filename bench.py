@@ -387,7 +387,8 @@ def tracker_run(args, world=1, rank=0, local_rank=0, steps=None, warmup=None):
     group = t2d.Group(args.width, args.height, cams, device=local_rank, max_objects=max_obj)
     create_ms = 1e3 * (time.perf_counter() - c_t0)
     warm = ctypes.c_double()
-    warm_ms = warm.value if L.psn_lk_sdma_warmup_ms(local_rank, ctypes.byref(warm)) == 0 else None
+    warm_ms = (warm.value if hasattr(L, "psn_lk_sdma_warmup_ms") and
+               L.psn_lk_sdma_warmup_ms(local_rank, ctypes.byref(warm)) == 0 else None)
     slot_bytes = t2d.result_slot_bytes(max_obj, 1)
     send = pinned((C, slot_bytes))
     # N > 1 always; N = 1 with --exchange (what the RCCL hand-off costs on one rank)

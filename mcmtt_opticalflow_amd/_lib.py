@@ -217,7 +217,8 @@ def load(path: str | None = None):
     L.psn_comm_destroy.argtypes = [vp]
     L.psn_comm_destroy.restype = None
     L.psn_lk_runtime_info.argtypes = [ctypes.c_char_p, ip]
-    L.psn_lk_sdma_warmup_ms.argtypes = [ip, ctypes.POINTER(ctypes.c_double)]
+    if hasattr(L, "psn_lk_sdma_warmup_ms"):  # (absent from the A/B experiments' older builds only)
+        L.psn_lk_sdma_warmup_ms.argtypes = [ip, ctypes.POINTER(ctypes.c_double)]
     _lib, _lib_path = L, path
     return L
 

@@ -868,7 +868,10 @@ static void lg_plan(const psn_lk_ctx *c, int w, int h, bool &jr, int &tq) {
 }
 
 // Validate and plan one query.
-static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, PlannedQuery &pq) {
+// no_bx16: a window of 13-16 units per thread goes to the large-window kernel
+// (the call has large windows anyway: one launch fewer, see track_device_impl)
+static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, PlannedQuery &pq,
+                      bool no_bx16 = false) {
     const psn_lk_params &p = q.params;
     const int limit = allow_scratch ? c->nslots : c->user_slots;
     if (q.prev_slot < 0 || q.prev_slot >= limit || q.next_slot < 0 || q.next_slot >= limit)
@@ -931,8 +934,11 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
     d.dv_cw = psn::div_magic(nc);
     {  // box-window kernel: units of 4 pixels, <= kBxMaxUPT per thread
         const long need = ((long)h * psn::bx_qw(w) + psn::kBxNT - 1) / psn::kBxNT;
-        const int upt = need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : 12;
-        if (need <= psn::kBxMaxUPT && psn::BxLayout(w, h, upt).total <= psn::kBxMaxLds) {
+        const int upt = need <= 4 ? 4 : need <= 8 ? 8 : need <= 10 ? 10 : need <= 12 ? 12 : 16;
+        const bool notail = sse && w % 8 == 0;
+        // (a unit's J offset in the region, y * bx_jrp(w) + 4 q, is a 16-bit half)
+        if (need <= psn::kBxMaxUPT && psn::BxLayout(w, h, upt).total <= psn::bx_max_lds(upt, notail) &&
+            (long)psn::st_jreg_h(h) * psn::bx_jrp(w) < 65536) {
             pq.bx_upt = upt;
             pq.bx_lds = psn::BxLayout(w, h, upt).total;
             d.bx_tre = psn::bx_err_rows(w, h, psn::BxLayout(w, h, 4).pb);
@@ -948,7 +954,7 @@ static int plan_query(psn_lk_ctx *c, const psn_lk_query &q, bool allow_scratch, 
         pq.cls = kClsLg;
     } else if (pq.single && !c->force_generic) {
         pq.cls = kClsSt;
-    } else if (pq.bx_upt > 0 && c->box && !c->force_generic && !forced) {
+    } else if (pq.bx_upt > 0 && c->box && !c->force_generic && !forced && !(no_bx16 && pq.bx_upt == 16)) {
         pq.cls = kClsBx;
         pq.key = 10 * pq.bx_upt + ((sse && w % 8 == 0) ? 1 : 0);
     } else if (pq.tiled_tr > 0 && (c->force_generic || !c->box || forced)) {
@@ -1173,6 +1179,21 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
         int rc = plan_query(c, q[i], allow_scratch, plan.back());
         if (rc) return rc;
     }
+    // The 16-unit box kernel (two workgroups per CU) beats the large-window kernel
+    // on a launch of its own (512 points of 70x201: 513 vs 581 us), but a call
+    // that holds large windows as well would launch one class more on the same
+    // stream, each launch a fraction of the GPU with its own tail: there its
+    // windows join the large-window launch (PETS-like boxes: 406 vs 450
+    // camera-frames/s with the extra launch)
+    if (std::any_of(plan.begin(), plan.end(), [](const PlannedQuery &pq) { return pq.cls == kClsLg; }))
+        for (PlannedQuery &pq : plan)
+            if (pq.cls == kClsBx && pq.bx_upt == 16) {
+                PlannedQuery lq;
+                lq.src = pq.src;
+                int rc = plan_query(c, q[pq.src], allow_scratch, lq, true);
+                if (rc) return rc;
+                pq = lq;
+            }
     // slots built on the ingest stream must be complete before the LK reads them;
     // a deferred build of a slot this call reads runs first, as its own launch
     std::vector<int> &used = c->used_slots;  // distinct slots this call reads

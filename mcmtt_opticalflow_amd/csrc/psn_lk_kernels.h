@@ -233,21 +233,26 @@ struct LkStLayout {
 // bx_jrp(w)) | a union of the level's I patch (bytes, rows of bx_pm(w) dwords)
 // and the row-tiled float chain planes of the ordered-sum fallbacks.
 constexpr int kBxNT = 256;
-constexpr int kBxMaxUPT = 12;
+constexpr int kBxMaxUPT = 16;
 constexpr int kBxRecInts = 8 * 15 + 4;                 // per wave and chain: {total, max, min prefix, -} at lanes 31 and 63; term flag
 constexpr int kBxXInts = 2 * 4 * kBxRecInts;           // two parities x 4 waves
 constexpr int kBxScrBytes = (kBxXInts + 32) * 4 + 64;  // + results / err partials
-constexpr int kBxMaxLds = 64 * 1024;
+constexpr int kBxMaxLds = 64 * 1024;   // three or four workgroups per CU
+constexpr int kBxMaxLds2 = 80 * 1024;  // the two-per-CU builds
 constexpr int kBxLdsTarget = 53 * 1024;  // three workgroups per CU
 // workgroups per CU of lk_kernel_bx<upt, notail> (its __launch_bounds__): the
 // 4-unit build fits 128 VGPRs, so four per CU when the LDS plan allows it; the
 // builds whose registers do not fit 168 VGPRs at three per CU (12 units, and 10
-// units with the scalar-tail chain: 8-33 spilled VGPRs) run two per CU
+// units with the scalar-tail chain: 8-33 spilled VGPRs; 16 units) run two per CU
 __host__ __device__ constexpr int bx_occupancy(int upt, bool notail) {
     return upt <= 4 ? 4 : (upt >= 12 || (!notail && upt >= 10)) ? 2 : 3;
 }
 __host__ __device__ constexpr int bx_lds_target(int upt, bool notail) {
-    return bx_occupancy(upt, notail) == 4 ? 40 * 1024 : bx_occupancy(upt, notail) == 3 ? kBxLdsTarget : kBxMaxLds;
+    return bx_occupancy(upt, notail) == 4 ? 40 * 1024 : bx_occupancy(upt, notail) == 3 ? kBxLdsTarget : kBxMaxLds2;
+}
+// the largest LDS plan of a lk_kernel_bx<upt, notail> launch
+__host__ __device__ constexpr int bx_max_lds(int upt, bool notail) {
+    return bx_occupancy(upt, notail) == 2 ? kBxMaxLds2 : kBxMaxLds;
 }
 __host__ __device__ inline int bx_qw(int w) { return (w + 3) >> 2; }
 __host__ __device__ inline int bx_pm(int w) { return bx_qw(w) + 2; }      // I patch dwords per row
@@ -374,7 +379,8 @@ static_assert(lg_scr_bytes() + lg_tiles_a_bytes(kLgTQs[0]) <= kMaxLdsBytes &&
                   lg_scr_bytes() + lg_tiles_a_bytes(kLgTQs[1]) <= kMaxLdsBytes,
               "kLgTQs: a large-window tile plan exceeds 160 KB");
 static_assert(kLgJrMaxLds > 0 && kLgJrMaxLds <= kMaxLdsBytes, "PSN_LG_JR_MAX_KB exceeds 160 KB");
-static_assert(kBxMaxLds <= kMaxLdsBytes && kBxLdsTarget <= kBxMaxLds, "box-kernel LDS caps exceed 160 KB");
+static_assert(kBxMaxLds <= kMaxLdsBytes && kBxLdsTarget <= kBxMaxLds && 2 * kBxMaxLds2 <= kMaxLdsBytes,
+              "box-kernel LDS caps exceed 160 KB");
 
 constexpr int kStEPTMax = 4;  // window pixels per thread held in registers by the single-tile kernel
 constexpr int kStMaxLds = 150 * 1024;

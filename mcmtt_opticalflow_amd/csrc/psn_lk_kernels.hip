@@ -3128,6 +3128,7 @@ hipError_t launch_lk_bx(const LkLaunchArgs &a, int total_wgs, int upt, bool nota
         PSN_BX_CASE(8)
         PSN_BX_CASE(10)
         PSN_BX_CASE(12)
+        PSN_BX_CASE(16)
         default: return hipErrorInvalidValue;
     }
 #undef PSN_BX_CASE
@@ -3192,7 +3193,8 @@ hipError_t lk_kernels_init() {
     const void *bx[] = {(const void *)lk_kernel_bx<4, false>, (const void *)lk_kernel_bx<8, false>,
                         (const void *)lk_kernel_bx<10, false>, (const void *)lk_kernel_bx<12, false>,
                         (const void *)lk_kernel_bx<4, true>, (const void *)lk_kernel_bx<8, true>,
-                        (const void *)lk_kernel_bx<10, true>, (const void *)lk_kernel_bx<12, true>};
+                        (const void *)lk_kernel_bx<10, true>, (const void *)lk_kernel_bx<12, true>,
+                        (const void *)lk_kernel_bx<16, false>, (const void *)lk_kernel_bx<16, true>};
     for (const void *f : bx)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds)) != hipSuccess) return e;
     if ((e = lg_kernels_init()) != hipSuccess) return e;

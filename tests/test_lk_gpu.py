@@ -565,3 +565,35 @@ def test_lk_mixed_window_classes_one_call(oracle_mod):
         assert_same((cn[first:first + c], cs_[first:first + c], ce[first:first + c]),
                     tuple(r[:c] if r is not None else None for r in ref), f"counted {win}")
         np.testing.assert_array_equal(cn[first + c:first + n], sentinel[first + c:first + n])
+
+
+@pytest.mark.parametrize("W,H,win,flags,env,kern", [
+    (3840, 2160, (128, 128), 0, {}, "lk_kernel_bx<16, true>"),       # configs[4] Run, backward windows
+    (3840, 2160, (128, 128), 0, {"poison_lds": 1}, "lk_kernel_bx<16, true>"),
+    (1920, 1080, (80, 200), 0, {}, "lk_kernel_bx<16, true>"),        # PETS-sized boxes
+    (1920, 1080, (100, 160), 0, {}, "lk_kernel_bx<16, false>"),      # 100 % 8: the scalar-tail chain
+    (1920, 1080, (100, 160), 0, {"poison_lds": 1}, "lk_kernel_bx<16, false>"),
+    (1920, 1080, (90, 170), ACCUM_SCALAR, {}, "lk_kernel_bx<16, false>"),
+    (1920, 1080, (52, 300), GET_MIN_EIGENVALS, {}, "lk_kernel_bx<16, false>"),
+    (1920, 1080, (64, 200), 0, {}, "lk_kernel_bx<16, true>"),        # 3,200 units: 12.5 per thread
+    (1920, 1080, (72, 160), 0, {}, "lk_kernel_bx<12, true>"),        # 2,880 units: still the 12-unit build
+])
+def test_lk_box_kernel_16_units(oracle_mod, W, H, win, flags, env, kern):
+    """Box windows of 12-16 units of 4 px per thread (<= 4,096 units, two
+    workgroups per CU, 208/242 VGPRs, no scratch) run the 16-unit box kernel
+    instead of the large-window kernel: the oracle's bits, border points
+    included, and the launch's kernel is the one named."""
+    from mcmtt_opticalflow_amd import _lib
+
+    sc, f0, f1 = scene_pair(18, W, H, 96, box_w=win[0], box_h=win[1])
+    border = BORDER_PTS_1080 * np.float32([W / 1920, H / 1080])
+    pts = np.concatenate([sc.points_at(0), border.astype(np.float32)])
+    ref = oracle_ref(oracle_mod, f0, f1, pts, win, 3, flags=flags)
+    L = _lib.load()
+    with glk.LKContext(W, H, ring_slots=1, max_level_cap=3, variants=env) as ctx:
+        ctx.enable_timing(4, 1)
+        gpu = ctx.calc_optical_flow_pyr_lk(f0, f1, pts, win, 3, flags=flags)
+        ctx.sync()
+        tags = {_lib.kernel_of_tag(t) for _, t in _lib.timing_launches(L, ctx.handle, 4)}
+    assert_same(gpu, ref, f"box16 {win} flags {flags} {env}")
+    assert tags == {kern}, tags

@@ -30,7 +30,14 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/pets" -o run --outpu
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pets_fetch" -o run --output-format csv -- python3 "$B" --steps 20 --warmup 3 $P > "$OUT/pets_fetch.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pets_write" -o run --output-format csv -- python3 "$B" --steps 20 --warmup 3 $P > "$OUT/pets_write.log" 2>&1
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY -d "$OUT/pets_sq2" -o run --output-format csv -- python3 "$B" --steps 20 --warmup 3 $P > "$OUT/pets_sq2.log" 2>&1
+# the 4K Tracker2D Run (configs[4] shape: 8 x 4K cameras, 4096 points, 128 x 320 boxes): kernel trace and HBM bytes
+K="--width 3840 --height 2160 --cameras 8 --points 4096 --boxes 64 --no-cpu-baseline --no-secondary --no-legs --no-isolated --steps 6 --warmup 2 --measure-steps 2"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/k4" -o run --output-format csv -- python3 "$B" $K > "$OUT/k4_bench.json" 2> "$OUT/k4.log"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/k4_fetch" -o run --output-format csv -- python3 "$B" $K > "$OUT/k4_fetch.log" 2>&1
 python3 "$ROOT/tools/profile_summary.py" "$OUT" "$ROOT/mcmtt_opticalflow_amd/lib/libpsn_lk.so" "$OUT/profile.json" > "$OUT/profile_summary.log"
 find "$OUT/trace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 find "$OUT/ktrace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_mode_kernel_stats.csv" \;
+find "$OUT/iso" -name '*kernel_stats.csv' -exec cp {} "$OUT/isolated_kernel_stats.csv" \;
+find "$OUT/pets" -name '*kernel_stats.csv' -exec cp {} "$OUT/pets_kernel_stats.csv" \;
+find "$OUT/k4" -name '*kernel_stats.csv' -exec cp {} "$OUT/k4_kernel_stats.csv" \;
 echo "profile $R done"

@@ -170,6 +170,24 @@ def main():
                                                                    "compute")},
                                 "note": "bench.py --box-dist pets under --kernel-trace (the timed frames plus warm-up "
                                         "and measurement frames); busy_us = union of a kernel's launch intervals"}
+    if os.path.isdir(os.path.join(d, "k4")):
+        kk, span = trace_stats(os.path.join(d, "k4"))
+        fetch4, _ = counters(os.path.join(d, "k4_fetch"))
+        for k, e in kk.items():
+            fv = fetch4.get(k, {}).get("FETCH_SIZE", [])
+            if fv:
+                e["fetch_bytes_per_launch"] = round(mean(fv) * 1024 * ff)
+        meta = {}
+        if os.path.exists(os.path.join(d, "k4_bench.json")):
+            try:
+                meta = json.loads(open(os.path.join(d, "k4_bench.json")).read().strip().splitlines()[-1])
+            except (ValueError, IndexError):
+                meta = {}
+        extra["tracker_4k"] = {"kernels": dict(sorted(kk.items(), key=lambda kv: -kv[1]["busy_us"])),
+                               "trace_span_us": span,
+                               "bench": {k: meta.get(k) for k in ("value", "unit", "ms_per_step", "steps", "warmup")},
+                               "note": "bench.py at 3840x2160, 8 cameras x 4096 points, 128x320 boxes under "
+                                       "--kernel-trace; fetch_bytes_per_launch from a FETCH_SIZE pass (read_u8 factor)"}
     summary = {"lib_sha16": hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16],
                "calibration": cal, "kernels": dict(sorted(kernels.items(), key=lambda kv: -kv[1].get("share_pct", 0))),
                **extra,
