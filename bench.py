@@ -1019,55 +1019,79 @@ def tracker_main(args):
         dist.destroy_process_group()
 
 
+def run_child(argv, timeout=600):
+    """One bench.py line in a fresh process (one rank, this GPU): each leg starts
+    from the same process state as the default line -- streams, their hardware
+    queues, host and device allocations of earlier legs do not carry over (a
+    configs[4] leg after five Tracker2D legs in one process measured 1,199 vs
+    2,053 frames/s alone)."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    sys.stderr.write(p.stderr[-4000:])
+    if p.returncode != 0:
+        raise RuntimeError(f"bench leg {argv} failed ({p.returncode})")
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def child_args(args, **over):
+    """argv of a child line: this run's shared options plus the leg's own."""
+    base = ["--no-legs", "--no-secondary", "--no-cpu-baseline", "--no-isolated", "--period", str(args.period),
+            "--measure-steps", str(args.measure_steps), "--profile", args.profile]
+    if args.lib_dir:
+        base += ["--lib-dir", args.lib_dir]
+    for k, v in over.items():
+        base += [f"--{k.replace('_', '-')}", str(v)]
+    return base
+
+
 def tracker_legs(args, profile):
-    """Extra single-GPU lines of the default run: configs[3] on one GPU (8 cameras
-    x 2048 points, the strong-scaling run's N=1), the GridFAST Run, PETS-like mixed
-    boxes, the realistic Run (GridFAST + PETS boxes), configs[4]."""
+    """Extra single-GPU lines of the default run, each in its own process
+    (run_child): configs[3] on one GPU (8 cameras x 2048 points, the
+    strong-scaling run's N=1), the GridFAST Run, PETS-like mixed boxes, the
+    realistic Run (GridFAST + PETS boxes, with its CPU baseline), configs[4]
+    (host and HBM frames), and configs[4] through the whole Tracker2D Run."""
     legs = {}
-    a3 = argparse.Namespace(**{**vars(args), "total_cameras": 8, "points": 2048, "boxes": 32, "verify": False,
-                               "isolated": False})
-    r3 = tracker_run(a3, steps=args.leg_steps, warmup=3)
-    l3 = tracker_line(a3, r3, 1, 8, "strong", None)
+    steps = str(args.leg_steps)
+    l3 = run_child(child_args(args, total_cameras=8, points=2048, boxes=32, steps=steps, warmup=3))
     legs["configs3_1gpu"] = {k: l3[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["configs3_1gpu"]["roofline"] = {k: l3["roofline"].get(k) for k in ("kernel", "achieved", "frac",
                                                                             "avg_launch_us", "per_kernel_us")}
-    ag = argparse.Namespace(**{**vars(args), "features": "gridfast", "verify": False, "isolated": False})
-    rg = tracker_run(ag, steps=args.leg_steps, warmup=3)
-    lg = tracker_line(ag, rg, 1, args.cameras, "weak", None)
+    lg = run_child(child_args(args, features="gridfast", steps=steps, warmup=3))
     legs["gridfast"] = {k: lg[k] for k in ("value", "unit", "ms_per_step", "steps", "config")}
-    am = argparse.Namespace(**{**vars(args), "box_dist": "pets", "verify": False, "isolated": False})
-    rm = tracker_run(am, steps=args.leg_steps, warmup=3)
-    lm = tracker_line(am, rm, 1, args.cameras, "weak", None)
+    lm = run_child(child_args(args, box_dist="pets", steps=steps, warmup=3))
     legs["mixed_boxes"] = {k: lm[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["mixed_boxes"]["lk_launches"] = {k: lm["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
+    am = argparse.Namespace(**{**vars(args), "box_dist": "pets", "verify": False, "isolated": False})
     legs["mixed_boxes"]["roofline"] = mixed_roofline(am, lm, profile)
     # the reference Run's real per-frame work together (PSNWhere_Tracker2D.cpp:735-757, 776-782,
     # 871-877): GridFAST per detection feeding PETS-sized box windows
-    ar = argparse.Namespace(**{**vars(args), "features": "gridfast", "box_dist": "pets", "verify": False,
-                               "isolated": False})
-    rr = tracker_run(ar, steps=args.leg_steps, warmup=3)
-    lr = tracker_line(ar, rr, 1, args.cameras, "weak", None)
+    lr = run_child(child_args(args, features="gridfast", box_dist="pets", steps=steps, warmup=3))
     legs["realistic"] = {k: lr[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
     legs["realistic"]["lk_launches"] = {k: lr["roofline"].get(k) for k in ("kernel", "avg_launch_us", "per_kernel_us")}
     if not args.no_cpu_baseline:  # the reference's real per-frame work on the host cores (oracle restatement)
         progress("realistic leg: cpu baseline")
+        ar = argparse.Namespace(**{**vars(args), "features": "gridfast", "box_dist": "pets"})
         cb = tracker_cpu_baseline(ar, legs=("share", "single"))
         legs["realistic"]["cpu_baseline"] = cb
         legs["realistic"]["speedup_vs_cpu"] = round(lr["value"] / cb["value"], 1)
         legs["realistic"]["speedup_vs_cpu_single_thread"] = round(lr["value"] / cb["single_thread"], 1)
-    legs["config4"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3)["line"]
-    legs["config4_frames_in_hbm"] = config4_run(args, 1, 0, 0, steps=max(args.leg_steps // 2, 10), warmup=3,
-                                                ingest="hbm")["line"]
+    c4_steps = str(max(args.leg_steps // 2, 10))
+    for name, ingest in (("config4", "host"), ("config4_frames_in_hbm", "hbm")):
+        l4 = run_child(child_args(args, mode="config4", c4_ingest=ingest, steps=c4_steps, warmup=3))
+        legs[name] = {"workload": l4["config"]["workload"], "ingest": ingest,
+                      **{k: l4[k] for k in ("value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "roofline")}}
     # configs[4] through the whole Tracker2D Run: 8 x 4K BGR cameras, 4096 points per camera
-    # (64 detections x 64), 128 x 320 boxes (SURVEY 8(d)): 128 x 128 backward and 128 x 320
-    # forward windows -- the large-window kernel
-    a4 = argparse.Namespace(**{**vars(args), "width": 3840, "height": 2160, "cameras": 8, "points": 4096,
-                               "boxes": 64, "verify": False, "box_dist": "uniform", "isolated": False})
-    r4 = tracker_run(a4, steps=max(args.leg_steps // 8, 5), warmup=2)
-    l4 = tracker_line(a4, r4, 1, 8, "weak", None)
-    legs["config4_tracker"] = {k: l4[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
-    legs["config4_tracker"]["lk_launches"] = {k: l4["roofline"].get(k) for k in ("kernel", "avg_launch_us",
-                                                                               "per_kernel_us")}
+    # (64 detections x 64), 128 x 320 boxes (SURVEY 8(d)): 128 x 128 backward windows (the
+    # 16-unit box kernel) and 128 x 320 forward windows (the large-window kernel)
+    l4t = run_child(child_args(args, width=3840, height=2160, cameras=8, points=4096, boxes=64,
+                               steps=max(args.leg_steps // 8, 5), warmup=2))
+    legs["config4_tracker"] = {k: l4t[k] for k in ("value", "unit", "ms_per_step", "steps", "config", "compute")}
+    legs["config4_tracker"]["lk_launches"] = {k: l4t["roofline"].get(k) for k in ("kernel", "avg_launch_us",
+                                                                                 "per_kernel_us")}
+    legs["note"] = "each leg is a bench.py line of its own process (run_child)"
     return legs
 
 
@@ -1235,14 +1259,12 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
 
 
 def kernel_secondary(args):
-    r = kernel_run(args, 400, 20, C=max(1, args.kcameras), N=args.kpoints)
-    ach = r["launch_bytes"] / (r["lk_us"] * 1e-6) / 1e9
+    """BASELINE.json configs[1] (--mode kernel) as a line of its own process."""
+    l1 = run_child(child_args(args, mode="kernel", steps=400, warmup=20, kcameras=max(1, args.kcameras),
+                              kpoints=args.kpoints))
     return {"workload": "BASELINE.json configs[1]: 1 camera, 1920x1080 gray resident in HBM, 512 points, 4 levels, "
                         "21x21 window, fused pyramid build + LK + propagation",
-            "value": round(r["fps"], 2), "unit": "frames/s", "ms_per_step": round(r["ms_per_step"], 5),
-            "roofline": {"kernel": "lk_kernel_st+fused_pyramid", "bound": "latency", "achieved": round(ach, 2),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 5),
-                         "bytes_per_launch": r["launch_bytes"], "avg_launch_us": round(r["lk_us"], 3)}}
+            **{k: l1[k] for k in ("value", "unit", "ms_per_step", "roofline")}}
 
 
 def config4_run(args, world, rank, local_rank, steps, warmup, ingest="host"):
@@ -1283,7 +1305,7 @@ def kernel_main(args):
     # all-gather is the library's RCCL communicator (psn_comm)
     init_control_plane(world)
     if args.mode == "config4":
-        res = config4_run(args, world, rank, local_rank, args.steps, args.warmup)
+        res = config4_run(args, world, rank, local_rank, args.steps, args.warmup, ingest=args.c4_ingest)
         if rank == 0:
             line = res["line"]
             out = {"metric": METRIC, "value": line["value"], "unit": "frames/s", "n_gpus": world, "steps": args.steps,
@@ -1411,6 +1433,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-legs", action="store_true")
     ap.add_argument("--dry-run", action="store_true")
     ap.add_argument("--lib-dir", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--runtime", choices=["rocm", "torch"], default="rocm", help=argparse.SUPPRESS)
+    ap.add_argument("--c4-ingest", choices=["host", "hbm"], default="host",
+                    help="--mode config4: BGR frames uploaded from pinned host memory every frame, or gray frames "
+                         "resident in HBM")
     ap.add_argument("--profile", default=DEFAULT_PROFILE,
                     help="round profile summary (tools/profile_summary.py) for roofline.traffic / valu")
     args = ap.parse_args(argv)
@@ -1433,6 +1459,8 @@ def main():
     # plane): one HIP/HSA/RCCL runtime in this process, ROCm's (psn_runtime.cpp)
     from mcmtt_opticalflow_amd import _lib
 
+    if args.runtime == "torch":  # diagnostic: torch first, so the library binds torch's bundled ROCm runtime
+        import torch  # noqa: F401
     if args.lib_dir:  # A/B experiments: another build of both libraries (tools/gpu_ab.sh)
         from mcmtt_opticalflow_amd import tracker2d
 
