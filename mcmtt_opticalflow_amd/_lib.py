@@ -185,6 +185,7 @@ def load(path: str | None = None):
     L.psn_lk_track.argtypes = [vp, ctypes.POINTER(LkQuery), ip, fp, fp, u8p, fp]
     L.psn_lk_track_device.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp]
     L.psn_lk_track_device_counted.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, vp, vp, vp, vp]
+    L.psn_lk_track_device_counted_strided.argtypes = [vp, ctypes.POINTER(LkQuery), ip, vp, ip, vp, vp, vp, vp]
     L.psn_calc_optical_flow_pyr_lk.argtypes = [vp, u8p, u8p, ip, fp, fp, u8p, fp, ip, ctypes.POINTER(LkParams)]
     L.psn_lk_read_level.argtypes = [vp, ip, ip, u8p, ip]
     L.psn_lk_level_size.argtypes = [vp, ip, ctypes.POINTER(ip), ctypes.POINTER(ip)]

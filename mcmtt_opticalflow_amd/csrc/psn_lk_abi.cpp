@@ -1033,6 +1033,7 @@ static int launch_group(psn_lk_ctx *c, std::vector<PlannedQuery *> &grp, int cls
     a.stamps = c->d_stamps;
     a.samples = c->count_samples ? c->d_samples : nullptr;
     a.counts = d_counts;
+    a.count_stride = count_stride;
     int wgs = 0, maxpx = 0, rows_ow = 0, lds_ow = 0, lds = 0;
     for (size_t i = 0; i < grp.size(); i++) {
         PlannedQuery &pq = *grp[i];
@@ -1194,6 +1195,55 @@ static int track_device_impl(psn_lk_ctx *c, const psn_lk_query *q, int nq, const
                 if (rc) return rc;
                 pq = lq;
             }
+    // Consecutive caller queries with the same plan and the same point count,
+    // their point blocks a constant stride apart, become one merged query of
+    // sub-queries (LkQueryDev::sub_pts; each keeps its points, its device count
+    // and its result slots, so the outputs are the same bits). Tracker2D's uniform
+    // boxes are one query per camera then, not one per detection, and a call of
+    // more than kMaxQueries detections -- configs[3]: 8 cameras x 32, the 4K Run:
+    // 8 x 64 -- is one launch per kernel class instead of one per 32 detections,
+    // each with its own tail.
+    if (plan.size() > 1) {
+        auto same_plan = [](const PlannedQuery &x, const PlannedQuery &y) {
+            const psn::LkQueryDev &a = x.d, &b = y.d;
+            return x.cls == y.cls && x.key == y.key && a.prev_slot == b.prev_slot && a.next_slot == b.next_slot &&
+                   a.num_pts == b.num_pts && a.win_w == b.win_w && a.win_h == b.win_h &&
+                   a.max_level == b.max_level && a.max_count == b.max_count && a.flags == b.flags &&
+                   a.tile_rows == b.tile_rows && a.min_eig == b.min_eig && a.eps2 == b.eps2 && a.dv_w == b.dv_w &&
+                   a.dv_dw == b.dv_dw && a.dv_pm == b.dv_pm && a.dv_jrw == b.dv_jrw && a.dv_jrw4 == b.dv_jrw4 &&
+                   a.dv_g == b.dv_g && a.dv_cw == b.dv_cw && a.ow_g == b.ow_g && a.ow_rg == b.ow_rg &&
+                   a.bx_tre == b.bx_tre && a.bx_hw == b.bx_hw && a.dv_bxpm == b.dv_bxpm && a.dv_bxjr == b.dv_bxjr &&
+                   x.single == y.single && x.st_lds == y.st_lds && x.ow_rows == y.ow_rows && x.ow_lds == y.ow_lds &&
+                   x.ovl_lds == y.ovl_lds && x.bx_upt == y.bx_upt && x.bx_lds == y.bx_lds &&
+                   x.tiled_tr == y.tiled_tr && x.lg_tr == y.lg_tr && x.lg_jr == y.lg_jr && x.lg_tq == y.lg_tq;
+        };
+        size_t o = 0;
+        int nsub = 1, stride = 0;  // sub-queries of plan[o] so far, their point stride
+        for (size_t i = 1; i < plan.size(); i++) {
+            const PlannedQuery &f = plan[o], &x = plan[i];
+            const int sp = nsub == 1 ? x.d.pt_begin - f.d.pt_begin : stride;
+            if (same_plan(f, x) && x.src == f.src + nsub && sp >= f.d.num_pts && sp > 0 &&
+                x.d.pt_begin == f.d.pt_begin + nsub * sp) {
+                stride = sp;
+                nsub++;
+                continue;
+            }
+            if (nsub > 1) {
+                plan[o].d.sub_pts = plan[o].d.num_pts;
+                plan[o].d.sub_pstride = stride;
+                plan[o].d.num_pts *= nsub;
+            }
+            plan[++o] = plan[i];
+            nsub = 1;
+            stride = 0;
+        }
+        if (nsub > 1) {
+            plan[o].d.sub_pts = plan[o].d.num_pts;
+            plan[o].d.sub_pstride = stride;
+            plan[o].d.num_pts *= nsub;
+        }
+        plan.resize(o + 1);
+    }
     // slots built on the ingest stream must be complete before the LK reads them;
     // a deferred build of a slot this call reads runs first, as its own launch
     std::vector<int> &used = c->used_slots;  // distinct slots this call reads

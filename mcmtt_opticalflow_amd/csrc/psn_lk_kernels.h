@@ -56,7 +56,25 @@ struct LkQueryDev {
         int st_ovl; // single-tile one-wave kernel: 1 = the finer levels' A phase runs beside the iterations
     };
     unsigned dv_bxpm, dv_bxjr;
+    // a merged query (sub_pts > 0): sub-queries of sub_pts points each, sub-query
+    // j's points from pt_begin + j * sub_pstride, its device count at
+    // counts[qidx + j * LkLaunchArgs::count_stride] (the caller's queries k..k+n-1
+    // of one plan; 0: one query)
+    int sub_pts, sub_pstride;
 };
+// Workgroup g's point in query Q (g - Q.wg_begin >= 0), or -1 when it is past
+// its (sub-)query's device count
+__device__ __forceinline__ int lk_query_point(const LkQueryDev &Q, const int *counts, int count_stride, int g) {
+    int loc = g - Q.wg_begin;
+    if (Q.sub_pts > 0) {
+        const int sub = loc / Q.sub_pts;
+        loc -= sub * Q.sub_pts;
+        if (counts && loc >= counts[Q.qidx + sub * count_stride]) return -1;
+        return Q.pt_begin + sub * Q.sub_pstride + loc;
+    }
+    if (counts && loc >= counts[Q.qidx]) return -1;
+    return Q.pt_begin + loc;
+}
 __host__ __device__ inline unsigned div_magic(int d) { return d > 0 ? ((1u << 22) + (unsigned)d - 1u) / (unsigned)d : 0u; }
 
 // Ring geometry as kernel arguments (every slot has the same level layout):
@@ -83,6 +101,7 @@ struct LkLaunchArgs {
     // capacity): workgroups past a query's count exit at once (device-side
     // chains whose counts come from a previous kernel)
     const int *counts;
+    int count_stride;        // counts of consecutive caller queries are count_stride apart
     LkQueryDev q[kMaxQueries];
     // Deferred pyramid build fused into this launch (single-tile kernel only):
     // workgroups that finish their point pull top-level tiles of `pyr` from

@@ -266,8 +266,8 @@ __global__ __launch_bounds__(NT) void lk_kernel(LkLaunchArgs A) {
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
     const LkQueryDev &Q = A.q[qi];
-    if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) return;  // past the query's device count
-    const int pi = Q.pt_begin + (g - Q.wg_begin);
+    const int pi = lk_query_point(Q, A.counts, A.count_stride, g);
+    if (pi < 0) return;  // past the query's device count
     const int w = Q.win_w, h = Q.win_h;
     const int TR = Q.tile_rows;
     const int maxL = Q.max_level;
@@ -1076,8 +1076,8 @@ __global__ __launch_bounds__(NT, OCC) void lk_kernel_st(LkLaunchArgs A) {
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
     const LkQueryDev &Q = A.q[qi];
-    if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) return;  // past the query's device count
-    const int pi = Q.pt_begin + (g - Q.wg_begin);
+    const int pi = lk_query_point(Q, A.counts, A.count_stride, g);
+    if (pi < 0) return;  // past the query's device count
     const int w = Q.win_w, h = Q.win_h, wh = w * h;
     const int maxL = Q.max_level, nlev = maxL + 1;
     const int flags = Q.flags;
@@ -2081,8 +2081,8 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT, NOTAIL)) void lk_kernel_bx
     int qi = 0;
     while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
     const LkQueryDev &Q = A.q[qi];
-    if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) return;  // past the query's device count
-    const int pi = Q.pt_begin + (g - Q.wg_begin);
+    const int pi = lk_query_point(Q, A.counts, A.count_stride, g);
+    if (pi < 0) return;  // past the query's device count
     const int w = Q.win_w, h = Q.win_h;
     const int maxL = Q.max_level, flags = Q.flags;
     const bool sse = (flags & PSN_LK_ACCUM_SCALAR) == 0;

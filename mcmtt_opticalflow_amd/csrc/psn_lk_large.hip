@@ -292,8 +292,8 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
         int qi = 0;
         while (qi + 1 < A.nq && g >= A.q[qi + 1].wg_begin) qi++;
         const LkQueryDev &Q = A.q[qi];
-        if (A.counts && g - Q.wg_begin >= A.counts[Q.qidx]) continue;  // past the query's device count
-        const int pi = Q.pt_begin + (g - Q.wg_begin);
+        const int pi = lk_query_point(Q, A.counts, A.count_stride, g);
+        if (pi < 0) continue;  // past the query's device count
         const int w = Q.win_w, h = Q.win_h, TR = Q.tile_rows;
         const int maxL = Q.max_level, flags = Q.flags;
         const bool sse = (flags & PSN_LK_ACCUM_SCALAR) == 0;

@@ -194,6 +194,14 @@ class LKContext:
         self._check(self._L.psn_lk_track_device_counted(self._h, arr, len(queries), d_counts, d_prev, d_next,
                                                         d_status, d_err), "track_device_counted")
 
+    def track_device_counted_strided(self, queries: list[LkQuery], d_counts: int, count_stride: int, d_prev: int,
+                                     d_next: int, d_status: int, d_err: int | None):
+        """As track_device_counted with query i's count at d_counts[i * count_stride]."""
+        arr = (LkQuery * max(len(queries), 1))(*queries)
+        self._check(self._L.psn_lk_track_device_counted_strided(self._h, arr, len(queries), d_counts, count_stride,
+                                                                d_prev, d_next, d_status, d_err),
+                    "track_device_counted_strided")
+
     def enable_timing(self, capacity: int = 1024, every: int = 1):
         """HIP-event timing of every `every`-th push (pyramid launch) / track (LK launch) call."""
         self._check(self._L.psn_lk_enable_timing(self._h, int(capacity), int(every)), "enable_timing")

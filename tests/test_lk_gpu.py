@@ -597,3 +597,50 @@ def test_lk_box_kernel_16_units(oracle_mod, W, H, win, flags, env, kern):
         tags = {_lib.kernel_of_tag(t) for _, t in _lib.timing_launches(L, ctx.handle, 4)}
     assert_same(gpu, ref, f"box16 {win} flags {flags} {env}")
     assert tags == {kern}, tags
+
+
+@pytest.mark.parametrize("stride", [1, 3])
+def test_lk_merged_counted_queries(oracle_mod, stride):
+    """Many counted queries of one plan (more than the 32 of a launch's table)
+    merge into sub-queries of one launch (LkQueryDev::sub_pts): blocks of 12-point
+    capacity 16 points apart, device counts 0..12 at stride `stride`, a window
+    change in the middle (a second merged run), an empty query between runs
+    (no merge across it), windows of the single-tile, box and large kernels.
+    Every point inside a count matches the oracle bit for bit; the rest of every
+    block and the gaps stay untouched."""
+    import hiprt
+
+    W, H, CAP, GAP = 1920, 1080, 12, 16
+    sc, f0, f1 = scene_pair(19, W, H, 1500, box_w=100, box_h=250)
+    wins = [(21, 21)] * 30 + [(64, 160)] * 40 + [(100, 250)] * 6 + [(64, 160)] * 14
+    nq = len(wins)
+    pts = sc.points_at(0)[:GAP * nq]
+    rng = np.random.default_rng(5)
+    counts = rng.integers(0, CAP + 1, nq).astype(np.int32)
+    counts[[3, 31, 77]] = [0, CAP, CAP]
+    dc = np.zeros(nq * stride, np.int32)
+    dc[::stride] = counts
+    sentinel = np.full(pts.shape, -7.0, np.float32)
+    d_f0, d_f1 = hiprt.DeviceBuffer.from_array(f0), hiprt.DeviceBuffer.from_array(f1)
+    d_p, d_n = hiprt.DeviceBuffer.from_array(pts), hiprt.DeviceBuffer.from_array(sentinel)
+    d_s, d_e = hiprt.DeviceBuffer.from_array(np.full(len(pts), 9, np.uint8)), hiprt.DeviceBuffer(4 * len(pts))
+    d_c = hiprt.DeviceBuffer.from_array(dc)
+    qs = [glk.make_query(0, 1, GAP * i, CAP if i != 50 else 0, glk.make_params(w, 3)) for i, w in enumerate(wins)]
+    with glk.LKContext(W, H, ring_slots=2, max_level_cap=3) as ctx:
+        ctx.push_frame_device(0, d_f0.addr, W, 1)
+        ctx.push_frame_device(1, d_f1.addr, W, 1)
+        if stride == 1:
+            ctx.track_device_counted(qs, d_c.addr, d_p.addr, d_n.addr, d_s.addr, d_e.addr)
+        else:
+            ctx.track_device_counted_strided(qs, d_c.addr, stride, d_p.addr, d_n.addr, d_s.addr, d_e.addr)
+        ctx.sync()
+    g_n, g_s = d_n.to_array(pts.shape, np.float32), d_s.to_array(len(pts), np.uint8)
+    g_e = d_e.to_array(len(pts), np.float32)
+    for i, (w, c) in enumerate(zip(wins, counts)):
+        lo = GAP * i
+        c = 0 if i == 50 else int(c)
+        if c:
+            ref = oracle_ref(oracle_mod, f0, f1, pts[lo:lo + c], w, 3)
+            assert_same((g_n[lo:lo + c], g_s[lo:lo + c], g_e[lo:lo + c]), ref, f"query {i} {w}")
+        np.testing.assert_array_equal(g_n[lo + c:lo + GAP], sentinel[lo + c:lo + GAP], f"query {i} untouched")
+        assert (g_s[lo + c:lo + GAP] == 9).all(), i
