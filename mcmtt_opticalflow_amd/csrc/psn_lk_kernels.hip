@@ -2143,9 +2143,10 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT, NOTAIL)) void lk_kernel_bx
     const float FLT_SCALE = 1.f / (1 << 20);
     int par = 0;
 #ifdef PSN_LK_STAMPS
-    unsigned long long bx_acc[16] = {}, bx_t = 0, bx_t0 = 0;
+    unsigned long long bx_acc[16] = {}, bx_t = 0, bx_t0 = 0, bx_r0 = 0;
     BX_CLK(bx_t0);
     bx_t = bx_t0;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(bx_r0) : : "memory");  // 100 MHz
 #endif
 
     unsigned IP[UPT][2], XP[UPT][2], YP[UPT][2];  // I, Ix, Iy as packed 16-bit pairs (pixels 0,1 and 2,3)
@@ -3096,8 +3097,18 @@ __global__ __launch_bounds__(kBxNT, bx_occupancy(UPT, NOTAIL)) void lk_kernel_bx
         unsigned long long t_end;
         BX_CLK(t_end);
         bx_acc[15] = t_end - bx_t0;
-        if (tid == 0 && A.stamps)  // thread 0: also the chain lane of the tile stamps 12-14
+        unsigned long long r1;
+        unsigned hwid, xcc;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1) : : "memory");
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (tid == 0 && A.stamps) {  // thread 0: also the chain lane of the tile stamps 12-14
             for (int i = 0; i < 16; i++) A.stamps[(size_t)g * 64 + i] = bx_acc[i];
+            // residency: realtime (100 MHz) start / end and the CU it ran on
+            A.stamps[(size_t)g * 64 + 16] = bx_r0;
+            A.stamps[(size_t)g * 64 + 17] = r1;
+            A.stamps[(size_t)g * 64 + 18] = ((unsigned long long)xcc << 32) | hwid;
+        }
     }
 #endif
     if (tid == 0) {

@@ -59,6 +59,38 @@ def main():
     it = max(s[:, 10].sum(), 1)
     out["per_iteration"] = {k: round(float(ph[:, i].sum() / it), 1) for i, k in enumerate(PHASES) if i >= 3}
     out["per_iteration"]["b_publish_only"] = round(float(s[:, 9].sum() / it), 1)  # inside b_publish_eval
+    # residency (stamps 16-18: s_memrealtime at 100 MHz at the start / end, HW_ID and
+    # XCC_ID): how many workgroups each CU held at once, and the idle CU time
+    r0, r1, hw = s[:, 16], s[:, 17], s[:, 18]
+    if r1.max() > 0:
+        hwid, xcc = hw & 0xffffffff, hw >> 32
+        cu = (xcc << 16) | (((hwid >> 13) & 7) << 8) | (((hwid >> 12) & 1) << 4) | ((hwid >> 8) & 15)
+        t0 = int(r0.min())
+        span = int(r1.max()) - t0
+        conc, per_cu = [], []
+        for c in np.unique(cu):
+            m = cu == c
+            ev = sorted([(int(a), 1) for a in r0[m]] + [(int(b), -1) for b in r1[m]])
+            cur = mx = 0
+            busy = last = 0
+            for t, d in ev:
+                if cur > 0:
+                    busy += t - last
+                cur += d
+                last = t
+                mx = max(mx, cur)
+            dur = int((r1[m] - r0[m]).sum())
+            per_cu.append((int(m.sum()), mx, dur / max(busy, 1), busy))
+        arr = np.array(per_cu, float)
+        out["residency"] = {"span_us": round(span / 100.0, 1), "cus": int(len(per_cu)),
+                            "wgs_per_cu": [int(arr[:, 0].min()), float(arr[:, 0].mean()), int(arr[:, 0].max())],
+                            "max_concurrent_per_cu": [int(arr[:, 1].min()), int(arr[:, 1].max())],
+                            "mean_concurrency_while_busy": round(float(arr[:, 2].mean()), 3),
+                            "cu_busy_frac_of_span": round(float(arr[:, 3].mean() / max(span, 1)), 3),
+                            "wg_us_mean": round(float((r1 - r0).mean()) / 100.0, 1),
+                            "wg_us_max": round(float((r1 - r0).max()) / 100.0, 1),
+                            "clock_ghz": round(float(tot.mean() / max((r1 - r0).mean(), 1) / 10.0), 3),
+                            "last_start_us": round((int(r0.max()) - t0) / 100.0, 1)}
     print(json.dumps(out, indent=1))
 
 
