@@ -260,15 +260,7 @@ __device__ __forceinline__ float lg_tiles(int qs, int NQ, float *buf, int nch, f
     } while (0)
 #endif
 
-#ifndef PSN_LG_MB
-#define PSN_LG_MB 4
-#endif
-constexpr int kLgMB = PSN_LG_MB;  // quads per batch of slot loads in the passes over the window
-// main pass: the next batch's slot loads issued before the current batch is
-// summed (two register buffers), so a batch waits for its loads only once per pass
-#ifndef PSN_LG_PIPE
-#define PSN_LG_PIPE 0
-#endif
+constexpr int kLgMB = 4;  // quads per batch of slot loads in the passes over the window
 
 // Minimum waves per SIMD of the build (__launch_bounds__: k workgroups per CU of
 // 256 threads = k waves per SIMD; a build parameter for occupancy A/Bs)
@@ -628,32 +620,6 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
                     };
                     // batches of kLgMB quads: their slot loads in flight together
                     int k = 0;
-#if PSN_LG_PIPE
-                    {
-                        uint2 ipa[kLgMB], xpa[kLgMB], ypa[kLgMB], ipb[kLgMB], xpb[kLgMB], ypb[kLgMB];
-                        auto ld = [&](uint2(&ip)[kLgMB], uint2(&xp)[kLgMB], uint2(&yp)[kLgMB], int kk) {
-#pragma unroll
-                            for (int u = 0; u < kLgMB; u++) {
-                                const int ix = (kk + u) * NT + tid;
-                                ip[u] = IPs[ix];
-                                xp[u] = XPs[ix];
-                                yp[u] = YPs[ix];
-                            }
-                        };
-                        if (kLgMB <= cnt) ld(ipa, xpa, ypa, 0);
-                        while (k + kLgMB <= cnt) {
-                            if (k + 2 * kLgMB <= cnt) ld(ipb, xpb, ypb, k + kLgMB);
-#pragma unroll
-                            for (int u = 0; u < kLgMB; u++) quad(ipa[u], xpa[u], ypa[u]);
-                            k += kLgMB;
-                            if (k + kLgMB > cnt) break;
-                            if (k + 2 * kLgMB <= cnt) ld(ipa, xpa, ypa, k + kLgMB);
-#pragma unroll
-                            for (int u = 0; u < kLgMB; u++) quad(ipb[u], xpb[u], ypb[u]);
-                            k += kLgMB;
-                        }
-                    }
-#else
                     for (; k + kLgMB <= cnt; k += kLgMB) {
                         uint2 ip[kLgMB], xp[kLgMB], yp[kLgMB];
 #pragma unroll
@@ -666,7 +632,6 @@ __global__ __launch_bounds__(kLgNT, PSN_LG_WAVES) void lk_kernel_lg(LkLaunchArgs
 #pragma unroll
                         for (int u = 0; u < kLgMB; u++) quad(ip[u], xp[u], yp[u]);
                     }
-#endif
                     for (; k < cnt; k++) {
                         const int ix = k * NT + tid;
                         quad(IPs[ix], XPs[ix], YPs[ix]);
