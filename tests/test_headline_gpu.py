@@ -72,3 +72,14 @@ def test_headline_realistic_run_matches_oracle(oracle_mod):
     v = _verify("--features", "gridfast", "--box-dist", "pets", "--cameras", "2", steps=2, warmup=2)
     assert v["mismatches"] == 0, v["first_mismatch"]
     assert v["objects_checked"] >= 2 * 8 * 2
+
+
+def test_4k_tracker_run_matches_oracle(oracle_mod):
+    """The 4K Tracker2D Run (legs.config4_tracker's shape, scaled down): 3840x2160
+    BGR, 128x320 boxes -- the backward chains' 128x128 windows on the 16-unit box
+    kernel, the forward 128x320 windows on the large-window kernel, the
+    detections of a camera merged into one sub-query launch per class."""
+    v = _verify("--width", "3840", "--height", "2160", "--cameras", "2", "--points", "64", "--boxes", "4",
+                steps=2, warmup=2)
+    assert v["mismatches"] == 0, v["first_mismatch"]
+    assert v["objects_checked"] >= 2 * 4 * 3

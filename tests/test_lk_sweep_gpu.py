@@ -78,13 +78,19 @@ def test_lk_random_sweep(oracle_mod, seed):
 def test_lk_random_batched_queries(oracle_mod, seed):
     """Several random queries (each its own window, depth, flags, criteria and
     direction between the two ring slots) in ONE track call: the per-class
-    launches of a mixed call, as Tracker2D issues its backward / forward calls."""
+    launches of a mixed call, as Tracker2D issues its backward / forward calls;
+    runs of repeated queries (contiguous points) merge into sub-queries."""
     rng = np.random.default_rng(9100 + seed)
     W, H = int(rng.integers(640, 1500)), int(rng.integers(480, 1000))
     sc = synth.make_scene(seed % 13, W, H, 200, max_speed=float(rng.uniform(1.0, 5.0)))
     frames = [sc.frame(0), sc.frame(1)]
     specs, first = [], 0
-    for _ in range(int(rng.integers(2, 7))):
+    for _ in range(int(rng.integers(2, 9))):
+        if specs and rng.random() < 0.4:  # the previous query again: merged into sub-queries
+            a, b, _, n, win, ml, flags, crit = specs[-1]
+            specs.append((a, b, first, n, win, ml, flags, crit))
+            first += n
+            continue
         win = _window(rng)
         n = int(rng.integers(0, 30))
         ml = glk.effective_max_level(W, H, win[0], win[1], int(rng.integers(0, 5)))
@@ -93,7 +99,8 @@ def test_lk_random_batched_queries(oracle_mod, seed):
         a = int(rng.integers(0, 2))
         specs.append((a, 1 - a, first, n, win, ml, flags, crit))
         first += n
-    pts = np.concatenate([sc.points_at(0), sc.points_at(1)])[rng.permutation(400)[:max(first, 1)]]
+    pool = np.concatenate([sc.points_at(0), sc.points_at(1)])
+    pts = pool[rng.permutation(len(pool))[:max(first, 1)] % len(pool)]
     var = _VARIANTS[int(rng.integers(0, len(_VARIANTS)))]
     with glk.LKContext(W, H, ring_slots=2, max_level_cap=4, variants=var) as ctx:
         for s, f in enumerate(frames):
