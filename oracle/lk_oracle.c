@@ -623,6 +623,7 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
     const float scale = (float)(1. / (1 << level));
     const int cols = lv->cols, rows = lv->rows;
     const int sse = accum == ORACLE_ACCUM_SSE2;
+    const int exact = accum == ORACLE_ACCUM_EXACT;
     const int stepI = lv->stepI, dstep = lv->dstep;
     int16_t *Iw = ibuf, *dIw = ibuf + win_w * win_h; /* dIw interleaved (Ix, Iy) */
 
@@ -662,6 +663,7 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
 
     float A11 = 0, A12 = 0, A22 = 0;
     float qA11[4] = {0, 0, 0, 0}, qA12[4] = {0, 0, 0, 0}, qA22[4] = {0, 0, 0, 0};
+    long long eA11 = 0, eA12 = 0, eA22 = 0;
     for (int y = 0; y < win_h; y++) {
         const uint8_t *src = lv->I + (long)(y + ipy) * stepI + ipx;
         const int16_t *dsrc = lv->dI + (long)(y + ipy) * dstep + 2 * ipx;
@@ -692,10 +694,21 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
             Iptr[x] = (int16_t)ival;
             dIptr[2 * x] = (int16_t)ixval;
             dIptr[2 * x + 1] = (int16_t)iyval;
+            if (exact) {
+                eA11 += (long long)ixval * ixval;
+                eA12 += (long long)ixval * iyval;
+                eA22 += (long long)iyval * iyval;
+                continue;
+            }
             A11 += (float)(ixval * ixval);
             A12 += (float)(ixval * iyval);
             A22 += (float)(iyval * iyval);
         }
+    }
+    if (exact) {
+        A11 = (float)eA11;
+        A12 = (float)eA12;
+        A22 = (float)eA22;
     }
     if (sse) {
         A11 += qA11[0] + qA11[1] + qA11[2] + qA11[3];
@@ -739,6 +752,7 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
 
         float b1 = 0, b2 = 0;
         float qb0[4] = {0, 0, 0, 0}, qb1[4] = {0, 0, 0, 0};
+        long long eb1 = 0, eb2 = 0;
         if (g_bsum_log || g_chain_log) {
             long long *t1 = (long long *)malloc(sizeof(long long) * 2 * win_w * win_h), *t2 = t1 + win_w * win_h;
             for (int y = 0; y < win_h; y++)
@@ -784,9 +798,18 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
             }
             for (; x < win_w; x++) {
                 int diff = DESCALE(BILIN(Jptr + x, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5) - Iptr[x];
+                if (exact) {
+                    eb1 += (long long)diff * dIptr[2 * x];
+                    eb2 += (long long)diff * dIptr[2 * x + 1];
+                    continue;
+                }
                 b1 += (float)(diff * dIptr[2 * x]);
                 b2 += (float)(diff * dIptr[2 * x + 1]);
             }
+        }
+        if (exact) {
+            b1 = (float)eb1;
+            b2 = (float)eb2;
         }
         if (sse) {
             float bb[4];
@@ -827,14 +850,19 @@ static void lk_point_level(const level_view *lv, int level, int max_level, const
         iw10 = cv_round((1.f - aa) * bb * (float)(1 << W_BITS));
         iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
         float errval = 0.f;
+        long long eerr = 0;
         for (int y = 0; y < win_h; y++) {
             const uint8_t *Jptr = lv->J + (long)(y + iqy) * stepI + iqx;
             const int16_t *Iptr = Iw + y * win_w;
             for (int x = 0; x < win_w; x++) {
                 int diff = DESCALE(BILIN(Jptr + x, stepI, iw00, iw01, iw10, iw11), W_BITS1 - 5) - Iptr[x];
-                errval += fabsf((float)diff);
+                if (exact)
+                    eerr += diff < 0 ? -diff : diff;
+                else
+                    errval += fabsf((float)diff);
             }
         }
+        if (exact) errval = (float)eerr;
         err[i] = errval * 1.f / (float)(32 * win_w * win_h);
     }
 }

@@ -30,6 +30,11 @@ extern "C" {
  * 1 = the scalar (no-SIMD) build: one sequential float chain per sum. */
 #define ORACLE_ACCUM_SSE2 0
 #define ORACLE_ACCUM_SCALAR 1
+/* analysis only (no reference counterpart): A / b / err window sums as exact
+ * int64 integers, each converted to float once -- the order-free sums SURVEY
+ * Appendix A names "int64_exact"; its distance from the SSE2 order is measured
+ * in tests/test_oracle.py::test_exact_sums_vs_sse2_order */
+#define ORACLE_ACCUM_EXACT 2
 
 /* cv::OPTFLOW_* flag values (OpenCV 2.4.6 video/tracking.hpp) */
 #define ORACLE_USE_INITIAL_FLOW 4

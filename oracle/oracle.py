@@ -23,6 +23,7 @@ _lib = None
 
 ACCUM_SSE2 = 0
 ACCUM_SCALAR = 1
+ACCUM_EXACT = 2  # analysis only: order-free int64 window sums (lk_oracle.h ORACLE_ACCUM_EXACT)
 USE_INITIAL_FLOW = 4
 GET_MIN_EIGENVALS = 8
 
