@@ -91,6 +91,13 @@ def main():
                             "wg_us_max": round(float((r1 - r0).max()) / 100.0, 1),
                             "clock_ghz": round(float(tot.mean() / max((r1 - r0).mean(), 1) / 10.0), 3),
                             "last_start_us": round((int(r0.max()) - t0) / 100.0, 1)}
+        # per XCD: the static share of the grid (blockIdx round-robin) and when it ends
+        xs = {}
+        for x in np.unique(xcc):
+            m = xcc == x
+            xs[int(x)] = {"wgs": int(m.sum()), "end_us": round((int(r1[m].max()) - t0) / 100.0, 1),
+                          "wg_us_sum_ms": round(float((r1[m] - r0[m]).sum()) / 1e5, 2)}
+        out["residency"]["per_xcd"] = xs
     print(json.dumps(out, indent=1))
 
 
