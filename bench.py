@@ -1210,6 +1210,7 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     hdr_tab[:, :, 1] = np.arange(t_end, dtype=np.int32)[:, None]
     L = ctx._L
     L.psn_t2d_upload_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    hstream = hip.Stream() if comm is None else None
 
     def step(t):
         cur, prv = ptrs[t % 2], ptrs[(t - 1) % 2]
@@ -1217,7 +1218,9 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
         ctx.track_device(queries[t % R], prv[1], cur[1], cur[3], cur[2])
         if smoother is not None:  # lost points (status 0) are not inserted
             smoother.insert_device(cur[1], 2, cur[3], sg_ptrs[0], sg_ptrs[1])
-        rc = L.psn_t2d_upload_device(cur[0], hdr_pin[t].ctypes.data, 16 * C, stream.handle)
+        # the header bytes are disjoint from what the LK writes: at N = 1 they go on
+        # a stream of their own, beside the launch; N > 1 orders them before the gather
+        rc = L.psn_t2d_upload_device(cur[0], hdr_pin[t].ctypes.data, 16 * C, (hstream or stream).handle)
         if rc:
             raise RuntimeError(f"psn_t2d_upload_device failed ({rc})")
         if comm is not None:
@@ -1247,6 +1250,8 @@ def kernel_run(args, steps, warmup, world=1, rank=0, local_rank=0, C=1, W=1920, 
     if comm is not None:
         pdist.comm_destroy(comm)
     stream.destroy()
+    if hstream is not None:
+        hstream.destroy()
     if pinned is not None:
         pinned.close()
     hdr_alloc.close()
