@@ -296,6 +296,15 @@ int psn_gridfast_detect(psn_lk_ctx *ctx, int slot, const int *rois, int nroi, co
                         uint32_t seed, float *out_xy, int *out_count, int *out_total);
 int psn_gridfast_detect_device(psn_lk_ctx *ctx, int slot, const int *rois, int nroi, const psn_gridfast_params *p,
                                uint32_t seed, float *d_out_xy, int *d_out_count, int *d_out_total);
+/* Several frames' detections at once (PSNWhere_Tracker2D.cpp:734-757 run per
+ * camera): set i = nrois[i] rois on ring slot slots[i]; the sets' rois lie
+ * consecutively in `rois` and their outputs consecutively in the out arrays.
+ * Same results as nset psn_gridfast_detect_device calls at consecutive output
+ * offsets (the shuffle key is the roi's index within its set), in as few
+ * launches as kGfMaxRois (64) rois per launch allow. Async, device pointers. */
+int psn_gridfast_detect_device_sets(psn_lk_ctx *ctx, int nset, const int *slots, const int *nrois, const int *rois,
+                                    const psn_gridfast_params *p, uint32_t seed, float *d_out_xy, int *d_out_count,
+                                    int *d_out_total);
 
 /* ---- multi-GPU: per-camera tracklet slots all-gathered over RCCL/xGMI ----
  * Replaces the in-process std::vector<stTrack2DResult> hand-off into

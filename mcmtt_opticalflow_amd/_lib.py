@@ -204,6 +204,9 @@ def load(path: str | None = None):
     gfa = [vp, ip, vp, ip, ctypes.POINTER(GridFastParams), ctypes.c_uint32, vp, vp, vp]
     L.psn_gridfast_detect.argtypes = gfa
     L.psn_gridfast_detect_device.argtypes = gfa
+    if hasattr(L, "psn_gridfast_detect_device_sets"):  # (absent from the A/B experiments' older builds only)
+        L.psn_gridfast_detect_device_sets.argtypes = [vp, ip, vp, vp, vp, ctypes.POINTER(GridFastParams),
+                                                      ctypes.c_uint32, vp, vp, vp]
     L.psn_sg_create.argtypes = [ip, ip, ip, ip, ip, ctypes.POINTER(vp)]
     L.psn_sg_destroy.argtypes = [vp]
     L.psn_sg_destroy.restype = None

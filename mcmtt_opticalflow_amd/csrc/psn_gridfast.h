@@ -13,10 +13,8 @@ constexpr int kGfMaxLds = 96 * 1024; // dynamic LDS of the per-cell kernel
 constexpr int kGfMaxTotal = 4096;   // maxTotalKeypoints limit (selection sort in LDS)
 
 struct GridFastArgs {
-    const uint8_t *img;  // level 0 of a ring slot (the frame's gray image)
-    int w, h, pitch;
+    int w, h, pitch;     // level 0 of the context's ring slots (every slot alike)
     int nroi;
-    int roi_base;        // index of rois[0] in the caller's array (shuffle key)
     int threshold, nonmax, grid_rows, grid_cols, per_cell, cap;
     int rw_max, strip, list_cap;  // LDS plan: widest region of the launch, strip rows, keypoint list entries
     uint32_t seed;
@@ -26,6 +24,8 @@ struct GridFastArgs {
     int *out_count;      // [nroi] min(total, cap)
     int *out_total;      // [nroi] keypoints before the cap (newKeypoints.size())
     int4 rois[kGfMaxRois];
+    const uint8_t *roi_img[kGfMaxRois];  // level 0 of the roi's ring slot (its frame's gray image)
+    int roi_key[kGfMaxRois];             // the roi's index in its set (shuffle key)
 };
 
 // Dynamic LDS bytes of the per-cell kernel for a plan (rw_max, strip, list_cap).

@@ -143,6 +143,7 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_cell_kernel(GridFastArgs 
     const int cx0 = (cj * A.w) / A.grid_cols, cx1 = ((cj + 1) * A.w) / A.grid_cols;
     const int dy0 = cy0 + 3, dy1 = cy1 - 3, dx0 = cx0 + 3, dx1 = cx1 - 3;
     const int4 roi = A.rois[r];
+    const uint8_t *img = A.roi_img[r];
     const int ax0 = max(dx0, roi.x), ax1 = min(dx1, roi.x + roi.z);
     const int ay0 = max(dy0, roi.y), ay1 = min(dy1, roi.y + roi.w);
     int *cnt = A.cell_cnt + (size_t)r * ncell + cell;
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_cell_kernel(GridFastArgs 
                         dst[k] = -1;
                         if (q < n) {
                             const int yy = fdiv(q, PW, invPW), xx = q - yy * PW;
-                            v[k] = A.img[(size_t)clampi(y0 - 4 + yy, 0, A.h - 1) * A.pitch + clampi(ax0 - 4 + xx, 0, A.w - 1)];
+                            v[k] = img[(size_t)clampi(y0 - 4 + yy, 0, A.h - 1) * A.pitch + clampi(ax0 - 4 + xx, 0, A.w - 1)];
                             dst[k] = yy * PC + xx;
                         }
                     }
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_select_kernel(GridFastArg
     const int n = off[ncell];
     int P = 1;
     while (P < n) P <<= 1;
-    const uint32_t h0 = mix32(A.seed + 0x9e3779b9u * (uint32_t)(A.roi_base + r + 1));
+    const uint32_t h0 = mix32(A.seed + 0x9e3779b9u * (uint32_t)(A.roi_key[r] + 1));
     for (int c = 0; c < ncell; c++) {
         const uint32_t *src = A.cell_kp + ((size_t)r * ncell + c) * A.per_cell;
         for (int j = tid; j < off[c + 1] - off[c]; j += kGfThreads) cand[off[c] + j] = src[j];

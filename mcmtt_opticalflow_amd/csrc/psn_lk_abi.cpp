@@ -654,7 +654,6 @@ static int record_slots_free(psn_lk_ctx *c, const int *slots, int n) {
     if (e->refs == 0) c->ev_free.push_back(e);
     return PSN_LK_OK;
 }
-static int record_slot_free(psn_lk_ctx *c, int slot) { return record_slots_free(c, &slot, 1); }
 
 // Make stream s wait until every recorded read of `slot` is done (before a new build into it).
 static int wait_slot_free(psn_lk_ctx *c, int slot, hipStream_t s) {
@@ -1496,8 +1495,11 @@ void psn_gridfast_default_params(psn_gridfast_params *p) {
     p->cap = 100;  // PSN_2D_FEATURE_MAX_NUM_TRACK (PSNWhere_Tracker2D.cpp:13)
 }
 
-static int gridfast_impl(psn_lk_ctx *c, int slot, const int *rois, int nroi, const psn_gridfast_params *pp,
-                         uint32_t seed, float *d_xy, int *d_cnt, int *d_tot) {
+// nset sets of rois, set i = nrois[i] rois on ring slot slots[i], all sets'
+// rois consecutive in `rois` and in the outputs; a launch covers up to
+// kGfMaxRois rois of any sets (the shuffle key restarts at 0 per set).
+static int gridfast_impl(psn_lk_ctx *c, int nset, const int *slots, const int *nrois, const int *rois,
+                         const psn_gridfast_params *pp, uint32_t seed, float *d_xy, int *d_cnt, int *d_tot) {
     psn_gridfast_params p;
     if (pp)
         p = *pp;
@@ -1509,18 +1511,35 @@ static int gridfast_impl(psn_lk_ctx *c, int slot, const int *rois, int nroi, con
                        p.max_total, p.cap);
     if ((c->width + p.grid_cols - 1) / p.grid_cols - 6 > psn::kGfMaxRegionW)
         return set_err(c, PSN_LK_ERR_UNSUPPORTED, "gridfast: cell width above %d", psn::kGfMaxRegionW + 6);
-    if (slot < 0 || slot >= c->nslots || !c->filled[slot]) return set_err(c, PSN_LK_ERR_SLOT, "slot %d not filled", slot);
+    int nroi = 0;
+    std::vector<int> used;  // distinct slots with rois
+    for (int i = 0; i < nset; i++) {
+        const int slot = slots[i];
+        if (slot < 0 || slot >= c->nslots || !c->filled[slot])
+            return set_err(c, PSN_LK_ERR_SLOT, "slot %d not filled", slot);
+        if (nrois[i] < 0) return set_err(c, PSN_LK_ERR_ARG, "gridfast: set %d has %d rois", i, nrois[i]);
+        nroi += nrois[i];
+        if (nrois[i] > 0 && std::find(used.begin(), used.end(), slot) == used.end()) used.push_back(slot);
+    }
     if (nroi == 0) return PSN_LK_OK;
-    // the frame must be in the slot: a deferred build of it runs first
-    if (c->pend && c->pend_slot == slot) {
-        int rc = flush_pending(c);
+    for (int slot : used) {
+        // the frame must be in the slot: a deferred build of it runs first
+        if (c->pend && c->pend_slot == slot) {
+            int rc = flush_pending(c);
+            if (rc) return rc;
+        }
+        int rc = wait_slot_ready(c, slot);
         if (rc) return rc;
     }
-    int rc = wait_slot_ready(c, slot);
-    if (rc) return rc;
+    std::vector<const uint8_t *> roi_img((size_t)nroi);
+    std::vector<int> roi_key((size_t)nroi);
+    for (int i = 0, k = 0; i < nset; i++)
+        for (int j = 0; j < nrois[i]; j++, k++) {
+            roi_img[k] = c->h_slots[(size_t)slots[i] * psn::kMaxLevels].p;
+            roi_key[k] = j;
+        }
     psn::GridFastArgs a{};
-    const LevelDev &L = c->h_slots[(size_t)slot * psn::kMaxLevels];
-    a.img = L.p;
+    const LevelDev &L = c->h_slots[(size_t)used[0] * psn::kMaxLevels];
     a.w = L.w;
     a.h = L.h;
     a.pitch = L.pitch;
@@ -1553,7 +1572,6 @@ static int gridfast_impl(psn_lk_ctx *c, int slot, const int *rois, int nroi, con
     for (int base = 0; base < nroi; base += psn::kGfMaxRois) {
         const int n = std::min(psn::kGfMaxRois, nroi - base);
         a.nroi = n;
-        a.roi_base = base;
         a.out_xy = d_xy + (size_t)base * p.cap * 2;
         a.out_count = d_cnt + base;
         a.out_total = d_tot ? d_tot + base : nullptr;
@@ -1575,17 +1593,31 @@ static int gridfast_impl(psn_lk_ctx *c, int slot, const int *rois, int nroi, con
             int y1 = std::min((long long)r[1] + r[3], (long long)c->height) > y0 ? (int)std::min((long long)r[1] + r[3], (long long)c->height) : y0;
             if (r[2] <= 0 || r[3] <= 0) x1 = x0, y1 = y0;
             a.rois[i] = make_int4(x0, y0, x1 - x0, y1 - y0);
+            a.roi_img[i] = roi_img[base + i];
+            a.roi_key[i] = roi_key[base + i];
         }
         HIPCHK(c, psn::launch_gridfast(a, c->stream));
     }
-    return record_slot_free(c, slot);  // a later build into this slot waits for these reads
+    // a later build into these slots waits for these reads
+    return record_slots_free(c, used.data(), (int)used.size());
 }
 
 int psn_gridfast_detect_device(psn_lk_ctx *c, int slot, const int *rois, int nroi, const psn_gridfast_params *p,
                                uint32_t seed, float *d_out_xy, int *d_out_count, int *d_out_total) {
     if (!c || nroi < 0 || (nroi > 0 && (!rois || !d_out_xy || !d_out_count))) return PSN_LK_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    return gridfast_impl(c, slot, rois, nroi, p, seed, d_out_xy, d_out_count, d_out_total);
+    return gridfast_impl(c, 1, &slot, &nroi, rois, p, seed, d_out_xy, d_out_count, d_out_total);
+}
+
+int psn_gridfast_detect_device_sets(psn_lk_ctx *c, int nset, const int *slots, const int *nrois, const int *rois,
+                                    const psn_gridfast_params *p, uint32_t seed, float *d_out_xy, int *d_out_count,
+                                    int *d_out_total) {
+    if (!c || nset < 0 || (nset > 0 && (!slots || !nrois))) return PSN_LK_ERR_ARG;
+    long long total = 0;
+    for (int i = 0; i < nset; i++) total += std::max(nrois[i], 0);
+    if (total > INT32_MAX || (total > 0 && (!rois || !d_out_xy || !d_out_count))) return PSN_LK_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    return gridfast_impl(c, nset, slots, nrois, rois, p, seed, d_out_xy, d_out_count, d_out_total);
 }
 
 int psn_gridfast_detect(psn_lk_ctx *c, int slot, const int *rois, int nroi, const psn_gridfast_params *pp,
@@ -1597,7 +1629,7 @@ int psn_gridfast_detect(psn_lk_ctx *c, int slot, const int *rois, int nroi, cons
         p = *pp;
     else
         psn_gridfast_default_params(&p);
-    if (nroi == 0 || p.cap < 0) return gridfast_impl(c, slot, rois, nroi, &p, seed, nullptr, nullptr, nullptr);
+    if (nroi == 0 || p.cap < 0) return gridfast_impl(c, 1, &slot, &nroi, rois, &p, seed, nullptr, nullptr, nullptr);
     const size_t xy_need = (size_t)nroi * std::max(p.cap, 1) * 2;
     if (c->gf_out_cap < xy_need) {
         if (c->d_gf_xy) (void)hipFree(c->d_gf_xy);
@@ -1614,7 +1646,7 @@ int psn_gridfast_detect(psn_lk_ctx *c, int slot, const int *rois, int nroi, cons
         HIPCHK(c, hipMalloc(&c->d_gf_ot, (size_t)nroi * sizeof(int)));
         c->gf_nroi_cap = nroi;
     }
-    int rc = gridfast_impl(c, slot, rois, nroi, &p, seed, c->d_gf_xy, c->d_gf_oc, c->d_gf_ot);
+    int rc = gridfast_impl(c, 1, &slot, &nroi, rois, &p, seed, c->d_gf_xy, c->d_gf_oc, c->d_gf_ot);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(out_count, c->d_gf_oc, (size_t)nroi * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     if (out_total)

@@ -603,26 +603,30 @@ int Tracker2DFlow::PassLaunchChains(std::vector<PassCam> &pc, bool gridfast, uin
             psn_gridfast_params gp;
             psn_gridfast_default_params(&gp);
             gp.cap = (int)cap;  // kT2dMaxFeatures
-            std::vector<int> rois;
+            std::vector<int> rois(4 * K), slots, nrois;
             // the detector's cell scratch lives in the LK context: the previous
             // pass's detections (on the other chain stream) are done with it first
             if (gf_rec_) chk(hipStreamWaitEvent(st, (hipEvent_t)ev_gf_, 0), "gridfast scratch");
+            // every camera's detections in one detector launch (per camera in the
+            // reference: sets of rois at consecutive k, outputs at p.k0)
             for (PassCam &p : pc) {
                 const size_t n = p.dets->size();
                 if (!n) continue;
-                rois.assign(4 * n, 0);
+                slots.push_back(cams_[p.cam].ring[kT2dInterval - 1]);
+                nrois.push_back((int)n);
                 for (size_t i = 0; i < n; i++) {
                     // cv::Rect((int)x, (int)y, (int)w, (int)h) of the cropped, scaled box
                     const Rect r = (*p.dets)[i].box.scale(kFlowScale).cropWithSize(width_, height_);
-                    rois[4 * i] = (int)r.x;
-                    rois[4 * i + 1] = (int)r.y;
-                    rois[4 * i + 2] = (int)r.w;
-                    rois[4 * i + 3] = (int)r.h;
+                    const size_t k = p.k0 + i;
+                    rois[4 * k] = (int)r.x;
+                    rois[4 * k + 1] = (int)r.y;
+                    rois[4 * k + 2] = (int)r.w;
+                    rois[4 * k + 3] = (int)r.h;
                 }
-                rc = psn_gridfast_detect_device(lk_, cams_[p.cam].ring[kT2dInterval - 1], rois.data(), (int)n, &gp, seed,
-                                                db.d_in + 2 * cap * p.k0, db.d_cnt + p.k0, db.d_tot + p.k0);
-                if (rc) return fail(rc, "psn_gridfast_detect_device");
             }
+            rc = psn_gridfast_detect_device_sets(lk_, (int)slots.size(), slots.data(), nrois.data(), rois.data(), &gp,
+                                                 seed, db.d_in, db.d_cnt, db.d_tot);
+            if (rc) return fail(rc, "psn_gridfast_detect_device_sets");
             chk(hipEventRecord((hipEvent_t)ev_gf_, st), "gridfast event");
             gf_rec_ = !rc;
             if (!rc && ((rc = psn_t2d_download_device(b.h_rawcnt, db.d_cnt, K * 4, st)) ||

@@ -187,6 +187,39 @@ class LKContext:
                                                        ctypes.c_uint32(seed & 0xffffffff), d_xy, d_count, d_total),
                     "gridfast_detect_device")
 
+    def gridfast_detect_sets(self, slots, roi_sets, params: GridFastParams | None = None, seed: int = 0):
+        """psn_gridfast_detect_device_sets: set i = roi_sets[i] on ring slot
+        slots[i], all sets in as few launches as possible. Returns, per set,
+        (list of (n_j, 2) f32 point arrays, totals before the cap) -- what
+        gridfast_detect(slots[i], roi_sets[i]) returns."""
+        from . import hip
+
+        p = params or gridfast_params()
+        sets = [np.asarray(r, dtype=np.int32).reshape(-1, 4) for r in roi_sets]
+        nrois = np.array([r.shape[0] for r in sets], np.int32)
+        sl = np.ascontiguousarray(np.asarray(slots, np.int32))
+        if sl.shape[0] != len(sets):
+            raise ValueError("one slot per roi set")
+        r = np.ascontiguousarray(np.concatenate(sets + [np.zeros((0, 4), np.int32)]))
+        n, cap = r.shape[0], max(p.cap, 0)
+        d_xy = hip.DeviceBuffer(max(n, 1) * max(cap, 1) * 8)
+        d_cnt, d_tot = hip.DeviceBuffer(max(n, 1) * 4), hip.DeviceBuffer(max(n, 1) * 4)
+        try:
+            self._check(self._L.psn_gridfast_detect_device_sets(
+                self._h, len(sets), sl.ctypes.data, nrois.ctypes.data, r.ctypes.data, ctypes.byref(p),
+                ctypes.c_uint32(seed & 0xffffffff), d_xy.addr, d_cnt.addr, d_tot.addr), "gridfast_detect_sets")
+            xy = d_xy.to_array((max(n, 1), max(cap, 1), 2), np.float32)
+            cnt = d_cnt.to_array(max(n, 1), np.int32)
+            tot = d_tot.to_array(max(n, 1), np.int32)
+        finally:
+            for b in (d_xy, d_cnt, d_tot):
+                b.free()
+        out, k = [], 0
+        for m in nrois:
+            out.append(([xy[k + j, :cnt[k + j]].copy() for j in range(m)], tot[k:k + m].copy()))
+            k += m
+        return out
+
     def track_device_counted(self, queries: list[LkQuery], d_counts: int, d_prev: int, d_next: int, d_status: int,
                              d_err: int | None):
         """Queries sized num_pts (capacity); query i processes d_counts[i] points (device int32)."""

@@ -199,3 +199,30 @@ def test_gridfast_gpu_many_rois(oracle_mod):
         ctx.push_frame(0, f)
         g_pts, g_tot = ctx.gridfast_detect(0, rois, seed=42)
     _compare(g_pts, g_tot, r_pts, r_tot, rois)
+
+
+@pytest.mark.gpu
+def test_gridfast_gpu_sets_match_per_frame(oracle_mod):
+    """psn_gridfast_detect_device_sets (every camera's detections in one launch,
+    as the tracker runs them): per set, exactly the oracle on that set's frame
+    with the set-local shuffle keys. Sets of 30, 0, 45 and 3 rois: the 64-roi
+    launch boundary falls inside the third set."""
+    from mcmtt_opticalflow_amd import lk as glk
+
+    w, h = 1920, 1080
+    rng = np.random.default_rng(17)
+    frames = [synth.make_scene(c, w, h, 64).frame(0) for c in range(4)]
+    sizes = [30, 0, 45, 3]
+    sets = [[(int(x), int(y), int(bw), int(bh)) for x, y, bw, bh in
+             zip(rng.integers(-30, w - 40, n), rng.integers(-30, h - 60, n), rng.integers(8, 260, n),
+                 rng.integers(8, 400, n))] for n in sizes]
+    sets[3][0] = (0, 0, 0, 0)  # empty roi
+    with glk.LKContext(w, h, ring_slots=4, max_level_cap=0) as ctx:
+        for s, f in enumerate(frames):
+            ctx.push_frame(s, f)
+        got = ctx.gridfast_detect_sets([2, 0, 1, 3], [sets[0], sets[1], sets[2], sets[3]], seed=77)
+        one = ctx.gridfast_detect(1, sets[2], seed=77)
+    for (g_pts, g_tot), slot, rois in zip(got, [2, 0, 1, 3], sets):
+        r_pts, r_tot = oracle_mod.gridfast_detect(frames[slot], rois, seed=77) if rois else ([], np.zeros(0))
+        _compare(g_pts, g_tot, r_pts, r_tot, rois)
+    _compare(got[2][0], got[2][1], one[0], one[1], sets[2])
