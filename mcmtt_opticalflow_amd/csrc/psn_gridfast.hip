@@ -316,7 +316,13 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_cell_kernel(GridFastArgs 
 }
 
 // One workgroup per roi: the cells' keypoints concatenated in grid order,
-// ordered by the seeded hash key (bitonic sort in LDS), the first `cap` out.
+// ordered by the seeded hash key, the first `cap` out. Keys are unique
+// (hash << 32 | candidate index). Only the `cap` smallest are needed: a 256-bin
+// histogram of the hashes' top byte finds the bin b holding the cap-th key,
+// the keys of bins <= b (about cap + n / 256) are ranked against each other
+// (a key's position = the number of smaller keys in that set, which holds
+// every smaller key of all n), and a key of rank < cap is written at its rank.
+// A set larger than kGfRankMax (cap near n) takes a bitonic sort of all keys.
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352du;
@@ -326,10 +332,16 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     return x;
 }
 
+constexpr int kGfRankMax = 512;
+static_assert(kGfThreads == 256, "one histogram bin per thread");
+
 __global__ __launch_bounds__(kGfThreads) void gridfast_select_kernel(GridFastArgs A) {
     __shared__ unsigned long long key[kGfMaxTotal];
     __shared__ uint32_t cand[kGfMaxTotal];
+    __shared__ unsigned long long small[kGfRankMax];
     __shared__ int off[257];
+    __shared__ int hist[256];
+    __shared__ int nsmall, bsel;
     const int r = blockIdx.x, tid = threadIdx.x;
     const int ncell = A.grid_rows * A.grid_cols;
     const int *cnt = A.cell_cnt + (size_t)r * ncell;
@@ -340,18 +352,72 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_select_kernel(GridFastArg
             s += cnt[c];
         }
         off[ncell] = s;
+        nsmall = 0;
     }
+    hist[tid] = 0;  // kGfThreads == 256 bins
     __syncthreads();
     const int n = off[ncell];
-    int P = 1;
-    while (P < n) P <<= 1;
+    const int m = min(n, A.cap);
+    float *o = A.out_xy + (size_t)r * A.cap * 2;
+    if (tid == 0) {
+        A.out_count[r] = m;
+        if (A.out_total) A.out_total[r] = n;
+    }
+    if (m <= 0) return;
     const uint32_t h0 = mix32(A.seed + 0x9e3779b9u * (uint32_t)(A.roi_key[r] + 1));
     for (int c = 0; c < ncell; c++) {
         const uint32_t *src = A.cell_kp + ((size_t)r * ncell + c) * A.per_cell;
         for (int j = tid; j < off[c + 1] - off[c]; j += kGfThreads) cand[off[c] + j] = src[j];
     }
-    for (int k = tid; k < P; k += kGfThreads)
-        key[k] = k < n ? ((unsigned long long)mix32(h0 ^ (uint32_t)k) << 32) | (uint32_t)k : ~0ull;
+    for (int k = tid; k < n; k += kGfThreads) {
+        const uint32_t h = mix32(h0 ^ (uint32_t)k);
+        key[k] = ((unsigned long long)h << 32) | (uint32_t)k;
+        atomicAdd(&hist[h >> 24], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {  // bin of the m-th smallest key: wave-wide scan of 4 bins per lane
+        const int b4 = hist[4 * tid] + hist[4 * tid + 1] + hist[4 * tid + 2] + hist[4 * tid + 3];
+        int x = b4;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d, 64);
+            if (tid >= d) x += y;
+        }
+        const unsigned long long hit = __ballot(x >= m);  // x: bins [0, 4 tid + 4)
+        const int lane = __ffsll((long long)hit) - 1;
+        if (tid == lane) {
+            int cum = x - b4, b = 4 * tid;
+            while (cum + hist[b] < m) cum += hist[b++];
+            bsel = b;
+        }
+    }
+    __syncthreads();
+    const uint32_t bmax = (uint32_t)bsel;
+    for (int k = tid; k < n; k += kGfThreads) {
+        const unsigned long long q = key[k];
+        if ((uint32_t)(q >> 56) <= bmax) {
+            const int i = atomicAdd(&nsmall, 1);
+            if (i < kGfRankMax) small[i] = q;
+        }
+    }
+    __syncthreads();
+    const int ns = nsmall;
+    if (ns <= kGfRankMax) {
+        for (int i = tid; i < ns; i += kGfThreads) {
+            const unsigned long long q = small[i];
+            int rank = 0;
+            for (int j = 0; j < ns; j++) rank += small[j] < q;
+            if (rank < m) {
+                const uint32_t p = cand[(uint32_t)q];
+                o[2 * rank] = (float)(p & 0xffffu);
+                o[2 * rank + 1] = (float)(p >> 16);
+            }
+        }
+        return;
+    }
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int k = n + tid; k < P; k += kGfThreads) key[k] = ~0ull;
     __syncthreads();
     for (int size = 2; size <= P; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -368,16 +434,10 @@ __global__ __launch_bounds__(kGfThreads) void gridfast_select_kernel(GridFastArg
             __syncthreads();
         }
     }
-    const int m = min(n, A.cap);
-    float *o = A.out_xy + (size_t)r * A.cap * 2;
     for (int i = tid; i < m; i += kGfThreads) {
         const uint32_t p = cand[(uint32_t)key[i]];
         o[2 * i] = (float)(p & 0xffffu);
         o[2 * i + 1] = (float)(p >> 16);
-    }
-    if (tid == 0) {
-        A.out_count[r] = m;
-        if (A.out_total) A.out_total[r] = n;
     }
 }
 
