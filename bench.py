@@ -74,7 +74,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level paramete
 N_SIMD, CLOCK_HZ = 256 * 4, 2.4e9
 VALU_PEAK_WAVE_INSTR = N_SIMD * CLOCK_HZ / 2.0
 OPS_PER_SAMPLE = 8  # ~8 integer ops per window sample per iteration
-DEFAULT_PROFILE = os.path.join(ROOT, "profiles", "r06b_tracker_profile.json")
+DEFAULT_PROFILE = os.path.join(ROOT, "profiles", "r06c_tracker_profile.json")
 
 
 def progress(msg):

@@ -332,7 +332,10 @@ int psn_lk_runtime_info(char *buf, int len);
 /* Wall time (ms) the first psn_lk_create on `device` spent setting up the
  * device's SDMA engines (one 4-KB copy per engine each way, so a later frame
  * upload never lands on an engine whose queue ROCr has yet to create);
- * PSN_LK_ERR_ARG when no context was created on the device yet. */
+ * PSN_LK_ERR_ARG when no context was created on the device yet. The warm-up is
+ * skipped (about 0 ms) when the environment sets PSN_LK_SDMA_WARMUP=0, or when
+ * no HSA agent matches the HIP device (several agents on its PCI function and
+ * none with its UUID); psn_lk_create succeeds either way. */
 int psn_lk_sdma_warmup_ms(int device, double *ms);
 
 #ifdef __cplusplus

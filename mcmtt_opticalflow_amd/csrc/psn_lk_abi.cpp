@@ -256,6 +256,10 @@ hsa_status_t pick_agent(hsa_agent_t a, void *arg) {
     return HSA_STATUS_SUCCESS;
 }
 void warm_sdma_engines(int device) {
+    // PSN_LK_SDMA_WARMUP=0: skipped (no create-time cost; the first upload per
+    // engine then stalls once, as without the warm-up)
+    const char *env = getenv("PSN_LK_SDMA_WARMUP");
+    if (env && env[0] == '0') return;
     int bus = 0, dev = 0, dom = 0;
     if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
         hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||

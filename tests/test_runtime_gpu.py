@@ -125,3 +125,34 @@ def test_bench_exchange_flag_one_rank(oracle_mod):
     r = bench.tracker_run(args, steps=4, warmup=2)
     v = bench.verify_tracker(args, r)
     assert v["frames"] == 6 and v["mismatches"] == 0, v
+
+
+WARM = r"""
+import ctypes, json, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from mcmtt_opticalflow_amd import lk as glk, _lib, synth
+L = _lib.load()
+sc = synth.make_scene(0, 640, 480, 64)
+pts = sc.points_at(0).astype(np.float32)
+nxt, st, err = glk.calc_optical_flow_pyr_lk(sc.frame(0), sc.frame(1), pts, (21, 21), 3)
+ms = ctypes.c_double(-1.0)
+rc = L.psn_lk_sdma_warmup_ms(0, ctypes.byref(ms))
+print(json.dumps({{"rc": rc, "ms": ms.value, "tracked": int(st.sum()), "n": len(pts)}}))
+"""
+
+
+@pytest.mark.parametrize("warm", ["1", "0"])
+def test_sdma_warmup_recorded_and_optional(warm):
+    """The first psn_lk_create of a process sets up the SDMA engines and records
+    the wall time it took (bounded); PSN_LK_SDMA_WARMUP=0 skips it (the path a
+    device whose HSA agent cannot be matched takes) and the context still
+    creates and tracks."""
+    env = dict(os.environ, PSN_LK_SDMA_WARMUP=warm)
+    p = subprocess.run([sys.executable, "-u", "-c", WARM.format(root=ROOT)], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["rc"] == 0, out
+    assert 0.0 <= out["ms"] < (5000.0 if warm == "1" else 5.0), out
+    assert out["tracked"] > out["n"] // 2, out
